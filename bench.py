@@ -1,0 +1,269 @@
+#!/usr/bin/env python3
+"""Benchmark: device-resident RS(6,3) encode + worst-case decode, 1 MiB cells.
+
+One "step" = one pass of the hot path over one batch: Coder::encode of every
+stripe (6 data cells -> 3 parity cells) followed by Coder::decode of every
+stripe with data shards {0,1,2} missing (survivors 3,4,5,6,7,8 -> 3
+reconstructed cells).  Both are the same gfx950 kernel (6 inputs, 3
+outputs), launched through the C ABI on torch's current stream.
+
+value = data bytes coded per second over all ranks, GiB/s, counting k*cell
+per stripe for the encode and again for the decode -- the reference
+Criterion convention Throughput::Bytes(6 x slice) (rust/benches/ec.rs:30,42).
+
+Multi-GPU: stripes are independent, so every rank codes its own batch of
+`--stripes` stripes (weak scaling) with no data-path collective; the
+process group is used only for the barrier and the max-over-ranks time.
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "hdfs-native_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+METRIC = "GiB/s device-resident RS(6,3) encode+decode, 1 MiB cells, at 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+HBM_COPY_GBS = 6290.0  # measured float4 copy, same guide
+GIB = float(1 << 30)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--k", type=int, default=6)
+    ap.add_argument("--m", type=int, default=3)
+    ap.add_argument("--cell", type=int, default=1 << 20)
+    ap.add_argument("--stripes", type=int, default=1024, help="stripes per GPU")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="also time the oracle stripe-parallel on T threads")
+    ap.add_argument("--host-path", action="store_true", help="also measure the pinned H2D+encode+D2H pipeline")
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--tune", default="", help="key=value,... passed to hec_tune_set (measurement)")
+    ap.add_argument("--encode-only", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(k, m, cell, seconds, threads=1):
+    """Times the C restatement of the reference loop (oracle, matrix.rs:204-231
+    order) on the host: encode + decode({0..m-1} missing) of 1-stripe calls,
+    the same work as one Coder::encode + Coder::decode per stripe."""
+    import ctypes
+
+    import numpy as np
+
+    import ec_oracle
+    from hdfs_native_ec.synth import batch_data
+    lib = ec_oracle.load_c_oracle()
+    data = batch_data(1, k, cell)[0]
+    par = np.empty((m, cell), dtype=np.uint8)
+    rec = np.empty((k, cell), dtype=np.uint8)
+    ins = (ctypes.c_void_p * k)(*[data[i].ctypes.data for i in range(k)])
+    outs = (ctypes.c_void_p * m)(*[par[j].ctypes.data for j in range(m)])
+    shards = (ctypes.c_void_p * (k + m))(*([0] * m + [data[i].ctypes.data for i in range(m, k)] +
+                                            [par[j].ctypes.data for j in range(m)]))
+    recs = (ctypes.c_void_p * (k + m))(*([rec[i].ctypes.data for i in range(k)] + [0] * m))
+    counts = [0] * threads
+    stop = time.perf_counter() + seconds
+
+    def work(t):
+        while time.perf_counter() < stop:
+            lib.orc_encode(k, m, ins, cell, outs)
+            lib.orc_decode(k, m, shards, cell, recs)
+            counts[t] += 1
+
+    t0 = time.perf_counter()
+    ths = [threading.Thread(target=work, args=(t,)) for t in range(threads)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    el = time.perf_counter() - t0
+    assert np.array_equal(rec[:m], data[:m]), "cpu baseline decode mismatch"
+    n = sum(counts)
+    return {"value": round(2 * n * k * cell / GIB / el, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "sample": f"{n} x (encode + decode 0..{m - 1} missing) of one RS({k},{m}) stripe, {cell} B cells, "
+                      f"{el:.1f} s, C restatement oracle/ec_oracle.c (reference Rust path unbuildable here)"}
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import hdfs_native_ec as H
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    for kv in filter(None, args.tune.split(",")):
+        key, val = kv.split("=")
+        H.tune_set(int(key), int(val))
+
+    k, m, cell, S = args.k, args.m, args.cell, args.stripes
+    coder = H.Coder(k, m, local)
+    g = torch.Generator(device=dev)
+    g.manual_seed(0x5EED_EC00 + rank)
+    data = torch.randint(0, 256, (S, k, cell), dtype=torch.uint8, device=dev, generator=g)
+    parity = torch.empty((S, m, cell), dtype=torch.uint8, device=dev)
+    rec = torch.empty((S, m, cell), dtype=torch.uint8, device=dev)  # reconstructed data 0..m-1
+    stream = torch.cuda.current_stream(dev)
+    sp = stream.cuda_stream
+
+    dp, ds = H.stripe_layout_ptrs(data, k)
+    pp, ps = H.stripe_layout_ptrs(parity, m)
+    rp, rs = H.stripe_layout_ptrs(rec, m)
+    miss = list(range(m))  # worst case: m data shards missing
+    shard_ptrs = [None if i in miss else dp[i] for i in range(k)] + pp
+    out_ptrs = [rp[i] if i in miss else 0 for i in range(k)]
+    out_strides = [rs[0]] * k
+
+    def encode():
+        coder.encode_device(dp, ds, pp, ps, cell, S, sp)
+
+    def decode():
+        coder.decode_device(shard_ptrs, ds + ps, out_ptrs, out_strides, cell, S, sp)
+
+    def step(events=None):
+        if events is not None:
+            events[0].record(stream)
+        encode()
+        if events is not None:
+            events[1].record(stream)
+        if not args.encode_only:
+            decode()
+        if events is not None:
+            events[2].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+
+    # correctness gate (not timed): decode reconstructs the erased shards and
+    # one stripe matches the oracle bit for bit
+    if not args.encode_only:
+        assert torch.equal(rec, data[:, :m]), "decode != original"
+    import ec_oracle
+    clib = ec_oracle.load_c_oracle()
+    s0 = data[0].cpu().numpy()
+    want = ec_oracle.c_encode(clib, k, m, list(s0))
+    assert all(np.array_equal(parity[0, j].cpu().numpy(), want[j]) for j in range(m)), "parity != oracle"
+
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(evs[i])
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    enc_ms = [evs[i][0].elapsed_time(evs[i][1]) for i in range(args.steps)]
+    dec_ms = [evs[i][1].elapsed_time(evs[i][2]) for i in range(args.steps)] if not args.encode_only else []
+    launch_ms = enc_ms + dec_ms
+    avg_launch_ms = sum(launch_ms) / len(launch_ms)
+    ops = 1 if args.encode_only else 2
+    bytes_per_step = ops * k * cell * S * world
+    value = bytes_per_step * args.steps / elapsed / GIB
+    algo_bytes = (k + m) * cell * S  # per launch: k inputs read + m outputs written
+    achieved = algo_bytes / (avg_launch_ms * 1e-3) / 1e9
+
+    traffic = None
+    if os.path.exists(args.traffic):
+        with open(args.traffic) as f:
+            tr = json.load(f)
+        if tr.get("config") == {"k": k, "m": m, "cell": cell, "stripes": S}:
+            traffic = tr.get("hbm_bytes_per_launch")
+
+    result = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic: seeded uniform random bytes (torch.randint on device, seed 0x5EED_EC00+rank)",
+        "config": {
+            "workload": f"RS({k},{m}) {cell >> 10} KiB cells: encode + decode with data shards "
+                        f"{{{','.join(map(str, miss))}}} missing, {S} stripes per GPU"
+                        + (" (encode only)" if args.encode_only else ""),
+            "k": k, "m": m, "cell_bytes": cell, "stripes_per_gpu": S,
+            "parallelism": f"stripe-sharded x{world}, no collectives",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "kernel": f"gf_matmul_v16<{k},{m}> (encode and decode launches)",
+            "algorithmic_bytes_per_launch": algo_bytes,
+            "avg_launch_ms": round(avg_launch_ms, 4),
+            "frac_of_measured_copy": round(achieved / HBM_COPY_GBS, 4),
+        },
+        "encode_GiBps": round(k * cell * S / (sum(enc_ms) / len(enc_ms) * 1e-3) / GIB, 2),
+        "decode_GiBps": round(k * cell * S / (sum(dec_ms) / len(dec_ms) * 1e-3) / GIB, 2) if dec_ms else None,
+        "parity_check": "ok",
+    }
+
+    if args.host_path and rank == 0:
+        hs = min(S, 256)
+        h_in = data[:hs].cpu().pin_memory()
+        h_out = torch.empty((hs, m, cell), dtype=torch.uint8).pin_memory()
+        coder.encode_host_batch(h_in.data_ptr(), h_out.data_ptr(), cell, hs, 16)
+        reps = 3
+        th0 = time.perf_counter()
+        for _ in range(reps):
+            coder.encode_host_batch(h_in.data_ptr(), h_out.data_ptr(), cell, hs, 16)
+        th = (time.perf_counter() - th0) / reps
+        assert torch.equal(h_out, parity[:hs].cpu())
+        result["host_path"] = {"encode_GiBps_pcie_inclusive": round(k * cell * hs / th / GIB, 2),
+                               "stripes": hs, "chunk_stripes": 16,
+                               "note": "pinned host -> H2D -> encode -> D2H -> pinned host, 2-slot overlap"}
+
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        result["cpu_baseline"] = cpu_baseline(k, m, cell, args.cpu_seconds, 1)
+        if args.cpu_threads > 1:
+            result["cpu_baseline_parallel"] = cpu_baseline(k, m, cell, args.cpu_seconds, args.cpu_threads)
+    elif rank == 0:
+        result["cpu_baseline"] = None
+
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    coder.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

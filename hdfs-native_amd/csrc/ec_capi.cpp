@@ -1,0 +1,465 @@
+// ec_capi.cpp -- implementation of the C ABI in include/hdfs_ec_amd.h.
+//
+// Host-side logic of hdfs-native's Coder (rust/src/ec/gf256.rs:25-138) on top
+// of the HIP kernels in ec_kernels.hip:
+//   * coding matrix (gen_rs_matrix, gf256.rs:40-57) built once per coder;
+//   * decode plans (first-k-present survivors, inverse, missing-data rows;
+//     gf256.rs:84-126) computed once per erasure mask and cached -- the
+//     reference rebuilds Coder and re-inverts per decoded row (ec/mod.rs:71);
+//   * host-buffer calls stage through coder-owned device buffers;
+//   * device calls only enqueue kernels on the caller's stream.
+// Nothing here throws or aborts across the ABI: every entry point catches.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/hdfs_ec_amd.h"
+#include "ec_kernels.hpp"
+#include "gf256.hpp"
+
+namespace {
+
+struct DecodePlan {
+    int status = HEC_OK;
+    std::vector<size_t> survivors;  // k
+    std::vector<size_t> missing;    // e
+    std::vector<uint8_t> matrix;    // e x k
+};
+
+// Restores the caller's current HIP device on scope exit.
+struct DeviceGuard {
+    int prev = -1;
+    bool ok = false;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        ok = hipSetDevice(dev) == hipSuccess;
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+}  // namespace
+
+struct hec_coder {
+    size_t k = 0, m = 0;
+    int device = 0;
+    std::vector<uint8_t> enc;  // (k+m) x k
+
+    std::mutex plan_mu;
+    std::unordered_map<uint64_t, DecodePlan> plans;  // key: presence bitmask (k+m <= 48)
+
+    std::mutex host_mu;  // serialises the host-buffer API (staging buffers)
+    hipStream_t stream = nullptr;
+    hipStream_t copy_stream[2] = {nullptr, nullptr};
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    uint8_t* dbuf = nullptr;
+    size_t dbuf_bytes = 0;
+};
+
+namespace {
+
+int to_status(int kernel_rc) {
+    if (kernel_rc == 0) return HEC_OK;
+    if (kernel_rc == -1) return HEC_ERR_INVALID_ARG;
+    return HEC_ERR_DEVICE;
+}
+
+DecodePlan compute_plan(size_t k, size_t m, const uint8_t* present) {
+    DecodePlan p;
+    std::vector<size_t> valid;
+    for (size_t i = 0; i < k + m; i++) {
+        if (present[i])
+            valid.push_back(i);
+        else if (i < k)
+            p.missing.push_back(i);  // gf256.rs:96-97: only data indices
+    }
+    if (p.missing.empty()) return p;  // gf256.rs:102-105
+    if (valid.size() < k) {           // gf256.rs:107-111
+        p.status = HEC_ERR_NOT_ENOUGH_SHARDS;
+        return p;
+    }
+    p.survivors.assign(valid.begin(), valid.begin() + k);  // first k present, ascending
+    const std::vector<uint8_t> enc = hec::gen_rs_matrix(k, m);
+    std::vector<uint8_t> sub(k * k);
+    for (size_t r = 0; r < k; r++) std::memcpy(&sub[r * k], &enc[p.survivors[r] * k], k);  // select_rows
+    if (!hec::invert(sub.data(), k)) {
+        p.status = HEC_ERR_SINGULAR;
+        return p;
+    }
+    p.matrix.resize(p.missing.size() * k);
+    for (size_t r = 0; r < p.missing.size(); r++)  // select_rows(invalid), ascending
+        std::memcpy(&p.matrix[r * k], &sub[p.missing[r] * k], k);
+    return p;
+}
+
+const DecodePlan& cached_plan(hec_coder* c, const uint8_t* present) {
+    uint64_t key = 0;
+    for (size_t i = 0; i < c->k + c->m; i++)
+        if (present[i]) key |= uint64_t(1) << i;
+    std::lock_guard<std::mutex> lk(c->plan_mu);
+    auto it = c->plans.find(key);
+    if (it != c->plans.end()) return it->second;
+    return c->plans.emplace(key, compute_plan(c->k, c->m, present)).first->second;
+}
+
+// Runs out[j] = sum_i mat[j*cols+i] * in[i] over a batch, <= 4 rows per launch.
+int matmul_batch(int device, const uint8_t* mat, size_t rows, size_t cols, const uint8_t* const* in,
+                 const size_t* in_strides, uint8_t* const* out, const size_t* out_strides, size_t cell_len,
+                 size_t stripes, hipStream_t stream) {
+    if (rows == 0 || cols == 0 || cols > size_t(hec::kMaxK) || cell_len == 0 || !mat || !in || !out ||
+        !in_strides || !out_strides)
+        return HEC_ERR_INVALID_ARG;
+    if (stripes == 0) return HEC_OK;
+    for (size_t i = 0; i < cols; i++)
+        if (!in[i]) return HEC_ERR_INVALID_ARG;
+    for (size_t j = 0; j < rows; j++)
+        if (!out[j]) return HEC_ERR_INVALID_ARG;
+    for (size_t r0 = 0; r0 < rows; r0 += hec::kMaxR) {
+        hec::MatmulArgs a;
+        std::memset(&a, 0, sizeof(a));
+        const size_t nr = std::min(rows - r0, size_t(hec::kMaxR));
+        for (size_t i = 0; i < cols; i++) {
+            a.in[i] = in[i];
+            a.in_stride[i] = in_strides[i];
+        }
+        for (size_t j = 0; j < nr; j++) {
+            a.out[j] = out[r0 + j];
+            a.out_stride[j] = out_strides[r0 + j];
+            for (size_t i = 0; i < cols; i++) a.coef[j * hec::kMaxK + i] = mat[(r0 + j) * cols + i];
+        }
+        a.k = int32_t(cols);
+        a.r = int32_t(nr);
+        a.cell_len = cell_len;
+        a.stripes = stripes;
+        const int rc = hec::launch_gf_matmul(a, device, stream);
+        if (rc != 0) return to_status(rc);
+    }
+    return HEC_OK;
+}
+
+int ensure_dbuf(hec_coder* c, size_t bytes) {
+    if (c->dbuf_bytes >= bytes) return HEC_OK;
+    if (c->dbuf) (void)hipFree(c->dbuf);
+    c->dbuf = nullptr;
+    c->dbuf_bytes = 0;
+    if (hipMalloc(&c->dbuf, bytes) != hipSuccess) {
+        (void)hipGetLastError();
+        return HEC_ERR_NO_MEMORY;
+    }
+    c->dbuf_bytes = bytes;
+    return HEC_OK;
+}
+
+template <typename F>
+int guarded(F&& f) {
+    try {
+        return f();
+    } catch (const std::bad_alloc&) {
+        return HEC_ERR_NO_MEMORY;
+    } catch (...) {
+        return HEC_ERR_DEVICE;
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* hec_strerror(int status) {
+    switch (status) {
+        case HEC_OK: return "ok";
+        case HEC_ERR_INVALID_ARG: return "invalid argument";
+        case HEC_ERR_NOT_ENOUGH_SHARDS: return "erasure coding error: Not enough valid shards";
+        case HEC_ERR_UNSUPPORTED_CODEC: return "unsupported erasure coding policy";
+        case HEC_ERR_DEVICE: return "HIP device error";
+        case HEC_ERR_NO_MEMORY: return "out of memory";
+        case HEC_ERR_SINGULAR: return "Matrix is singular";
+        default: return "unknown status";
+    }
+}
+
+int hec_abi_version(void) { return HEC_ABI_VERSION; }
+
+int hec_gen_rs_matrix(size_t data_units, size_t parity_units, uint8_t* out) {
+    if (!out || data_units == 0 || data_units + parity_units > 256) return HEC_ERR_INVALID_ARG;
+    return guarded([&] {
+        const std::vector<uint8_t> m = hec::gen_rs_matrix(data_units, parity_units);
+        std::memcpy(out, m.data(), m.size());
+        return HEC_OK;
+    });
+}
+
+int hec_matrix_invert(uint8_t* mat, size_t n) {
+    if (!mat || n == 0) return HEC_ERR_INVALID_ARG;
+    return guarded([&] { return hec::invert(mat, n) ? HEC_OK : HEC_ERR_SINGULAR; });
+}
+
+int hec_decode_plan(size_t data_units, size_t parity_units, const uint8_t* present, size_t* n_missing,
+                    size_t* survivors, size_t* missing, uint8_t* matrix) {
+    if (!present || !n_missing || data_units == 0 || parity_units == 0 || data_units + parity_units > 256)
+        return HEC_ERR_INVALID_ARG;
+    return guarded([&] {
+        DecodePlan p = compute_plan(data_units, parity_units, present);
+        *n_missing = p.missing.size();
+        if (p.status != HEC_OK) return p.status;
+        if (survivors) std::copy(p.survivors.begin(), p.survivors.end(), survivors);
+        if (missing) std::copy(p.missing.begin(), p.missing.end(), missing);
+        if (matrix) std::copy(p.matrix.begin(), p.matrix.end(), matrix);
+        return HEC_OK;
+    });
+}
+
+int hec_coder_create(size_t data_units, size_t parity_units, int device, hec_coder_t** out) {
+    if (!out) return HEC_ERR_INVALID_ARG;
+    *out = nullptr;
+    if (data_units == 0 || data_units > HEC_MAX_DATA_UNITS || parity_units == 0 ||
+        parity_units > HEC_MAX_PARITY_UNITS)
+        return HEC_ERR_INVALID_ARG;
+    return guarded([&] {
+        int ndev = 0;
+        if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) {
+            (void)hipGetLastError();
+            return HEC_ERR_DEVICE;
+        }
+        auto* c = new hec_coder();
+        c->k = data_units;
+        c->m = parity_units;
+        c->device = device;
+        c->enc = hec::gen_rs_matrix(data_units, parity_units);
+        DeviceGuard g(device);
+        bool ok = g.ok;
+        ok = ok && hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess;
+        for (int i = 0; i < 2 && ok; i++)
+            ok = hipStreamCreateWithFlags(&c->copy_stream[i], hipStreamNonBlocking) == hipSuccess;
+        for (int i = 0; i < 4 && ok; i++)
+            ok = hipEventCreateWithFlags(&c->ev[i], hipEventDisableTiming) == hipSuccess;
+        if (!ok) {
+            (void)hipGetLastError();
+            hec_coder_destroy(c);
+            return HEC_ERR_DEVICE;
+        }
+        *out = c;
+        return HEC_OK;
+    });
+}
+
+void hec_coder_destroy(hec_coder_t* c) {
+    if (!c) return;
+    try {
+        DeviceGuard g(c->device);
+        if (c->stream) (void)hipStreamSynchronize(c->stream);
+        for (auto s : c->copy_stream)
+            if (s) (void)hipStreamSynchronize(s);
+        if (c->dbuf) (void)hipFree(c->dbuf);
+        for (auto e : c->ev)
+            if (e) (void)hipEventDestroy(e);
+        for (auto s : c->copy_stream)
+            if (s) (void)hipStreamDestroy(s);
+        if (c->stream) (void)hipStreamDestroy(c->stream);
+    } catch (...) {
+    }
+    delete c;
+}
+
+size_t hec_coder_data_units(const hec_coder_t* c) { return c ? c->k : 0; }
+size_t hec_coder_parity_units(const hec_coder_t* c) { return c ? c->m : 0; }
+int hec_coder_device(const hec_coder_t* c) { return c ? c->device : -1; }
+
+int hec_gf_matmul_device(hec_coder_t* c, const uint8_t* matrix, size_t rows, size_t cols,
+                         const uint8_t* const* d_in, const size_t* in_strides, uint8_t* const* d_out,
+                         const size_t* out_strides, size_t cell_len, size_t stripes, void* hip_stream) {
+    if (!c) return HEC_ERR_INVALID_ARG;
+    return guarded([&] {
+        DeviceGuard g(c->device);
+        if (!g.ok) return HEC_ERR_DEVICE;
+        return matmul_batch(c->device, matrix, rows, cols, d_in, in_strides, d_out, out_strides, cell_len, stripes,
+                            static_cast<hipStream_t>(hip_stream));
+    });
+}
+
+int hec_encode_device(hec_coder_t* c, const uint8_t* const* d_data, const size_t* data_strides,
+                      uint8_t* const* d_parity, const size_t* parity_strides, size_t cell_len, size_t stripes,
+                      void* hip_stream) {
+    if (!c) return HEC_ERR_INVALID_ARG;
+    return hec_gf_matmul_device(c, c->enc.data() + c->k * c->k, c->m, c->k, d_data, data_strides, d_parity,
+                                parity_strides, cell_len, stripes, hip_stream);
+}
+
+int hec_decode_device(hec_coder_t* c, const uint8_t* const* d_shards, const size_t* shard_strides,
+                      uint8_t* const* d_out, const size_t* out_strides, size_t cell_len, size_t stripes,
+                      void* hip_stream) {
+    if (!c || !d_shards || !shard_strides || cell_len == 0) return HEC_ERR_INVALID_ARG;
+    return guarded([&] {
+        uint8_t present[HEC_MAX_DATA_UNITS + HEC_MAX_PARITY_UNITS];
+        for (size_t i = 0; i < c->k + c->m; i++) present[i] = d_shards[i] != nullptr;
+        const DecodePlan& p = cached_plan(c, present);
+        if (p.status != HEC_OK) return p.status;
+        if (p.missing.empty()) return HEC_OK;
+        if (!d_out || !out_strides) return HEC_ERR_INVALID_ARG;
+        const uint8_t* in[HEC_MAX_DATA_UNITS];
+        size_t ist[HEC_MAX_DATA_UNITS];
+        uint8_t* out[HEC_MAX_DATA_UNITS];
+        size_t ost[HEC_MAX_DATA_UNITS];
+        for (size_t r = 0; r < c->k; r++) {
+            in[r] = d_shards[p.survivors[r]];
+            ist[r] = shard_strides[p.survivors[r]];
+        }
+        for (size_t r = 0; r < p.missing.size(); r++) {
+            out[r] = d_out[p.missing[r]];
+            ost[r] = out_strides[p.missing[r]];
+        }
+        DeviceGuard g(c->device);
+        if (!g.ok) return HEC_ERR_DEVICE;
+        return matmul_batch(c->device, p.matrix.data(), p.missing.size(), c->k, in, ist, out, ost, cell_len, stripes,
+                            static_cast<hipStream_t>(hip_stream));
+    });
+}
+
+int hec_encode(hec_coder_t* c, const uint8_t* const* data, size_t shard_len, uint8_t* const* parity) {
+    if (!c || !data || !parity || shard_len == 0) return HEC_ERR_INVALID_ARG;
+    for (size_t i = 0; i < c->k; i++)
+        if (!data[i]) return HEC_ERR_INVALID_ARG;
+    for (size_t j = 0; j < c->m; j++)
+        if (!parity[j]) return HEC_ERR_INVALID_ARG;
+    return guarded([&] {
+        std::lock_guard<std::mutex> lk(c->host_mu);
+        DeviceGuard g(c->device);
+        if (!g.ok) return HEC_ERR_DEVICE;
+        const size_t pitch = (shard_len + 255) & ~size_t(255);
+        int rc = ensure_dbuf(c, pitch * (c->k + c->m));
+        if (rc != HEC_OK) return rc;
+        const uint8_t* din[HEC_MAX_DATA_UNITS];
+        uint8_t* dout[HEC_MAX_PARITY_UNITS];
+        size_t strides[HEC_MAX_DATA_UNITS + HEC_MAX_PARITY_UNITS];
+        for (size_t i = 0; i < c->k + c->m; i++) strides[i] = pitch;
+        for (size_t i = 0; i < c->k; i++) {
+            din[i] = c->dbuf + i * pitch;
+            if (hipMemcpyAsync(c->dbuf + i * pitch, data[i], shard_len, hipMemcpyHostToDevice, c->stream) !=
+                hipSuccess)
+                return HEC_ERR_DEVICE;
+        }
+        for (size_t j = 0; j < c->m; j++) dout[j] = c->dbuf + (c->k + j) * pitch;
+        rc = matmul_batch(c->device, c->enc.data() + c->k * c->k, c->m, c->k, din, strides, dout, strides, shard_len,
+                          1, c->stream);
+        if (rc != HEC_OK) return rc;
+        for (size_t j = 0; j < c->m; j++)
+            if (hipMemcpyAsync(parity[j], dout[j], shard_len, hipMemcpyDeviceToHost, c->stream) != hipSuccess)
+                return HEC_ERR_DEVICE;
+        return hipStreamSynchronize(c->stream) == hipSuccess ? HEC_OK : HEC_ERR_DEVICE;
+    });
+}
+
+int hec_decode(hec_coder_t* c, const uint8_t* const* shards, size_t shard_len, uint8_t* const* out) {
+    if (!c || !shards || shard_len == 0) return HEC_ERR_INVALID_ARG;
+    return guarded([&] {
+        uint8_t present[HEC_MAX_DATA_UNITS + HEC_MAX_PARITY_UNITS];
+        for (size_t i = 0; i < c->k + c->m; i++) present[i] = shards[i] != nullptr;
+        const DecodePlan& p = cached_plan(c, present);
+        if (p.status != HEC_OK) return p.status;
+        if (p.missing.empty()) return HEC_OK;
+        if (!out) return HEC_ERR_INVALID_ARG;
+        for (size_t i : p.missing)
+            if (!out[i]) return HEC_ERR_INVALID_ARG;
+        std::lock_guard<std::mutex> lk(c->host_mu);
+        DeviceGuard g(c->device);
+        if (!g.ok) return HEC_ERR_DEVICE;
+        const size_t e = p.missing.size();
+        const size_t pitch = (shard_len + 255) & ~size_t(255);
+        int rc = ensure_dbuf(c, pitch * (c->k + e));
+        if (rc != HEC_OK) return rc;
+        const uint8_t* din[HEC_MAX_DATA_UNITS];
+        uint8_t* dout[HEC_MAX_DATA_UNITS];
+        size_t strides[2 * HEC_MAX_DATA_UNITS];
+        for (size_t i = 0; i < c->k + e; i++) strides[i] = pitch;
+        for (size_t r = 0; r < c->k; r++) {
+            din[r] = c->dbuf + r * pitch;
+            if (hipMemcpyAsync(c->dbuf + r * pitch, shards[p.survivors[r]], shard_len, hipMemcpyHostToDevice,
+                               c->stream) != hipSuccess)
+                return HEC_ERR_DEVICE;
+        }
+        for (size_t r = 0; r < e; r++) dout[r] = c->dbuf + (c->k + r) * pitch;
+        rc = matmul_batch(c->device, p.matrix.data(), e, c->k, din, strides, dout, strides, shard_len, 1, c->stream);
+        if (rc != HEC_OK) return rc;
+        for (size_t r = 0; r < e; r++)
+            if (hipMemcpyAsync(out[p.missing[r]], dout[r], shard_len, hipMemcpyDeviceToHost, c->stream) != hipSuccess)
+                return HEC_ERR_DEVICE;
+        return hipStreamSynchronize(c->stream) == hipSuccess ? HEC_OK : HEC_ERR_DEVICE;
+    });
+}
+
+// Pipelined pinned-host batch: chunk q uses device slot q%2; H2D on
+// copy_stream[slot], encode on stream, D2H on copy_stream[slot] after the
+// encode's event; slot reuse waits on the previous D2H through stream order.
+int hec_encode_host_batch(hec_coder_t* c, const uint8_t* h_data, uint8_t* h_parity, size_t cell_len,
+                          size_t stripes, size_t chunk_stripes) {
+    if (!c || !h_data || !h_parity || cell_len == 0 || chunk_stripes == 0) return HEC_ERR_INVALID_ARG;
+    if (stripes == 0) return HEC_OK;
+    return guarded([&] {
+        std::lock_guard<std::mutex> lk(c->host_mu);
+        DeviceGuard g(c->device);
+        if (!g.ok) return HEC_ERR_DEVICE;
+        const size_t k = c->k, m = c->m;
+        chunk_stripes = std::min(chunk_stripes, stripes);
+        const size_t in_bytes = chunk_stripes * k * cell_len;
+        const size_t out_bytes = chunk_stripes * m * cell_len;
+        const size_t slot_bytes = in_bytes + out_bytes;
+        int rc = ensure_dbuf(c, 2 * slot_bytes);
+        if (rc != HEC_OK) return rc;
+        const size_t nchunks = (stripes + chunk_stripes - 1) / chunk_stripes;
+        for (size_t q = 0; q < nchunks; q++) {
+            const int slot = int(q & 1);
+            hipStream_t cs = c->copy_stream[slot];
+            uint8_t* din = c->dbuf + slot * slot_bytes;
+            uint8_t* dpar = din + in_bytes;
+            const size_t s0 = q * chunk_stripes;
+            const size_t ns = std::min(chunk_stripes, stripes - s0);
+            if (hipMemcpyAsync(din, h_data + s0 * k * cell_len, ns * k * cell_len, hipMemcpyHostToDevice, cs) !=
+                hipSuccess)
+                return HEC_ERR_DEVICE;
+            if (hipEventRecord(c->ev[slot], cs) != hipSuccess) return HEC_ERR_DEVICE;
+            if (hipStreamWaitEvent(c->stream, c->ev[slot], 0) != hipSuccess) return HEC_ERR_DEVICE;
+            const uint8_t* in[HEC_MAX_DATA_UNITS];
+            uint8_t* out[HEC_MAX_PARITY_UNITS];
+            size_t ist[HEC_MAX_DATA_UNITS], ost[HEC_MAX_PARITY_UNITS];
+            for (size_t i = 0; i < k; i++) {
+                in[i] = din + i * cell_len;
+                ist[i] = k * cell_len;
+            }
+            for (size_t j = 0; j < m; j++) {
+                out[j] = dpar + j * cell_len;
+                ost[j] = m * cell_len;
+            }
+            rc = matmul_batch(c->device, c->enc.data() + k * k, m, k, in, ist, out, ost, cell_len, ns, c->stream);
+            if (rc != HEC_OK) return rc;
+            if (hipEventRecord(c->ev[2 + slot], c->stream) != hipSuccess) return HEC_ERR_DEVICE;
+            if (hipStreamWaitEvent(cs, c->ev[2 + slot], 0) != hipSuccess) return HEC_ERR_DEVICE;
+            if (hipMemcpyAsync(h_parity + s0 * m * cell_len, dpar, ns * m * cell_len, hipMemcpyDeviceToHost, cs) !=
+                hipSuccess)
+                return HEC_ERR_DEVICE;
+        }
+        bool ok = hipStreamSynchronize(c->copy_stream[0]) == hipSuccess;
+        ok = hipStreamSynchronize(c->copy_stream[1]) == hipSuccess && ok;
+        ok = hipStreamSynchronize(c->stream) == hipSuccess && ok;
+        return ok ? HEC_OK : HEC_ERR_DEVICE;
+    });
+}
+
+// Tuning knobs for the measurement harness (not part of the reference API):
+// key 1 = column chunks per lane (1|2), 2 = non-temporal loads/stores (0|1),
+// 3 = blocks per CU (0 = occupancy-derived).
+int hec_tune_set(int key, int value) {
+    switch (key) {
+        case 1: hec::g_tune_unroll = value == 2 ? 2 : 1; return HEC_OK;
+        case 2: hec::g_tune_nt = value ? 1 : 0; return HEC_OK;
+        case 3: hec::g_tune_blocks_per_cu = value < 0 ? 0 : value; return HEC_OK;
+        default: return HEC_ERR_INVALID_ARG;
+    }
+}
+
+}  // extern "C"

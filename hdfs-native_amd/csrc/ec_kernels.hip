@@ -1,0 +1,353 @@
+// ec_kernels.hip -- hand-written gfx950 kernels for the GF(2^8) coding-matrix
+// multiply over stripe cells: the MI355X replacement for the reference's hot
+// loop, Mul<&[&[u8]]> for Matrix<GF256> (rust/src/ec/matrix.rs:204-231),
+// driven by Coder::encode (gf256.rs:61-80) and Coder::decode (gf256.rs:84-137).
+//
+//   out[j][b] = XOR_i  M[j][i] * in[i][b]       (GF(2^8), modulus 0x11D)
+//
+// Design (see DESIGN.md "Kernels"):
+//  * HBM-bound byte work, no MFMA.  Each lane owns one 16-byte column chunk
+//    of every shard of a stripe (global_load_dwordx4 / 1 KiB per wave per
+//    shard, fully coalesced), computes all R outputs from registers, writes
+//    R x 16 B with dwordx4 stores.  Every input byte is read from HBM once
+//    and every output byte written once: the algorithmic minimum (k+r)*cell.
+//  * Per block, the coding-matrix rows and the log/antilog tables are staged
+//    in LDS; from them the block builds, per coefficient c, three v_perm_b32
+//    product tables: c*x = T0[x&7] ^ T1[(x>>3)&7] ^ T2[x>>6] (the 3-3-2 split
+//    of the byte lets a 2-dword, 8-entry byte pool answer each lookup with
+//    one v_perm_b32 on four bytes at once).  Per input dword: 5 selector ops;
+//    per (input dword, coefficient): 3 v_perm_b32 + 2 XOR (v_bitop3).
+//  * Grid = resident blocks only, grid-stride over (stripe, column-tile)
+//    tiles so the table prologue is paid once per block.
+//  * Tails (cell_len % 16) and unaligned layouts use a byte-granular kernel
+//    with LDS log/antilog lookups -- same results, correctness path.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "ec_kernels.hpp"
+#include "gf256.hpp"
+
+namespace hec {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__constant__ GfTables kDevGf = GfTables();
+
+// One coefficient's product tables, 8 dwords (32 B) per entry so that a
+// ds_read_b128 + ds_read_b32 pair fetches it (broadcast: all lanes read the
+// same address, so no bank conflicts).
+struct PermTable {
+    uint32_t t0lo, t0hi, t1lo, t1hi, t2, pad0, pad1, pad2;
+};
+
+__device__ __forceinline__ uint8_t lds_gf_mul(const uint8_t* s_exp, const uint8_t* s_log, uint8_t a,
+                                              uint8_t b) {
+    return (a == 0 || b == 0) ? 0 : s_exp[s_log[a] + s_log[b]];
+}
+
+__device__ __forceinline__ uint32_t pack4(uint8_t a, uint8_t b, uint8_t c, uint8_t d) {
+    return uint32_t(a) | (uint32_t(b) << 8) | (uint32_t(c) << 16) | (uint32_t(d) << 24);
+}
+
+// Builds the v_perm_b32 product tables for coefficient c using the LDS
+// log/antilog tables.
+__device__ void build_perm_table(PermTable* t, uint8_t c, const uint8_t* s_exp, const uint8_t* s_log) {
+    uint8_t p0[8], p1[8], p2[4];
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+        p0[e] = lds_gf_mul(s_exp, s_log, c, uint8_t(e));
+        p1[e] = lds_gf_mul(s_exp, s_log, c, uint8_t(e << 3));
+    }
+#pragma unroll
+    for (int e = 0; e < 4; e++) p2[e] = lds_gf_mul(s_exp, s_log, c, uint8_t(e << 6));
+    t->t0lo = pack4(p0[0], p0[1], p0[2], p0[3]);
+    t->t0hi = pack4(p0[4], p0[5], p0[6], p0[7]);
+    t->t1lo = pack4(p1[0], p1[1], p1[2], p1[3]);
+    t->t1hi = pack4(p1[4], p1[5], p1[6], p1[7]);
+    t->t2 = pack4(p2[0], p2[1], p2[2], p2[3]);
+    t->pad0 = t->pad1 = t->pad2 = 0;
+}
+
+// c * x for the four bytes of x.  v_perm_b32(S0=hi, S1=lo, sel): selector
+// byte 0..3 picks a byte of lo, 4..7 a byte of hi.
+__device__ __forceinline__ uint32_t gf_mul4(uint32_t t0lo, uint32_t t0hi, uint32_t t1lo, uint32_t t1hi,
+                                            uint32_t t2, uint32_t s0, uint32_t s1, uint32_t s2) {
+    uint32_t a = __builtin_amdgcn_perm(t0hi, t0lo, s0);
+    uint32_t b = __builtin_amdgcn_perm(t1hi, t1lo, s1);
+    uint32_t c = __builtin_amdgcn_perm(t2, t2, s2);
+    return a ^ b ^ c;
+}
+
+struct Sel {
+    uint32_t s0, s1, s2;
+};
+
+__device__ __forceinline__ Sel make_sel(uint32_t x) {
+    Sel s;
+    s.s0 = x & 0x07070707u;
+    s.s1 = (x >> 3) & 0x07070707u;
+    s.s2 = (x >> 6) & 0x03030303u;
+    return s;
+}
+
+template <bool NT>
+__device__ __forceinline__ u32x4 load16(const uint8_t* p) {
+    if constexpr (NT)
+        return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    else
+        return *reinterpret_cast<const u32x4*>(p);
+}
+
+template <bool NT>
+__device__ __forceinline__ void store16(uint8_t* p, u32x4 v) {
+    if constexpr (NT)
+        __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
+    else
+        *reinterpret_cast<u32x4*>(p) = v;
+}
+
+// Stage log/antilog + coefficient rows in LDS, build the perm tables.
+template <int R>
+__device__ __forceinline__ void prologue(const MatmulArgs& a, int k, PermTable (*s_tab)[kMaxK], uint8_t* s_exp,
+                                         uint8_t* s_log, uint8_t* s_coef) {
+    static_assert(kBlock == 256, "prologue assumes 256 threads");
+    const int tid = threadIdx.x;
+    s_exp[tid] = kDevGf.exp[tid];
+    s_exp[tid + 256] = kDevGf.exp[tid + 256];
+    s_log[tid] = kDevGf.log[tid];
+    if (tid < R * kMaxK) s_coef[tid] = a.coef[tid];
+    __syncthreads();
+    for (int t = tid; t < R * k; t += kBlock) {
+        int j = t / k, i = t - j * k;
+        build_perm_table(&s_tab[j][i], s_coef[j * kMaxK + i], s_exp, s_log);
+    }
+    __syncthreads();
+}
+
+// ---------------------------------------------------------------------------
+// Vector kernel: 16 B per lane per shard, U column chunks per lane.
+// K = compile-time input count (0 = runtime a.k), R = outputs (1..4).
+// ---------------------------------------------------------------------------
+template <int K, int R, int U, bool NT>
+__global__ __launch_bounds__(kBlock) void gf_matmul_v16(MatmulArgs a) {
+    __shared__ PermTable s_tab[R][kMaxK];
+    __shared__ uint8_t s_exp[512];
+    __shared__ uint8_t s_log[256];
+    __shared__ uint8_t s_coef[R * kMaxK];
+    const int k = K ? K : a.k;
+    prologue<R>(a, k, s_tab, s_exp, s_log, s_coef);
+
+    const uint32_t chunks = a.chunks;  // 16-B chunks per cell
+    const uint32_t tps = a.tiles_per_stripe;
+    const uint32_t total = a.total_tiles;
+    constexpr uint32_t TILE = kBlock * U;
+
+    for (uint32_t tile = blockIdx.x; tile < total; tile += gridDim.x) {
+        const uint32_t stripe = tile / tps;
+        const uint32_t tcol = tile - stripe * tps;
+        // Keep the per-coefficient table reads inside the loop (LDS broadcast
+        // reads) instead of letting LICM pin R*K*5 VGPRs for the whole kernel.
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint32_t col = tcol * TILE + u * kBlock + threadIdx.x;
+            if (col >= chunks) continue;
+            const uint64_t off = uint64_t(col) * 16u;
+            u32x4 acc[R];
+#pragma unroll
+            for (int j = 0; j < R; j++) acc[j] = u32x4{0, 0, 0, 0};
+            if constexpr (K > 0) {
+                u32x4 x[K];
+#pragma unroll
+                for (int i = 0; i < K; i++) x[i] = load16<NT>(a.in[i] + uint64_t(stripe) * a.in_stride[i] + off);
+                // Issue every shard's load before any arithmetic: K x 1 KiB in
+                // flight per wave instead of the scheduler's 2.
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int i = 0; i < K; i++) {
+                    Sel s[4];
+#pragma unroll
+                    for (int d = 0; d < 4; d++) s[d] = make_sel(x[i][d]);
+#pragma unroll
+                    for (int j = 0; j < R; j++) {
+                        const PermTable& t = s_tab[j][i];
+                        const uint32_t t0lo = t.t0lo, t0hi = t.t0hi, t1lo = t.t1lo, t1hi = t.t1hi, t2 = t.t2;
+#pragma unroll
+                        for (int d = 0; d < 4; d++)
+                            acc[j][d] ^= gf_mul4(t0lo, t0hi, t1lo, t1hi, t2, s[d].s0, s[d].s1, s[d].s2);
+                    }
+                }
+            } else {
+                for (int i = 0; i < k; i++) {
+                    u32x4 x = load16<NT>(a.in[i] + uint64_t(stripe) * a.in_stride[i] + off);
+                    Sel s[4];
+#pragma unroll
+                    for (int d = 0; d < 4; d++) s[d] = make_sel(x[d]);
+#pragma unroll
+                    for (int j = 0; j < R; j++) {
+                        const PermTable& t = s_tab[j][i];
+                        const uint32_t t0lo = t.t0lo, t0hi = t.t0hi, t1lo = t.t1lo, t1hi = t.t1hi, t2 = t.t2;
+#pragma unroll
+                        for (int d = 0; d < 4; d++)
+                            acc[j][d] ^= gf_mul4(t0lo, t0hi, t1lo, t1hi, t2, s[d].s0, s[d].s1, s[d].s2);
+                    }
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < R; j++) store16<NT>(a.out[j] + uint64_t(stripe) * a.out_stride[j] + off, acc[j]);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Byte kernel: tails and unaligned layouts.  One thread per (stripe, byte) in
+// [a.byte_begin, a.cell_len); LDS log/antilog lookups.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void gf_matmul_bytes(MatmulArgs a) {
+    __shared__ uint8_t s_exp[512];
+    __shared__ uint8_t s_log[256];
+    __shared__ uint8_t s_lc[kMaxR * kMaxK];  // log of each coefficient
+    __shared__ uint8_t s_nz[kMaxR * kMaxK];
+    const int tid = threadIdx.x;
+    s_exp[tid] = kDevGf.exp[tid];
+    s_exp[tid + 256] = kDevGf.exp[tid + 256];
+    s_log[tid] = kDevGf.log[tid];
+    if (tid < kMaxR * kMaxK) {
+        const int t = tid;
+        uint8_t c = a.coef[t];
+        s_lc[t] = kDevGf.log[c];
+        s_nz[t] = c != 0;
+    }
+    __syncthreads();
+    const uint64_t width = a.cell_len - a.byte_begin;
+    const uint64_t total = width * a.stripes;
+    for (uint64_t g = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; g < total;
+         g += uint64_t(gridDim.x) * blockDim.x) {
+        const uint64_t stripe = g / width;
+        const uint64_t b = a.byte_begin + (g - stripe * width);
+        uint32_t acc[kMaxR] = {0, 0, 0, 0};
+        for (int i = 0; i < a.k; i++) {
+            const uint8_t x = a.in[i][stripe * a.in_stride[i] + b];
+            if (!x) continue;
+            const uint32_t lx = s_log[x];
+            for (int j = 0; j < a.r; j++)
+                if (s_nz[j * kMaxK + i]) acc[j] ^= s_exp[lx + s_lc[j * kMaxK + i]];
+        }
+        for (int j = 0; j < a.r; j++) a.out[j][stripe * a.out_stride[j] + b] = uint8_t(acc[j]);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Host-side dispatch
+// ---------------------------------------------------------------------------
+namespace {
+
+struct KernelInfo {
+    const void* fn = nullptr;
+    int blocks_per_cu = 0;
+};
+
+template <int K, int R, int U, bool NT>
+const void* vec_fn() {
+    return reinterpret_cast<const void*>(&gf_matmul_v16<K, R, U, NT>);
+}
+
+template <int R, int U, bool NT>
+const void* pick_k(int k) {
+    switch (k) {
+        case 2: return vec_fn<2, R, U, NT>();
+        case 3: return vec_fn<3, R, U, NT>();
+        case 6: return vec_fn<6, R, U, NT>();
+        case 10: return vec_fn<10, R, U, NT>();
+        default: return vec_fn<0, R, U, NT>();
+    }
+}
+
+template <int U, bool NT>
+const void* pick_r(int k, int r) {
+    switch (r) {
+        case 1: return pick_k<1, U, NT>(k);
+        case 2: return pick_k<2, U, NT>(k);
+        case 3: return pick_k<3, U, NT>(k);
+        default: return pick_k<4, U, NT>(k);
+    }
+}
+
+const void* pick_vec(int k, int r, int unroll, bool nt) {
+    if (unroll == 2) return nt ? pick_r<2, true>(k, r) : pick_r<2, false>(k, r);
+    return nt ? pick_r<1, true>(k, r) : pick_r<1, false>(k, r);
+}
+
+int g_num_cus[64] = {0};
+
+int num_cus(int dev) {
+    if (dev < 0 || dev >= 64) return 256;
+    if (!g_num_cus[dev]) {
+        int v = 0;
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+        g_num_cus[dev] = v;
+    }
+    return g_num_cus[dev];
+}
+
+int occupancy(const void* fn) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, kBlock, 0) != hipSuccess || nb <= 0) nb = 4;
+    return nb;
+}
+
+}  // namespace
+
+int g_tune_unroll = 1;
+int g_tune_nt = 0;
+int g_tune_blocks_per_cu = 0;  // 0 = occupancy-derived
+
+int launch_gf_matmul(const MatmulArgs& in, int device, hipStream_t stream) {
+    MatmulArgs a = in;
+    bool aligned = true;
+    for (int i = 0; i < a.k; i++)
+        aligned &= ((reinterpret_cast<uintptr_t>(a.in[i]) | a.in_stride[i]) & 15u) == 0;
+    for (int j = 0; j < a.r; j++)
+        aligned &= ((reinterpret_cast<uintptr_t>(a.out[j]) | a.out_stride[j]) & 15u) == 0;
+    const uint64_t chunks = aligned ? a.cell_len / 16 : 0;
+    const int cus = num_cus(device);
+
+    if (chunks > 0) {
+        const int unroll = g_tune_unroll == 2 ? 2 : 1;
+        const uint64_t tile = uint64_t(kBlock) * unroll;
+        const uint64_t tps = (chunks + tile - 1) / tile;
+        const uint64_t total = tps * a.stripes;
+        if (chunks > 0xFFFFFFFFull || total > 0xFFFFFFFFull) return -1;
+        a.chunks = uint32_t(chunks);
+        a.tiles_per_stripe = uint32_t(tps);
+        a.total_tiles = uint32_t(total);
+        const void* fn = pick_vec(a.k, a.r, unroll, g_tune_nt != 0);
+        static thread_local const void* last_fn = nullptr;
+        static thread_local int last_occ = 0;
+        if (fn != last_fn) {
+            last_occ = occupancy(fn);
+            last_fn = fn;
+        }
+        const int bpc = g_tune_blocks_per_cu > 0 ? g_tune_blocks_per_cu : last_occ;
+        uint64_t grid = uint64_t(cus) * bpc;
+        if (grid > total) grid = total;
+        void* args[] = {&a};
+        if (hipLaunchKernel(fn, dim3(uint32_t(grid)), dim3(kBlock), args, 0, stream) != hipSuccess) return -4;
+    }
+    const uint64_t begin = chunks * 16;
+    if (begin < a.cell_len) {
+        a.byte_begin = begin;
+        const uint64_t total = (a.cell_len - begin) * a.stripes;
+        uint64_t grid = (total + kBlock - 1) / kBlock;
+        const uint64_t cap = uint64_t(cus) * 8;
+        if (grid > cap) grid = cap;
+        void* args[] = {&a};
+        if (hipLaunchKernel(reinterpret_cast<const void*>(&gf_matmul_bytes), dim3(uint32_t(grid)), dim3(kBlock),
+                            args, 0, stream) != hipSuccess)
+            return -4;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -4;
+}
+
+}  // namespace hec

@@ -1,0 +1,41 @@
+// ec_kernels.hpp -- kernel argument block and launcher for the GF(2^8)
+// stripe-cell matrix multiply (see ec_kernels.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace hec {
+
+constexpr int kBlock = 256;  // threads per block (4 waves)
+constexpr int kMaxK = 32;    // inputs per launch (HEC_MAX_DATA_UNITS)
+constexpr int kMaxR = 4;     // outputs per launch (more rows are split)
+
+// Passed by value as the kernel argument (kernarg segment, ~800 B).
+struct MatmulArgs {
+    const uint8_t* in[kMaxK];
+    uint64_t in_stride[kMaxK];  // bytes between stripes for input i
+    uint8_t* out[kMaxR];
+    uint64_t out_stride[kMaxR];
+    uint8_t coef[kMaxR * kMaxK];  // row j, column i at [j*kMaxK + i]
+    int32_t k;                    // inputs used
+    int32_t r;                    // outputs used (1..kMaxR)
+    uint64_t cell_len;            // bytes per cell
+    uint64_t stripes;
+    uint64_t byte_begin;          // byte kernel: first byte handled
+    uint32_t chunks;              // vec kernel: 16-B chunks per cell
+    uint32_t tiles_per_stripe;
+    uint32_t total_tiles;
+};
+
+// Launches the multiply for one group of <= kMaxR output rows.  0 on
+// success, -1 invalid sizes, -4 HIP failure.
+int launch_gf_matmul(const MatmulArgs& a, int device, hipStream_t stream);
+
+// Tuning knobs (set through hec_tune_set).
+extern int g_tune_unroll;
+extern int g_tune_nt;
+extern int g_tune_blocks_per_cu;
+
+}  // namespace hec

@@ -1,0 +1,281 @@
+"""ctypes binding of the MI355X EC engine's C ABI (include/hdfs_ec_amd.h).
+
+Mirrors the reference's Rust surface so parity tests read like the
+reference's own tests:
+
+  hdfs_native::ec::gf256::Coder::new(data_units, parity_units)   gf256.rs:32-38
+  Coder::gen_rs_matrix(k, m)                                     gf256.rs:40-57
+  Coder::encode(&[Bytes]) -> Vec<Bytes>                          gf256.rs:61-80
+  Coder::decode(&mut [Option<Bytes>]) -> Result<()>              gf256.rs:84-137
+
+plus the batched device-resident entry points used by bench.py.  There is no
+CPU fallback anywhere: if lib/libhdfs_ec_amd.so is missing or fails to load,
+import raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import List, Optional, Sequence
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libhdfs_ec_amd.so")
+
+HEC_OK = 0
+HEC_ERR_INVALID_ARG = -1
+HEC_ERR_NOT_ENOUGH_SHARDS = -2
+HEC_ERR_UNSUPPORTED_CODEC = -3
+HEC_ERR_DEVICE = -4
+HEC_ERR_NO_MEMORY = -5
+HEC_ERR_SINGULAR = -6
+
+# Every symbol include/hdfs_ec_amd.h declares (checked by tests/test_capi.py).
+EXPORTS = [
+    "hec_strerror", "hec_abi_version", "hec_gen_rs_matrix", "hec_matrix_invert",
+    "hec_decode_plan", "hec_coder_create", "hec_coder_destroy", "hec_coder_data_units",
+    "hec_coder_parity_units", "hec_coder_device", "hec_encode", "hec_decode",
+    "hec_encode_device", "hec_decode_device", "hec_gf_matmul_device",
+    "hec_encode_host_batch", "hec_tune_set",
+]
+
+
+class HdfsError(Exception):
+    """Base of the errors the reference reports (rust/src/error.rs)."""
+
+
+class ErasureCodingError(HdfsError):
+    """HdfsError::ErasureCodingError (error.rs:34-35)."""
+
+
+class UnsupportedErasureCodingPolicy(HdfsError):
+    """HdfsError::UnsupportedErasureCodingPolicy (error.rs:32-33)."""
+
+
+class DeviceError(HdfsError):
+    pass
+
+
+def _load() -> ctypes.CDLL:
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} not built: run `make -C hdfs-native_amd` (or __graft_entry__.build()). "
+            "There is no CPU fallback.")
+    lib = ctypes.CDLL(LIB_PATH)
+    P, S, I = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+    PP = ctypes.POINTER(ctypes.c_void_p)
+    SP = ctypes.POINTER(ctypes.c_size_t)
+    sig = {
+        "hec_strerror": ([I], ctypes.c_char_p),
+        "hec_abi_version": ([], I),
+        "hec_gen_rs_matrix": ([S, S, P], I),
+        "hec_matrix_invert": ([P, S], I),
+        "hec_decode_plan": ([S, S, P, SP, SP, SP, P], I),
+        "hec_coder_create": ([S, S, I, ctypes.POINTER(P)], I),
+        "hec_coder_destroy": ([P], None),
+        "hec_coder_data_units": ([P], S),
+        "hec_coder_parity_units": ([P], S),
+        "hec_coder_device": ([P], I),
+        "hec_encode": ([P, PP, S, PP], I),
+        "hec_decode": ([P, PP, S, PP], I),
+        "hec_encode_device": ([P, PP, SP, PP, SP, S, S, P], I),
+        "hec_decode_device": ([P, PP, SP, PP, SP, S, S, P], I),
+        "hec_gf_matmul_device": ([P, P, S, S, PP, SP, PP, SP, S, S, P], I),
+        "hec_encode_host_batch": ([P, P, P, S, S, S], I),
+        "hec_tune_set": ([I, I], I),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    return lib
+
+
+lib = _load()
+
+
+def strerror(rc: int) -> str:
+    return lib.hec_strerror(rc).decode()
+
+
+def _check(rc: int) -> None:
+    if rc == HEC_OK:
+        return
+    msg = strerror(rc)
+    if rc == HEC_ERR_NOT_ENOUGH_SHARDS:
+        raise ErasureCodingError("Not enough valid shards")
+    if rc == HEC_ERR_UNSUPPORTED_CODEC:
+        raise UnsupportedErasureCodingPolicy(msg)
+    if rc in (HEC_ERR_INVALID_ARG, HEC_ERR_SINGULAR):
+        raise ValueError(msg)
+    if rc == HEC_ERR_NO_MEMORY:
+        raise MemoryError(msg)
+    raise DeviceError(f"{msg} (status {rc})")
+
+
+def _pp(addrs: Sequence[int]):
+    return (ctypes.c_void_p * len(addrs))(*addrs)
+
+
+def _sp(vals: Sequence[int]):
+    return (ctypes.c_size_t * len(vals))(*vals)
+
+
+def gen_rs_matrix(data_units: int, parity_units: int) -> List[List[int]]:
+    buf = (ctypes.c_uint8 * ((data_units + parity_units) * data_units))()
+    _check(lib.hec_gen_rs_matrix(data_units, parity_units, buf))
+    k = data_units
+    return [list(buf[r * k:(r + 1) * k]) for r in range(data_units + parity_units)]
+
+
+def matrix_invert(mat: List[List[int]]) -> List[List[int]]:
+    n = len(mat)
+    buf = (ctypes.c_uint8 * (n * n))(*[v for row in mat for v in row])
+    _check(lib.hec_matrix_invert(buf, n))
+    return [list(buf[r * n:(r + 1) * n]) for r in range(n)]
+
+
+def decode_plan(data_units: int, parity_units: int, present: Sequence[bool]):
+    k, m = data_units, parity_units
+    pres = (ctypes.c_uint8 * (k + m))(*[1 if p else 0 for p in present])
+    e = ctypes.c_size_t(0)
+    surv = (ctypes.c_size_t * k)()
+    miss = (ctypes.c_size_t * k)()
+    mat = (ctypes.c_uint8 * (k * k))()
+    _check(lib.hec_decode_plan(k, m, pres, ctypes.byref(e), surv, miss, mat))
+    e = e.value
+    return list(surv) if e else [], list(miss[:e]), [list(mat[r * k:(r + 1) * k]) for r in range(e)]
+
+
+def tune_set(key: int, value: int) -> None:
+    _check(lib.hec_tune_set(key, value))
+
+
+def _addr(buf) -> int:
+    """Address of a writable/readable contiguous host buffer (numpy array,
+    bytearray, ctypes array, or bytes via a copy-free view when possible)."""
+    import numpy as np
+    if isinstance(buf, np.ndarray):
+        assert buf.flags["C_CONTIGUOUS"]
+        return buf.ctypes.data
+    arr = np.frombuffer(buf, dtype=np.uint8)
+    return arr.ctypes.data
+
+
+class Coder:
+    """Drop-in for hdfs_native::ec::gf256::Coder on one MI355X."""
+
+    def __init__(self, data_units: int, parity_units: int, device: int = 0):
+        h = ctypes.c_void_p()
+        _check(lib.hec_coder_create(data_units, parity_units, device, ctypes.byref(h)))
+        self._h = h
+        self.data_units = data_units
+        self.parity_units = parity_units
+        self.device = device
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            lib.hec_coder_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    gen_rs_matrix = staticmethod(gen_rs_matrix)
+
+    # -- host-buffer API: Coder::encode / Coder::decode --------------------
+    def encode(self, data: Sequence[bytes]) -> List[bytes]:
+        """gf256.rs:61-80: returns m parity shards as bytes."""
+        import numpy as np
+        assert len(data) == self.data_units, "data.len() == data_units (gf256.rs:62)"
+        n = len(data[0])
+        assert all(len(d) == n for d in data), "equal shard lengths (gf256.rs:65)"
+        ins = [np.ascontiguousarray(np.frombuffer(bytes(d) if not isinstance(d, np.ndarray) else d,
+                                                  dtype=np.uint8)) for d in data]
+        outs = [np.empty(n, dtype=np.uint8) for _ in range(self.parity_units)]
+        _check(lib.hec_encode(self._h, _pp([a.ctypes.data for a in ins]), n,
+                              _pp([a.ctypes.data for a in outs])))
+        return [o.tobytes() for o in outs]
+
+    def decode(self, data: List[Optional[bytes]]) -> None:
+        """gf256.rs:84-137: fills missing data slots of `data` in place."""
+        import numpy as np
+        k, m = self.data_units, self.parity_units
+        assert len(data) == k + m
+        present = [d for d in data if d is not None]
+        if not present:
+            _check(HEC_ERR_NOT_ENOUGH_SHARDS if any(d is None for d in data[:k]) else HEC_OK)
+            return
+        n = len(present[0])
+        ins = [None if d is None else np.ascontiguousarray(np.frombuffer(bytes(d), dtype=np.uint8))
+               for d in data]
+        outs = [np.empty(n, dtype=np.uint8) if (i < k and data[i] is None) else None for i in range(k + m)]
+        _check(lib.hec_decode(self._h, _pp([0 if a is None else a.ctypes.data for a in ins]), n,
+                              _pp([0 if a is None else a.ctypes.data for a in outs])))
+        for i in range(k):
+            if data[i] is None:
+                data[i] = outs[i].tobytes()
+
+    # -- device-resident batched API ----------------------------------------
+    def encode_device(self, data_ptrs, data_strides, parity_ptrs, parity_strides, cell_len, stripes,
+                      stream: int = 0) -> None:
+        _check(lib.hec_encode_device(self._h, _pp(data_ptrs), _sp(data_strides), _pp(parity_ptrs),
+                                     _sp(parity_strides), cell_len, stripes, ctypes.c_void_p(stream)))
+
+    def decode_device(self, shard_ptrs, shard_strides, out_ptrs, out_strides, cell_len, stripes,
+                      stream: int = 0) -> None:
+        _check(lib.hec_decode_device(self._h, _pp([p or 0 for p in shard_ptrs]), _sp(shard_strides),
+                                     _pp([p or 0 for p in out_ptrs]), _sp(out_strides), cell_len, stripes,
+                                     ctypes.c_void_p(stream)))
+
+    def gf_matmul_device(self, matrix: List[List[int]], in_ptrs, in_strides, out_ptrs, out_strides, cell_len,
+                         stripes, stream: int = 0) -> None:
+        rows, cols = len(matrix), len(matrix[0])
+        mat = (ctypes.c_uint8 * (rows * cols))(*[v for r in matrix for v in r])
+        _check(lib.hec_gf_matmul_device(self._h, mat, rows, cols, _pp(in_ptrs), _sp(in_strides), _pp(out_ptrs),
+                                        _sp(out_strides), cell_len, stripes, ctypes.c_void_p(stream)))
+
+    def encode_host_batch(self, h_data_addr: int, h_parity_addr: int, cell_len: int, stripes: int,
+                          chunk_stripes: int) -> None:
+        _check(lib.hec_encode_host_batch(self._h, ctypes.c_void_p(h_data_addr), ctypes.c_void_p(h_parity_addr),
+                                         cell_len, stripes, chunk_stripes))
+
+
+# ---- torch helpers (device memory comes from torch; plumbing only) --------
+
+def stripe_layout_ptrs(t, units: int):
+    """For a uint8 tensor [stripes, units, cell] return (ptrs, strides)."""
+    assert t.dim() == 3 and t.shape[1] == units and t.is_contiguous()
+    cell = t.shape[2]
+    base = t.data_ptr()
+    return [base + i * cell for i in range(units)], [units * cell] * units
+
+
+def encode_batch(coder: Coder, data, parity, stream=None) -> None:
+    """data: uint8 cuda tensor [S, k, cell]; parity: [S, m, cell]."""
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream(data.device)
+    dp, ds = stripe_layout_ptrs(data, coder.data_units)
+    pp, ps = stripe_layout_ptrs(parity, coder.parity_units)
+    coder.encode_device(dp, ds, pp, ps, data.shape[2], data.shape[0], s.cuda_stream)
+
+
+def decode_batch(coder: Coder, data, parity, missing: Sequence[int], out, stream=None) -> None:
+    """Reconstruct data shards `missing` of every stripe (one erasure pattern
+    for the batch) from data [S,k,cell] / parity [S,m,cell] into out
+    [S,k,cell] (only the missing slots are written)."""
+    import torch
+    k, m = coder.data_units, coder.parity_units
+    s = stream if stream is not None else torch.cuda.current_stream(data.device)
+    dp, ds = stripe_layout_ptrs(data, k)
+    pp, ps = stripe_layout_ptrs(parity, m)
+    op, os_ = stripe_layout_ptrs(out, k)
+    miss = set(missing)
+    ptrs = [None if i in miss else dp[i] for i in range(k)] + pp
+    coder.decode_device(ptrs, ds + ps, op, os_, data.shape[2], data.shape[0], s.cuda_stream)

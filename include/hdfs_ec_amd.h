@@ -1,0 +1,158 @@
+/*
+ * hdfs_ec_amd.h -- C ABI of the MI355X-native Reed-Solomon erasure-coding
+ * engine that drops in behind hdfs-native's internal EC functions.
+ *
+ * Reference interface replaced (hdfs-native 0.14.1, Rust; public under the
+ * `benchmark` feature, rust/src/lib.rs:49-52):
+ *   hdfs_native::ec::gf256::Coder::new            rust/src/ec/gf256.rs:32-38
+ *   hdfs_native::ec::gf256::Coder::gen_rs_matrix  rust/src/ec/gf256.rs:40-57
+ *   hdfs_native::ec::gf256::Coder::encode         rust/src/ec/gf256.rs:61-80
+ *   hdfs_native::ec::gf256::Coder::decode         rust/src/ec/gf256.rs:84-137
+ *   Matrix::select_rows / Matrix::invert          rust/src/ec/matrix.rs:74-84, :101-162
+ *   Mul<&[&[u8]]> for Matrix (the hot loop)       rust/src/ec/matrix.rs:204-231
+ * Callers in the reference: CellBuffer::encode (rust/src/hdfs/block_writer.rs:838),
+ * EcSchema::ec_decode (rust/src/ec/mod.rs:71-72), rust/benches/ec.rs.
+ *
+ * Conventions
+ *  - Plain pointers and sizes only.  Every function returns an int status
+ *    (HEC_OK == 0) and never aborts or throws across the ABI.
+ *  - GF(2^8) modulo 0x11D, Hadoop Cauchy coding matrix: results are
+ *    bit-identical to the reference Coder on the same inputs.
+ *  - A coder is bound to one HIP device.  The host-buffer calls
+ *    (hec_encode/hec_decode) are synchronous and serialised per coder by an
+ *    internal lock (one coder may be shared by threads; use one coder per
+ *    thread for concurrency).  The device calls are asynchronous: they only
+ *    enqueue work on the caller's HIP stream (`hip_stream` is a hipStream_t
+ *    passed as void*; NULL = the null stream) and are lock-free.
+ */
+#ifndef HDFS_EC_AMD_H
+#define HDFS_EC_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HEC_ABI_VERSION 1
+
+/* Status codes */
+#define HEC_OK 0
+#define HEC_ERR_INVALID_ARG (-1)       /* reference: assert!/panic (gf256.rs:62-65, matrix.rs:57) */
+#define HEC_ERR_NOT_ENOUGH_SHARDS (-2) /* HdfsError::ErasureCodingError("Not enough valid shards") gf256.rs:107-111 */
+#define HEC_ERR_UNSUPPORTED_CODEC (-3) /* HdfsError::UnsupportedErasureCodingPolicy mod.rs:74-78 */
+#define HEC_ERR_DEVICE (-4)            /* HIP runtime / launch failure */
+#define HEC_ERR_NO_MEMORY (-5)         /* host or device allocation failed */
+#define HEC_ERR_SINGULAR (-6)          /* reference panics "Matrix is singular" matrix.rs:121-123 */
+
+/* Limits of this engine (the reference has k+m <= 256 through `r as u8`). */
+#define HEC_MAX_DATA_UNITS 32
+#define HEC_MAX_PARITY_UNITS 16
+
+typedef struct hec_coder hec_coder_t;
+
+/* Human-readable text for a status code (static storage). */
+const char *hec_strerror(int status);
+int hec_abi_version(void);
+
+/* ---- Field / matrix helpers (host only, no device needed) ------------- */
+
+/* Coder::gen_rs_matrix (gf256.rs:40-57): writes the (k+m) x k coding matrix,
+ * row-major, into out[(k+m)*k]. */
+int hec_gen_rs_matrix(size_t data_units, size_t parity_units, uint8_t *out);
+
+/* Matrix::invert (matrix.rs:101-162): in-place inverse of an n x n
+ * row-major matrix over GF(2^8).  HEC_ERR_SINGULAR where the reference panics. */
+int hec_matrix_invert(uint8_t *mat, size_t n);
+
+/* The decode plan of Coder::decode (gf256.rs:84-126) for a presence mask.
+ * present[k+m]: non-zero = shard available.  On HEC_OK:
+ *   *n_missing   = e, the number of missing DATA shards (0 => nothing to do);
+ *   survivors[k] = the first k present shard indices, ascending;
+ *   missing[e]   = the missing data indices, ascending;
+ *   matrix[e*k]  = rows of inverse(select_rows(encode_matrix, survivors))
+ *                  for the missing indices (row-major).
+ * Returns HEC_ERR_NOT_ENOUGH_SHARDS when e > 0 and fewer than k are present. */
+int hec_decode_plan(size_t data_units, size_t parity_units, const uint8_t *present,
+                    size_t *n_missing, size_t *survivors, size_t *missing, uint8_t *matrix);
+
+/* ---- Coder lifecycle (Coder::new, gf256.rs:32-38) --------------------- */
+
+/* Creates a coder for RS(data_units, parity_units) on HIP device `device`.
+ * 1 <= data_units <= HEC_MAX_DATA_UNITS, 1 <= parity_units <= HEC_MAX_PARITY_UNITS. */
+int hec_coder_create(size_t data_units, size_t parity_units, int device, hec_coder_t **out);
+void hec_coder_destroy(hec_coder_t *coder);
+size_t hec_coder_data_units(const hec_coder_t *coder);
+size_t hec_coder_parity_units(const hec_coder_t *coder);
+int hec_coder_device(const hec_coder_t *coder);
+
+/* ---- Host-buffer drop-ins (synchronous) -------------------------------- */
+
+/* Coder::encode (gf256.rs:61-80).  data[k] host buffers of shard_len bytes
+ * each; parity[m] caller-allocated host buffers of shard_len bytes, fully
+ * overwritten.  shard_len == 0 -> HEC_ERR_INVALID_ARG (the reference panics,
+ * matrix.rs:57).  Any shard_len >= 1 is accepted, including tails that are not
+ * a multiple of 16. */
+int hec_encode(hec_coder_t *coder, const uint8_t *const *data, size_t shard_len,
+               uint8_t *const *parity);
+
+/* Coder::decode (gf256.rs:84-137).  shards[k+m] host buffers of shard_len
+ * bytes, NULL = missing.  For every missing DATA index i (< k) out[i] must
+ * point to shard_len writable bytes and receives the reconstructed shard;
+ * out[] entries for present shards and for parity indices are never touched
+ * (missing parity is not regenerated, gf256.rs:96-97).  Survivors are the
+ * first k present shards in index order.  Returns HEC_OK without writing when
+ * no data shard is missing, HEC_ERR_NOT_ENOUGH_SHARDS when fewer than k
+ * shards are present. */
+int hec_decode(hec_coder_t *coder, const uint8_t *const *shards, size_t shard_len,
+               uint8_t *const *out);
+
+/* ---- Device-resident batched API (asynchronous, on hip_stream) --------- *
+ * A batch is `stripes` independent stripes of cell_len-byte cells.  Shard i
+ * of stripe s lives at  base[i] + s * stride[i]  (device pointers).  For the
+ * [stripe][shard][cell] layout pass base[i] = buf + i*cell_len and
+ * stride[i] = units*cell_len.  The fast path needs every base and stride
+ * 16-byte aligned; other layouts run a byte-granular kernel (same results). */
+
+/* Batched Coder::encode: parity[j] = sum_i C[k+j][i] * data[i]. */
+int hec_encode_device(hec_coder_t *coder, const uint8_t *const *d_data, const size_t *data_strides,
+                      uint8_t *const *d_parity, const size_t *parity_strides, size_t cell_len,
+                      size_t stripes, void *hip_stream);
+
+/* Batched Coder::decode with one erasure pattern for the whole batch.
+ * d_shards[k+m] (NULL = missing) with shard_strides[k+m]; d_out[k] with
+ * out_strides[k], used only for missing data indices.  The decode matrix is
+ * computed on the host once per pattern and cached in the coder. */
+int hec_decode_device(hec_coder_t *coder, const uint8_t *const *d_shards, const size_t *shard_strides,
+                      uint8_t *const *d_out, const size_t *out_strides, size_t cell_len,
+                      size_t stripes, void *hip_stream);
+
+/* The raw hot loop, Mul<&[&[u8]]> (matrix.rs:204-231), batched:
+ * out[j] = sum_i matrix[j*cols + i] * in[i] for j < rows, i < cols.
+ * Any rows >= 1 (launched 4 output rows at a time), 1 <= cols <=
+ * HEC_MAX_DATA_UNITS.  Runs on the coder's device. */
+int hec_gf_matmul_device(hec_coder_t *coder, const uint8_t *matrix, size_t rows, size_t cols,
+                         const uint8_t *const *d_in, const size_t *in_strides, uint8_t *const *d_out,
+                         const size_t *out_strides, size_t cell_len, size_t stripes, void *hip_stream);
+
+/* ---- Pinned-host pipelined batch (PCIe-inclusive path) ----------------- *
+ * Encodes a [stripe][k][cell] host batch into a [stripe][m][cell] host batch,
+ * streaming chunks of `chunk_stripes` stripes H2D -> encode -> D2H with
+ * copy/compute overlap on the coder's own streams.  Host buffers should be
+ * pinned (hipHostMalloc / registered) for full PCIe rate.  Synchronous. */
+int hec_encode_host_batch(hec_coder_t *coder, const uint8_t *h_data, uint8_t *h_parity,
+                          size_t cell_len, size_t stripes, size_t chunk_stripes);
+
+/* ---- Measurement knobs (not part of the reference interface) ---------- *
+ * key 1: 16-B column chunks per lane per tile (1 or 2)
+ * key 2: non-temporal global loads/stores (0 or 1)
+ * key 3: resident blocks per CU for the grid (0 = occupancy-derived)
+ * Process-wide; affects launches made after the call. */
+int hec_tune_set(int key, int value);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* HDFS_EC_AMD_H */

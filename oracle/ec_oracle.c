@@ -1,0 +1,267 @@
+/*
+ * ec_oracle.c -- CPU restatement of hdfs-native's Reed-Solomon erasure-coding
+ * path.  TEST INFRASTRUCTURE ONLY: this file is the checker that tests/,
+ * __graft_entry__.smoke() and bench.py's `cpu_baseline` leg compare the HIP
+ * path against.  Nothing in the shipped library links or calls it.
+ *
+ * Reference (read-only, Rust, hdfs-native 0.14.1) -- every function below
+ * cites the file:line it restates:
+ *   rust/src/ec/gf256.rs   GF(2^8) field decl, Coder::{gen_rs_matrix,encode,decode}
+ *   rust/src/ec/matrix.rs  Matrix::{select_rows,invert}, Mul<&[&[u8]]>
+ *
+ * The field arithmetic lives in the third-party crate g2p 1.2.2
+ * (Cargo.lock: g2p/g2gen/g2poly 1.2.2), which is not vendored in the
+ * reference checkout.  Its published algorithm for GF(2^8) is plain
+ * polynomial arithmetic modulo the declared modulus (gf256.rs:7,
+ * 0b1_0001_1101 = 0x11D): add = XOR, mul = carry-less product reduced mod
+ * 0x11D, div = mul by the multiplicative inverse.  We restate that with the
+ * usual exp/log tables over generator 2 (which is primitive for 0x11D).
+ *
+ * Pinning (see tests/test_oracle.py):
+ *   - gen_rs_matrix is checked against the exact Hadoop Cauchy matrices in
+ *     gf256.rs:144-192 (RS(3,2), RS(6,3), RS(10,4));
+ *   - invert is checked with M^-1 * M = I as in gf256.rs:194-202 and
+ *     ec/mod.rs:152-160;
+ *   - gf_mul is cross-checked against a bit-serial carry-less multiply.
+ * Byte-level parity over real data is not pinned by any runnable reference
+ * test (the Hadoop interop test needs Java/Maven); it is fully determined by
+ * the pinned field + matrix because the code is linear.
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define ORC_OK 0
+#define ORC_ERR_INVALID (-1)
+#define ORC_ERR_NOT_ENOUGH_SHARDS (-2)
+#define ORC_ERR_SINGULAR (-6)
+
+static uint8_t g_exp[512];
+static uint8_t g_log[256];
+static int g_init = 0;
+
+/* gf256.rs:7  g2p::g2p!(GF256, 8, modulus: 0b1_0001_1101) */
+static void gf_init(void) {
+    if (g_init) return;
+    unsigned x = 1;
+    for (int i = 0; i < 255; i++) {
+        g_exp[i] = (uint8_t)x;
+        g_log[x] = (uint8_t)i;
+        x <<= 1;
+        if (x & 0x100) x ^= 0x11D;
+    }
+    for (int i = 255; i < 512; i++) g_exp[i] = g_exp[i - 255];
+    g_log[0] = 0; /* unused */
+    g_init = 1;
+}
+
+uint8_t orc_gf_mul(uint8_t a, uint8_t b) {
+    gf_init();
+    if (a == 0 || b == 0) return 0;
+    return g_exp[g_log[a] + g_log[b]];
+}
+
+/* Bit-serial carry-less multiply mod 0x11D: the definition g2p implements. */
+uint8_t orc_gf_mul_slow(uint8_t a, uint8_t b) {
+    unsigned r = 0, aa = a;
+    for (int i = 0; i < 8; i++) {
+        if (b & (1u << i)) r ^= aa;
+        aa <<= 1;
+        if (aa & 0x100) aa ^= 0x11D;
+    }
+    return (uint8_t)r;
+}
+
+uint8_t orc_gf_inv(uint8_t a) {
+    gf_init();
+    if (a == 0) return 0; /* g2p panics on 1/0; callers never do it */
+    return g_exp[255 - g_log[a]];
+}
+
+uint8_t orc_gf_div(uint8_t a, uint8_t b) { return orc_gf_mul(a, orc_gf_inv(b)); }
+
+/* gf256.rs:40-57  Coder::gen_rs_matrix -> (k+m) x k row-major */
+int orc_gen_rs_matrix(size_t k, size_t m, uint8_t *out) {
+    if (k == 0 || k + m > 256 || !out) return ORC_ERR_INVALID;
+    memset(out, 0, (k + m) * k);
+    for (size_t r = 0; r < k; r++) out[r * k + r] = 1;
+    for (size_t r = k; r < k + m; r++)
+        for (size_t c = 0; c < k; c++) {
+            uint8_t s = (uint8_t)r ^ (uint8_t)c; /* GF256(r) + GF256(c) */
+            out[r * k + c] = s == 0 ? 0 : orc_gf_div(1, s);
+        }
+    return ORC_OK;
+}
+
+/* matrix.rs:101-162  Matrix::invert (Gauss-Jordan on [M | I]).  The row-swap
+ * loop (:112-118) swaps with EVERY later row that has a non-zero in the pivot
+ * column; we keep that exact behaviour.  Returns ORC_ERR_SINGULAR where the
+ * reference panics ("Matrix is singular", :121-123). */
+int orc_invert(uint8_t *mat, size_t n) {
+    if (!mat || n == 0) return ORC_ERR_INVALID;
+    size_t w = 2 * n;
+    uint8_t *a = (uint8_t *)calloc(n * w, 1);
+    if (!a) return ORC_ERR_INVALID;
+    for (size_t r = 0; r < n; r++) {
+        memcpy(a + r * w, mat + r * n, n);
+        a[r * w + n + r] = 1;
+    }
+    uint8_t *tmp = (uint8_t *)malloc(w);
+    for (size_t r = 0; r < n; r++) {
+        if (a[r * w + r] == 0) {
+            for (size_t rs = r + 1; rs < n; rs++) {
+                if (a[rs * w + r] != 0) {
+                    memcpy(tmp, a + r * w, w);
+                    memcpy(a + r * w, a + rs * w, w);
+                    memcpy(a + rs * w, tmp, w);
+                }
+            }
+        }
+        if (a[r * w + r] == 0) {
+            free(tmp);
+            free(a);
+            return ORC_ERR_SINGULAR;
+        }
+        if (a[r * w + r] != 1) {
+            uint8_t scale = orc_gf_div(1, a[r * w + r]);
+            for (size_t c = 0; c < w; c++) a[r * w + c] = orc_gf_mul(a[r * w + c], scale);
+        }
+        for (size_t rb = r + 1; rb < n; rb++) {
+            uint8_t scale = a[rb * w + r];
+            if (scale)
+                for (size_t c = 0; c < w; c++) a[rb * w + c] ^= orc_gf_mul(a[r * w + c], scale);
+        }
+    }
+    for (size_t r = 1; r < n; r++)
+        for (size_t ra = 0; ra < r; ra++) {
+            uint8_t scale = a[ra * w + r];
+            if (scale)
+                for (size_t c = 0; c < w; c++) a[ra * w + c] ^= orc_gf_mul(a[r * w + c], scale);
+        }
+    for (size_t r = 0; r < n; r++) memcpy(mat + r * n, a + r * w + n, n);
+    free(tmp);
+    free(a);
+    return ORC_OK;
+}
+
+/* matrix.rs:181-199  Mul<Matrix> (square/rect matrix product over GF(2^8)). */
+void orc_matmul(const uint8_t *a, const uint8_t *b, size_t ar, size_t ac, size_t bc, uint8_t *out) {
+    for (size_t i = 0; i < ar; i++)
+        for (size_t j = 0; j < bc; j++) {
+            uint8_t acc = 0;
+            for (size_t t = 0; t < ac; t++) acc ^= orc_gf_mul(a[i * ac + t], b[t * bc + j]);
+            out[i * bc + j] = acc;
+        }
+}
+
+/* matrix.rs:204-231  Mul<&[&[u8]]> -- THE hot loop, reference loop order:
+ * for each input shard i, for each output row j, for each byte b:
+ *   result[j][b] += M[j][i] * rhs[i][b]        (:220-227)
+ * M is r x k row-major; out[j] must hold n bytes; out is zeroed first
+ * (Matrix::zeroes, :213). */
+void orc_matmul_shards(const uint8_t *M, size_t r, size_t k, const uint8_t *const *in, size_t n,
+                       uint8_t *const *out) {
+    gf_init();
+    for (size_t j = 0; j < r; j++) memset(out[j], 0, n);
+    for (size_t i = 0; i < k; i++) {
+        const uint8_t *src = in[i];
+        for (size_t j = 0; j < r; j++) {
+            uint8_t c = M[j * k + i];
+            uint8_t *dst = out[j];
+            if (c == 0) continue; /* 0 * x == 0: adds nothing */
+            unsigned lc = g_log[c];
+            for (size_t b = 0; b < n; b++) {
+                uint8_t x = src[b];
+                if (x) dst[b] ^= g_exp[lc + g_log[x]];
+            }
+        }
+    }
+}
+
+/* gf256.rs:61-80  Coder::encode: select parity rows k..k+m (:70), multiply. */
+int orc_encode(size_t k, size_t m, const uint8_t *const *data, size_t n, uint8_t *const *parity) {
+    if (k == 0 || m == 0 || k + m > 256 || n == 0 || !data || !parity) return ORC_ERR_INVALID;
+    uint8_t *mat = (uint8_t *)malloc((k + m) * k);
+    orc_gen_rs_matrix(k, m, mat);
+    orc_matmul_shards(mat + k * k, m, k, data, n, parity);
+    free(mat);
+    return ORC_OK;
+}
+
+/* gf256.rs:84-137  Coder::decode.
+ * shards[k+m]: NULL = missing.  Selection rules restated exactly:
+ *   - survivors = the FIRST k present shards in index order (:90-95, :117);
+ *   - missing = absent DATA indices only, ascending (:96-97); parity is never
+ *     regenerated;
+ *   - no missing data -> OK, nothing written (:102-105);
+ *   - fewer than k present -> "Not enough valid shards" (:107-111).
+ * out[i] (i < k) receives the reconstructed data shard i for every missing i.
+ * If decode_rows_out != NULL it receives the e x k decode matrix (row-major,
+ * rows in ascending missing-index order) and *e_out the count e. */
+int orc_decode_matrix(size_t k, size_t m, const int *present, uint8_t *dm, size_t *e_out,
+                      size_t *surv_out) {
+    size_t valid = 0, e = 0;
+    size_t surv[256], miss[256];
+    for (size_t i = 0; i < k + m; i++) {
+        if (present[i]) {
+            if (valid < k) surv[valid] = i;
+            valid++;
+        } else if (i < k) {
+            miss[e++] = i;
+        }
+    }
+    *e_out = e;
+    if (e == 0) return ORC_OK;
+    if (valid < k) return ORC_ERR_NOT_ENOUGH_SHARDS;
+    uint8_t *enc = (uint8_t *)malloc((k + m) * k);
+    uint8_t *sub = (uint8_t *)malloc(k * k);
+    orc_gen_rs_matrix(k, m, enc);
+    for (size_t r = 0; r < k; r++) memcpy(sub + r * k, enc + surv[r] * k, k); /* select_rows */
+    int rc = orc_invert(sub, k);
+    if (rc == ORC_OK)
+        for (size_t r = 0; r < e; r++) memcpy(dm + r * k, sub + miss[r] * k, k);
+    if (surv_out)
+        for (size_t r = 0; r < k; r++) surv_out[r] = surv[r];
+    free(sub);
+    free(enc);
+    return rc;
+}
+
+int orc_decode(size_t k, size_t m, const uint8_t *const *shards, size_t n, uint8_t *const *out) {
+    if (k == 0 || m == 0 || k + m > 256 || n == 0 || !shards || !out) return ORC_ERR_INVALID;
+    int present[256];
+    for (size_t i = 0; i < k + m; i++) present[i] = shards[i] != NULL;
+    size_t e = 0, surv[256];
+    uint8_t *dm = (uint8_t *)malloc(k * k);
+    int rc = orc_decode_matrix(k, m, present, dm, &e, surv);
+    if (rc != ORC_OK || e == 0) {
+        free(dm);
+        return rc;
+    }
+    const uint8_t *in[256];
+    uint8_t *o[256];
+    size_t j = 0;
+    for (size_t r = 0; r < k; r++) in[r] = shards[surv[r]];
+    for (size_t i = 0; i < k; i++)
+        if (!shards[i]) o[j++] = out[i];
+    orc_matmul_shards(dm, e, k, in, n, o);
+    free(dm);
+    return ORC_OK;
+}
+
+/* Stripe-batched encode over a [stripe][shard][cell] layout, used by
+ * bench.py's cpu_baseline leg.  Single-threaded, reference loop order per
+ * stripe (one Coder::encode call per stripe). */
+int orc_encode_batch(size_t k, size_t m, const uint8_t *data, size_t n, size_t stripes, uint8_t *parity) {
+    const uint8_t *in[256];
+    uint8_t *out[256];
+    uint8_t *mat = (uint8_t *)malloc((k + m) * k);
+    orc_gen_rs_matrix(k, m, mat);
+    for (size_t s = 0; s < stripes; s++) {
+        for (size_t i = 0; i < k; i++) in[i] = data + (s * k + i) * n;
+        for (size_t j = 0; j < m; j++) out[j] = parity + (s * m + j) * n;
+        orc_matmul_shards(mat + k * k, m, k, in, n, out);
+    }
+    free(mat);
+    return ORC_OK;
+}

@@ -1,0 +1,277 @@
+"""Pure-Python / numpy twin of the C oracle (oracle/ec_oracle.c).
+
+TEST INFRASTRUCTURE ONLY -- imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg as the checker; never by the shipped library.
+
+Restates hdfs-native 0.14.1's EC path (read-only reference, Rust):
+  rust/src/ec/gf256.rs:7        field GF(2^8), modulus 0x11D (g2p 1.2.2, not vendored)
+  rust/src/ec/gf256.rs:40-57    Coder::gen_rs_matrix (Hadoop Cauchy matrix)
+  rust/src/ec/gf256.rs:61-80    Coder::encode
+  rust/src/ec/gf256.rs:84-137   Coder::decode (first-k-present survivors)
+  rust/src/ec/matrix.rs:74-84   Matrix::select_rows (ascending original order)
+  rust/src/ec/matrix.rs:101-162 Matrix::invert (Gauss-Jordan)
+  rust/src/ec/matrix.rs:204-231 Mul<&[&[u8]]> (the hot loop)
+  rust/src/ec/mod.rs:62-89      EcSchema::ec_decode
+  rust/src/ec/mod.rs:93-144     resolve_ec_policy
+  rust/src/hdfs/block_writer.rs:817-851  CellBuffer::encode padding semantics
+
+Pinning: tests/test_oracle.py checks this module and the C oracle against the
+reference's own KATs (gf256.rs:144-202, mod.rs:152-160) and against each other.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+POLY = 0x11D
+
+EXP = [0] * 512
+LOG = [0] * 256
+_x = 1
+for _i in range(255):
+    EXP[_i] = _x
+    LOG[_x] = _i
+    _x <<= 1
+    if _x & 0x100:
+        _x ^= POLY
+for _i in range(255, 512):
+    EXP[_i] = EXP[_i - 255]
+
+
+def gf_mul(a: int, b: int) -> int:
+    if a == 0 or b == 0:
+        return 0
+    return EXP[LOG[a] + LOG[b]]
+
+
+def gf_inv(a: int) -> int:
+    if a == 0:
+        raise ZeroDivisionError("GF(2^8) inverse of 0")
+    return EXP[255 - LOG[a]]
+
+
+def gf_div(a: int, b: int) -> int:
+    return gf_mul(a, gf_inv(b))
+
+
+# 256x256 product table for vectorised numpy multiply
+MUL_TABLE = np.zeros((256, 256), dtype=np.uint8)
+for _a in range(1, 256):
+    for _b in range(1, 256):
+        MUL_TABLE[_a, _b] = EXP[LOG[_a] + LOG[_b]]
+
+
+def gen_rs_matrix(k: int, m: int) -> List[List[int]]:
+    """gf256.rs:40-57: identity on top, row r>=k col c<k = 1/(r^c)."""
+    mat = [[0] * k for _ in range(k + m)]
+    for r in range(k):
+        mat[r][r] = 1
+    for r in range(k, k + m):
+        for c in range(k):
+            s = (r ^ c) & 0xFF
+            mat[r][c] = 0 if s == 0 else gf_div(1, s)
+    return mat
+
+
+def select_rows(mat: List[List[int]], rows) -> List[List[int]]:
+    """matrix.rs:74-84 -- HashSet filter: rows come out in ORIGINAL order."""
+    keep = set(rows)
+    return [row[:] for i, row in enumerate(mat) if i in keep]
+
+
+def invert(mat: List[List[int]]) -> List[List[int]]:
+    """matrix.rs:101-162, including the swap-with-every-later-nonzero-row loop."""
+    n = len(mat)
+    if any(len(r) != n for r in mat):
+        raise ValueError("Cannot invert a non-square matrix")
+    a = [row[:] + [1 if i == j else 0 for j in range(n)] for i, row in enumerate(mat)]
+    w = 2 * n
+    for r in range(n):
+        if a[r][r] == 0:
+            for rs in range(r + 1, n):
+                if a[rs][r] != 0:
+                    a[r], a[rs] = a[rs], a[r]
+        if a[r][r] == 0:
+            raise ArithmeticError("Matrix is singular")
+        if a[r][r] != 1:
+            scale = gf_div(1, a[r][r])
+            a[r] = [gf_mul(v, scale) for v in a[r]]
+        for rb in range(r + 1, n):
+            scale = a[rb][r]
+            if scale:
+                a[rb] = [a[rb][c] ^ gf_mul(a[r][c], scale) for c in range(w)]
+    for r in range(1, n):
+        for ra in range(r):
+            scale = a[ra][r]
+            if scale:
+                a[ra] = [a[ra][c] ^ gf_mul(a[r][c], scale) for c in range(w)]
+    return [row[n:] for row in a]
+
+
+def matmul(a: List[List[int]], b: List[List[int]]) -> List[List[int]]:
+    """matrix.rs:181-199."""
+    out = []
+    for row in a:
+        orow = []
+        for j in range(len(b[0])):
+            acc = 0
+            for t in range(len(b)):
+                acc ^= gf_mul(row[t], b[t][j])
+            orow.append(acc)
+        out.append(orow)
+    return out
+
+
+def identity(n: int) -> List[List[int]]:
+    return [[1 if i == j else 0 for j in range(n)] for i in range(n)]
+
+
+def matmul_shards(mat: List[List[int]], shards: Sequence[np.ndarray]) -> List[np.ndarray]:
+    """matrix.rs:204-231 (i -> j -> byte order), vectorised over bytes."""
+    n = len(shards[0])
+    assert all(len(s) == n for s in shards)
+    out = [np.zeros(n, dtype=np.uint8) for _ in mat]
+    for i, src in enumerate(shards):
+        src = np.asarray(src, dtype=np.uint8)
+        for j, row in enumerate(mat):
+            c = row[i]
+            if c:
+                out[j] ^= MUL_TABLE[c][src]
+    return out
+
+
+def encode(k: int, m: int, data: Sequence[np.ndarray]) -> List[np.ndarray]:
+    """gf256.rs:61-80."""
+    assert len(data) == k
+    n = len(data[0])
+    assert all(len(d) == n for d in data)
+    mat = select_rows(gen_rs_matrix(k, m), range(k, k + m))
+    return matmul_shards(mat, data)
+
+
+class NotEnoughShards(Exception):
+    """HdfsError::ErasureCodingError("Not enough valid shards") (gf256.rs:107-111)."""
+
+
+def decode_plan(k: int, m: int, present: Sequence[bool]):
+    """Returns (survivors, missing_data, decode_matrix) per gf256.rs:84-126."""
+    valid, invalid = [], []
+    for i, p in enumerate(present):
+        if p:
+            valid.append(i)
+        elif i < k:
+            invalid.append(i)
+    if not invalid:
+        return [], [], []
+    if len(valid) < k:
+        raise NotEnoughShards("Not enough valid shards")
+    surv = valid[:k]
+    dm = invert(select_rows(gen_rs_matrix(k, m), surv))
+    dm = select_rows(dm, invalid)
+    return surv, invalid, dm
+
+
+def decode(k: int, m: int, shards: List[Optional[np.ndarray]]) -> List[Optional[np.ndarray]]:
+    """gf256.rs:84-137: fills missing DATA slots in a copy of `shards`."""
+    assert len(shards) == k + m
+    surv, miss, dm = decode_plan(k, m, [s is not None for s in shards])
+    res = list(shards)
+    if not miss:
+        return res
+    rec = matmul_shards(dm, [shards[i] for i in surv])
+    for idx, arr in zip(miss, rec):
+        res[idx] = arr
+    return res
+
+
+# ---- EcSchema-level helpers (mod.rs / block_writer.rs) --------------------
+
+POLICIES = {  # mod.rs:93-144
+    1: ("rs", 6, 3, 1024 * 1024),
+    2: ("rs", 3, 2, 1024 * 1024),
+    3: ("rs-legacy", 6, 3, 1024 * 1024),
+    4: ("xor", 2, 1, 1024 * 1024),
+    5: ("rs", 10, 4, 1024 * 1024),
+}
+
+
+def cell_buffer_encode(k: int, m: int, cells: Sequence[bytes]) -> List[bytes]:
+    """block_writer.rs:817-851: pad every buffer to len(buffers[0]) with 0,
+    encode, truncate data back, append parity."""
+    size = len(cells[0])
+    padded = [np.frombuffer(bytes(c) + b"\0" * (size - len(c)), dtype=np.uint8) for c in cells]
+    parity = encode(k, m, padded)
+    return [bytes(c) for c in cells] + [p.tobytes() for p in parity]
+
+
+def ec_decode(k: int, m: int, cell_size: int, codec: str,
+              vertical: List[Optional[bytes]]) -> List[bytes]:
+    """mod.rs:62-89: decode when a data shard is missing, then split each data
+    shard into cell_size cells in row order."""
+    vs = list(vertical)
+    if not all(v is not None or i >= k for i, v in enumerate(vs)):
+        if codec != "rs":
+            raise NotImplementedError(f"codec: {codec}")
+        arrs = [None if v is None else np.frombuffer(v, dtype=np.uint8) for v in vs]
+        arrs = decode(k, m, arrs)
+        vs = [None if a is None else a.tobytes() for a in arrs]
+    cells = []
+    offs = [0] * k
+    while vs[0] is not None and offs[0] < len(vs[0]):
+        for i in range(k):
+            cells.append(vs[i][offs[i]:offs[i] + cell_size])
+            offs[i] += cell_size
+    return cells
+
+
+# ---- ctypes access to the C oracle ----------------------------------------
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+C_LIB_PATH = os.path.join(_HERE, "build", "liboracle_ec.so")
+
+
+def load_c_oracle() -> ctypes.CDLL:
+    lib = ctypes.CDLL(C_LIB_PATH)
+    P = ctypes.c_void_p
+    S = ctypes.c_size_t
+    lib.orc_gf_mul.argtypes = [ctypes.c_uint8, ctypes.c_uint8]
+    lib.orc_gf_mul.restype = ctypes.c_uint8
+    lib.orc_gf_mul_slow.argtypes = [ctypes.c_uint8, ctypes.c_uint8]
+    lib.orc_gf_mul_slow.restype = ctypes.c_uint8
+    lib.orc_gen_rs_matrix.argtypes = [S, S, P]
+    lib.orc_invert.argtypes = [P, S]
+    lib.orc_encode.argtypes = [S, S, P, S, P]
+    lib.orc_decode.argtypes = [S, S, P, S, P]
+    lib.orc_encode_batch.argtypes = [S, S, P, S, S, P]
+    lib.orc_matmul_shards.argtypes = [P, S, S, P, S, P]
+    lib.orc_decode_matrix.argtypes = [S, S, P, P, P, P]
+    return lib
+
+
+def _ptrs(arrs):
+    return (ctypes.c_void_p * len(arrs))(*[0 if a is None else a.ctypes.data for a in arrs])
+
+
+def c_encode(lib, k: int, m: int, data: Sequence[np.ndarray]) -> List[np.ndarray]:
+    n = len(data[0])
+    data = [np.ascontiguousarray(d, dtype=np.uint8) for d in data]
+    par = [np.empty(n, dtype=np.uint8) for _ in range(m)]
+    rc = lib.orc_encode(k, m, _ptrs(data), n, _ptrs(par))
+    if rc != 0:
+        raise RuntimeError(f"orc_encode rc={rc}")
+    return par
+
+
+def c_decode(lib, k: int, m: int, shards: List[Optional[np.ndarray]]):
+    n = len(next(s for s in shards if s is not None))
+    shards = [None if s is None else np.ascontiguousarray(s, dtype=np.uint8) for s in shards]
+    out = [np.empty(n, dtype=np.uint8) if (i < k and shards[i] is None) else None for i in range(k + m)]
+    rc = lib.orc_decode(k, m, _ptrs(shards), n, _ptrs(out))
+    if rc == -2:
+        raise NotEnoughShards("Not enough valid shards")
+    if rc != 0:
+        raise RuntimeError(f"orc_decode rc={rc}")
+    return [shards[i] if out[i] is None else out[i] for i in range(k + m)]

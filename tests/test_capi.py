@@ -1,0 +1,96 @@
+"""C-ABI checks that need no GPU: the library loads, exports every symbol the
+header declares, and its host-side helpers (coding matrix, inversion, decode
+plan) match the oracle.  No compute is launched here."""
+import ctypes
+import itertools
+import os
+import re
+
+import pytest
+
+import ec_oracle as O
+import hdfs_native_ec as H
+from conftest import ROOT, gpu_available
+
+HEADER = os.path.join(ROOT, "include", "hdfs_ec_amd.h")
+
+
+def header_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(hec_[a-z_0-9]+)\s*\(", text)))
+
+
+def test_header_declares_what_binding_binds():
+    assert header_functions() == sorted(H.EXPORTS)
+
+
+def test_library_exports_every_declared_symbol():
+    lib = ctypes.CDLL(H.LIB_PATH)
+    for name in header_functions():
+        assert hasattr(lib, name), name
+
+
+def test_abi_version_and_strerror():
+    assert H.lib.hec_abi_version() == 1
+    assert "Not enough valid shards" in H.strerror(H.HEC_ERR_NOT_ENOUGH_SHARDS)
+    assert H.strerror(12345) == "unknown status"
+
+
+@pytest.mark.parametrize("k,m", [(3, 2), (6, 3), (10, 4), (1, 1), (32, 16), (2, 1)])
+def test_gen_rs_matrix_matches_oracle(k, m):
+    assert H.gen_rs_matrix(k, m) == O.gen_rs_matrix(k, m)
+
+
+def test_gen_rs_matrix_rejects_bad_args():
+    buf = (ctypes.c_uint8 * 16)()
+    assert H.lib.hec_gen_rs_matrix(0, 2, buf) == H.HEC_ERR_INVALID_ARG
+    assert H.lib.hec_gen_rs_matrix(200, 100, buf) == H.HEC_ERR_INVALID_ARG
+    assert H.lib.hec_gen_rs_matrix(3, 2, None) == H.HEC_ERR_INVALID_ARG
+
+
+def test_invert_matches_oracle_every_rs63_submatrix():
+    for rows in itertools.combinations(range(9), 6):
+        sub = O.select_rows(O.gen_rs_matrix(6, 3), rows)
+        assert H.matrix_invert(sub) == O.invert(sub)
+
+
+def test_invert_singular_is_status_not_abort():
+    with pytest.raises(ValueError):
+        H.matrix_invert([[1, 1], [1, 1]])
+
+
+@pytest.mark.parametrize("k,m", [(3, 2), (6, 3), (10, 4)])
+def test_decode_plan_matches_oracle_all_patterns(k, m):
+    for e in range(0, m + 2):
+        for miss in itertools.combinations(range(k + m), e):
+            present = [i not in miss for i in range(k + m)]
+            try:
+                want = O.decode_plan(k, m, present)
+            except O.NotEnoughShards:
+                with pytest.raises(H.ErasureCodingError):
+                    H.decode_plan(k, m, present)
+                continue
+            assert H.decode_plan(k, m, present) == (list(want[0]), list(want[1]), want[2])
+
+
+def test_coder_create_validates_args():
+    h = ctypes.c_void_p()
+    assert H.lib.hec_coder_create(0, 3, 0, ctypes.byref(h)) == H.HEC_ERR_INVALID_ARG
+    assert H.lib.hec_coder_create(33, 3, 0, ctypes.byref(h)) == H.HEC_ERR_INVALID_ARG
+    assert H.lib.hec_coder_create(6, 17, 0, ctypes.byref(h)) == H.HEC_ERR_INVALID_ARG
+    assert H.lib.hec_coder_create(6, 3, 0, None) == H.HEC_ERR_INVALID_ARG
+
+
+def test_null_coder_calls_return_status():
+    assert H.lib.hec_encode(None, None, 16, None) == H.HEC_ERR_INVALID_ARG
+    assert H.lib.hec_decode(None, None, 16, None) == H.HEC_ERR_INVALID_ARG
+    assert H.lib.hec_coder_data_units(None) == 0
+    H.lib.hec_coder_destroy(None)
+
+
+@pytest.mark.skipif(gpu_available(), reason="checks the no-device error path")
+def test_coder_create_without_device_is_clean_error():
+    h = ctypes.c_void_p()
+    assert H.lib.hec_coder_create(6, 3, 0, ctypes.byref(h)) == H.HEC_ERR_DEVICE
+    assert not h.value

@@ -1,0 +1,297 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the CPU oracle
+and the committed golden vectors, bit-exact.  Full-size configs
+(BASELINE.json) are checked through size-independent properties:
+encode -> erase -> decode round trips, linearity, sampled-stripe oracle
+checks.  Edge cases follow the reference tests (rust/tests/test_ec.rs:77-87
+sizes 16 B .. +-4 B around cell boundaries; 0..m failures; m+1 fails)."""
+import itertools
+
+import numpy as np
+import pytest
+
+import ec_oracle as O
+import hdfs_native_ec as H
+from hdfs_native_ec.synth import batch_data, bench_counter_shards, splitmix64_bytes
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU test run without a GPU"
+    return torch.device("cuda:0")
+
+
+_coders = {}
+
+
+def coder(k, m):
+    if (k, m) not in _coders:
+        _coders[(k, m)] = H.Coder(k, m, 0)
+    return _coders[(k, m)]
+
+
+def oracle_batch_encode(c_oracle, k, m, data: np.ndarray) -> np.ndarray:
+    S, _, n = data.shape
+    par = np.empty((S, m, n), dtype=np.uint8)
+    d = np.ascontiguousarray(data)
+    assert c_oracle.orc_encode_batch(k, m, d.ctypes.data, n, S, par.ctypes.data) == 0
+    return par
+
+
+# ---- host-buffer API (Coder::encode / Coder::decode drop-ins) ------------
+
+def test_host_encode_matches_golden(golden):
+    manifest, arrays = golden
+    for case in manifest["cases"]:
+        k, m, key = case["k"], case["m"], case["key"]
+        data = arrays[key + "_data"]
+        want = arrays[key + "_parity"]
+        got = coder(k, m).encode([bytes(d) for d in data])
+        for j in range(m):
+            assert got[j] == want[j].tobytes(), (key, j)
+
+
+def test_host_decode_golden_all_patterns(golden):
+    manifest, arrays = golden
+    for k, m in [(3, 2), (6, 3), (10, 4)]:
+        for n in (17, 4096):
+            key = f"rs{k}_{m}_n{n}"
+            data, par = arrays[key + "_data"], arrays[key + "_parity"]
+            full = [bytes(x) for x in data] + [bytes(x) for x in par]
+            for e in range(1, m + 1):
+                for miss in itertools.combinations(range(k + m), e):
+                    shards = [None if i in miss else full[i] for i in range(k + m)]
+                    coder(k, m).decode(shards)
+                    for i in range(k):
+                        assert shards[i] == full[i], (key, miss, i)
+                    for i in range(k, k + m):  # parity never regenerated
+                        assert (shards[i] is None) == (i in miss)
+
+
+def test_host_decode_too_many_failures():
+    # test_ec.rs:116-121: m+1 failures must error
+    k, m, n = 6, 3, 64
+    data = [splitmix64_bytes(9 + i, n).tobytes() for i in range(k)]
+    par = coder(k, m).encode(data)
+    shards = [None] * (m + 1) + (data + par)[m + 1:]
+    with pytest.raises(H.ErasureCodingError):
+        coder(k, m).decode(shards)
+
+
+def test_host_decode_nothing_missing_is_noop():
+    k, m = 3, 2
+    data = [b"abc", b"def", b"ghi"]
+    shards = data + [None, None]
+    coder(k, m).decode(shards)
+    assert shards == data + [None, None]
+
+
+def test_host_encode_reference_bench_fill(c_oracle):
+    # rust/benches/ec.rs:16-33 at 1 MiB slices (the bench uses 16 MiB)
+    k, m, n = 6, 3, 1 << 20
+    data = bench_counter_shards(k, n)
+    got = coder(k, m).encode([d.tobytes() for d in data])
+    want = O.c_encode(c_oracle, k, m, list(data))
+    assert all(g == w.tobytes() for g, w in zip(got, want))
+
+
+@pytest.mark.parametrize("n", [1, 4, 15, 16, 17, 1000, 4093, (1 << 20) - 4, (1 << 20) + 4])
+def test_host_encode_odd_lengths(c_oracle, n):
+    k, m = 3, 2
+    data = [splitmix64_bytes(100 + i + n, n) for i in range(k)]
+    got = coder(k, m).encode([d.tobytes() for d in data])
+    want = O.c_encode(c_oracle, k, m, data)
+    assert all(g == w.tobytes() for g, w in zip(got, want))
+
+
+def test_host_encode_edge_fills(c_oracle):
+    for fill in (0x00, 0xFF, 0x01, 0x80):
+        for k, m in [(3, 2), (6, 3), (10, 4)]:
+            data = [np.full(4096, fill, dtype=np.uint8) for _ in range(k)]
+            got = coder(k, m).encode([d.tobytes() for d in data])
+            want = O.c_encode(c_oracle, k, m, data)
+            assert all(g == w.tobytes() for g, w in zip(got, want))
+
+
+# ---- device-resident batched API --------------------------------------
+
+@pytest.mark.parametrize("k,m", [(3, 2), (6, 3), (10, 4), (2, 1), (5, 3), (12, 4), (4, 8), (32, 16), (1, 1)])
+@pytest.mark.parametrize("cell", [4096, 4093, 48, 7])
+def test_device_encode_batch_vs_oracle(dev, c_oracle, k, m, cell):
+    S = 6
+    data = batch_data(S, k, cell, first=k * 100 + cell)
+    want = oracle_batch_encode(c_oracle, k, m, data)
+    d = torch.from_numpy(data).to(dev)
+    p = torch.full((S, m, cell), 0xA5, dtype=torch.uint8, device=dev)
+    H.encode_batch(coder(k, m), d, p)
+    torch.cuda.synchronize()
+    assert np.array_equal(p.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("k,m", [(3, 2), (6, 3), (10, 4)])
+def test_device_decode_batch_all_data_patterns(dev, c_oracle, k, m):
+    S, cell = 4, 4096 + 16
+    data = batch_data(S, k, cell, first=7)
+    par = oracle_batch_encode(c_oracle, k, m, data)
+    d = torch.from_numpy(data).to(dev)
+    p = torch.from_numpy(par).to(dev)
+    pats = [c for e in range(1, m + 1) for c in itertools.combinations(range(k), e)]
+    if len(pats) > 60:
+        pats = pats[:30] + pats[-30:]
+    for miss in pats:
+        out = torch.zeros_like(d)
+        H.decode_batch(coder(k, m), d, p, miss, out)
+        torch.cuda.synchronize()
+        o = out.cpu().numpy()
+        for i in range(k):
+            if i in miss:
+                assert np.array_equal(o[:, i], data[:, i]), (miss, i)
+            else:
+                assert not o[:, i].any()  # untouched
+
+
+def test_device_decode_parity_survivor_mix(dev, c_oracle):
+    # survivors are the first k present: missing {1, 7} in RS(6,3) uses
+    # data 0,2,3,4,5 + parity 6
+    k, m, S, cell = 6, 3, 3, 1024
+    data = batch_data(S, k, cell, first=3)
+    par = oracle_batch_encode(c_oracle, k, m, data)
+    d = torch.from_numpy(data).to(dev)
+    p = torch.from_numpy(par).to(dev)
+    p[:, 1] = 0  # parity index 7 "missing" -- must not be read
+    dp, ds = H.stripe_layout_ptrs(d, k)
+    pp, ps = H.stripe_layout_ptrs(p, m)
+    out = torch.zeros_like(d)
+    op, os_ = H.stripe_layout_ptrs(out, k)
+    ptrs = [dp[0], None, dp[2], dp[3], dp[4], dp[5], pp[0], None, pp[2]]
+    coder(k, m).decode_device(ptrs, ds + ps, op, os_, cell, S, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(out[:, 1].cpu().numpy(), data[:, 1])
+
+
+def test_device_not_enough_shards(dev):
+    k, m = 6, 3
+    d = torch.zeros((1, k, 64), dtype=torch.uint8, device=dev)
+    p = torch.zeros((1, m, 64), dtype=torch.uint8, device=dev)
+    out = torch.zeros_like(d)
+    with pytest.raises(H.ErasureCodingError):
+        H.decode_batch(coder(k, m), d, p, [0, 1, 2, 3], out)
+
+
+def test_device_unaligned_layout(dev, c_oracle):
+    # shard bases off 16-B alignment -> byte kernel; results identical
+    k, m, S, cell = 6, 3, 3, 1000
+    data = batch_data(S, k, cell, first=11)
+    want = oracle_batch_encode(c_oracle, k, m, data)
+    buf = torch.zeros(S * k * cell + 1, dtype=torch.uint8, device=dev)
+    buf[1:] = torch.from_numpy(data.ravel()).to(dev)
+    pbuf = torch.zeros(S * m * cell + 3, dtype=torch.uint8, device=dev)
+    base, pbase = buf.data_ptr() + 1, pbuf.data_ptr() + 3
+    coder(k, m).encode_device([base + i * cell for i in range(k)], [k * cell] * k,
+                              [pbase + j * cell for j in range(m)], [m * cell] * m, cell, S,
+                              torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    got = pbuf[3:].cpu().numpy().reshape(S, m, cell)
+    assert np.array_equal(got, want)
+
+
+def test_gf_matmul_device_arbitrary_matrix(dev):
+    # the raw Mul<&[&[u8]]> (matrix.rs:204-231) with a random 7x5 matrix
+    rng = np.random.default_rng(3)
+    mat = rng.integers(0, 256, size=(7, 5)).tolist()
+    S, cell = 2, 4096 + 48
+    data = batch_data(S, 5, cell, first=1)
+    d = torch.from_numpy(data).to(dev)
+    out = torch.zeros((S, 7, cell), dtype=torch.uint8, device=dev)
+    ip, is_ = H.stripe_layout_ptrs(d, 5)
+    op, os_ = H.stripe_layout_ptrs(out, 7)
+    coder(3, 2).gf_matmul_device(mat, ip, is_, op, os_, cell, S, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    o = out.cpu().numpy()
+    for s in range(S):
+        want = O.matmul_shards(mat, list(data[s]))
+        for j in range(7):
+            assert np.array_equal(o[s, j], want[j])
+
+
+@pytest.mark.parametrize("knob", [(1, 2), (2, 1), (3, 1), (3, 2)])
+def test_tuning_variants_bit_identical(dev, c_oracle, knob):
+    k, m, S, cell = 6, 3, 5, 8192 + 16
+    data = batch_data(S, k, cell, first=21)
+    want = oracle_batch_encode(c_oracle, k, m, data)
+    d = torch.from_numpy(data).to(dev)
+    p = torch.zeros((S, m, cell), dtype=torch.uint8, device=dev)
+    try:
+        H.tune_set(*knob)
+        H.encode_batch(coder(k, m), d, p)
+        torch.cuda.synchronize()
+    finally:
+        H.tune_set(1, 1)
+        H.tune_set(2, 0)
+        H.tune_set(3, 0)
+    assert np.array_equal(p.cpu().numpy(), want)
+
+
+def test_encode_host_batch_pinned(c_oracle):
+    k, m, S, cell = 6, 3, 9, 65536
+    data = batch_data(S, k, cell, first=40)
+    want = oracle_batch_encode(c_oracle, k, m, data)
+    h_in = torch.from_numpy(data).pin_memory()
+    h_out = torch.zeros((S, m, cell), dtype=torch.uint8).pin_memory()
+    coder(k, m).encode_host_batch(h_in.data_ptr(), h_out.data_ptr(), cell, S, 4)
+    assert np.array_equal(h_out.numpy(), want)
+
+
+# ---- full-size configs (BASELINE.json) via size-independent properties ---
+
+def _device_random(shape, dev, seed):
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    return torch.randint(0, 256, shape, dtype=torch.uint8, device=dev, generator=g)
+
+
+@pytest.mark.parametrize("k,m,cell,S", [(6, 3, 1 << 20, 64), (10, 4, 1 << 20, 32), (6, 3, 1 << 16, 2048),
+                                        (3, 2, 1 << 20, 64)])
+def test_full_size_roundtrip_and_sampled_oracle(dev, c_oracle, k, m, cell, S):
+    d = _device_random((S, k, cell), dev, seed=k * 1000 + S)
+    p = torch.empty((S, m, cell), dtype=torch.uint8, device=dev)
+    H.encode_batch(coder(k, m), d, p)
+    # worst case: the first m data shards missing
+    miss = list(range(m))
+    out = torch.zeros_like(d)
+    H.decode_batch(coder(k, m), d, p, miss, out)
+    torch.cuda.synchronize()
+    assert torch.equal(out[:, :m], d[:, :m])
+    # sampled stripes against the oracle
+    for s in (0, S // 2, S - 1):
+        data = d[s].cpu().numpy()
+        want = O.c_encode(c_oracle, k, m, list(data))
+        got = p[s].cpu().numpy()
+        for j in range(m):
+            assert np.array_equal(got[j], want[j]), (s, j)
+
+
+def test_linearity(dev):
+    k, m, S, cell = 6, 3, 16, 1 << 18
+    a = _device_random((S, k, cell), dev, 1)
+    b = _device_random((S, k, cell), dev, 2)
+    pa, pb, pab = (torch.empty((S, m, cell), dtype=torch.uint8, device=dev) for _ in range(3))
+    H.encode_batch(coder(k, m), a, pa)
+    H.encode_batch(coder(k, m), b, pb)
+    H.encode_batch(coder(k, m), a ^ b, pab)
+    torch.cuda.synchronize()
+    assert torch.equal(pab, pa ^ pb)
+
+
+def test_repeatable(dev):
+    k, m, S, cell = 10, 4, 8, 1 << 20
+    d = _device_random((S, k, cell), dev, 5)
+    p1 = torch.empty((S, m, cell), dtype=torch.uint8, device=dev)
+    p2 = torch.empty_like(p1)
+    H.encode_batch(coder(k, m), d, p1)
+    H.encode_batch(coder(k, m), d, p2)
+    torch.cuda.synchronize()
+    assert torch.equal(p1, p2)

@@ -1,0 +1,180 @@
+"""Pins the CPU oracle (oracle/) against the reference's own known-answer
+tests and checks the C and Python restatements agree.  CPU only."""
+import itertools
+
+import numpy as np
+import pytest
+
+import ec_oracle as O
+from hdfs_native_ec.synth import bench_counter_shards, splitmix64_bytes
+
+# rust/src/ec/gf256.rs:144-192 -- "taken directly from the matrices created
+# by Hadoop via RSUtil.genCauchyMatrix" (parity rows; identity rows above).
+KAT_PARITY_ROWS = {
+    (3, 2): [[244, 142, 1], [71, 167, 122]],
+    (6, 3): [[122, 186, 71, 167, 142, 244], [186, 122, 167, 71, 244, 142],
+             [173, 157, 221, 152, 61, 170]],
+    (10, 4): [[221, 152, 173, 157, 93, 150, 61, 170, 142, 244],
+              [152, 221, 157, 173, 150, 93, 170, 61, 244, 142],
+              [61, 170, 93, 150, 173, 157, 221, 152, 71, 167],
+              [170, 61, 150, 93, 157, 173, 152, 221, 167, 71]],
+}
+
+
+@pytest.mark.parametrize("k,m", list(KAT_PARITY_ROWS))
+def test_gen_rs_matrix_kat_python(k, m):
+    mat = O.gen_rs_matrix(k, m)
+    assert mat[:k] == O.identity(k)
+    assert mat[k:] == KAT_PARITY_ROWS[(k, m)]
+
+
+@pytest.mark.parametrize("k,m", list(KAT_PARITY_ROWS))
+def test_gen_rs_matrix_kat_c(c_oracle, k, m):
+    buf = np.zeros((k + m) * k, dtype=np.uint8)
+    assert c_oracle.orc_gen_rs_matrix(k, m, buf.ctypes.data) == 0
+    mat = buf.reshape(k + m, k).tolist()
+    assert mat[:k] == O.identity(k)
+    assert mat[k:] == KAT_PARITY_ROWS[(k, m)]
+
+
+def test_invert_kat_gf256_rs():
+    # gf256.rs:194-202: rows {2,3,4} of RS(3,2); M^-1 * M == I
+    mat = O.select_rows(O.gen_rs_matrix(3, 2), [2, 3, 4])
+    assert O.matmul(O.invert(mat), mat) == O.identity(3)
+
+
+def test_invert_kat_mod_rs():
+    # ec/mod.rs:152-160
+    mat = [[0, 0, 1], [244, 142, 1], [71, 167, 122]]
+    assert O.matmul(O.invert(mat), mat) == O.identity(3)
+
+
+def test_invert_bench_matrix():
+    # benches/ec.rs:6-14 inverts rows 3..8 of RS(6,3)
+    mat = O.select_rows(O.gen_rs_matrix(6, 3), range(3, 9))
+    inv = O.invert(mat)
+    assert O.matmul(inv, mat) == O.identity(6)
+    # survey probe: missing {0,1,2} decode rows
+    assert inv[:3] == [[130, 54, 212, 144, 144, 72], [213, 42, 96, 216, 214, 112], [153, 30, 142, 68, 72, 48]]
+
+
+def test_c_invert_matches_python(c_oracle):
+    for k, m in KAT_PARITY_ROWS:
+        for rows in itertools.combinations(range(k + m), k):
+            sub = O.select_rows(O.gen_rs_matrix(k, m), rows)
+            buf = np.array(sub, dtype=np.uint8).ravel().copy()
+            assert c_oracle.orc_invert(buf.ctypes.data, k) == 0
+            assert buf.reshape(k, k).tolist() == O.invert(sub)
+            if k == 10:
+                break  # 1001 combos of 10x10 in pure python is slow; one is enough here
+
+
+def test_select_rows_keeps_original_order():
+    # matrix.rs:74-84 filters through a HashSet: order of the iterator is ignored
+    mat = O.gen_rs_matrix(3, 2)
+    assert O.select_rows(mat, [4, 0, 2]) == [mat[0], mat[2], mat[4]]
+
+
+def test_singular_raises():
+    with pytest.raises(ArithmeticError):
+        O.invert([[1, 1], [1, 1]])
+
+
+def test_gf_mul_tables_vs_bitserial(c_oracle):
+    for a in range(256):
+        for b in range(0, 256, 7):
+            assert c_oracle.orc_gf_mul(a, b) == c_oracle.orc_gf_mul_slow(a, b) == O.gf_mul(a, b)
+
+
+def test_field_axioms():
+    for a in range(1, 256):
+        assert O.gf_mul(a, O.gf_inv(a)) == 1
+    # distributivity on a sample
+    rng = np.random.default_rng(1)
+    for a, b, c in rng.integers(0, 256, size=(500, 3)):
+        assert O.gf_mul(int(a), int(b) ^ int(c)) == O.gf_mul(int(a), int(b)) ^ O.gf_mul(int(a), int(c))
+
+
+@pytest.mark.parametrize("k,m", [(3, 2), (6, 3), (10, 4), (2, 1), (4, 4)])
+def test_c_and_python_encode_agree(c_oracle, k, m):
+    for n in (1, 15, 17, 257, 4093):
+        data = splitmix64_bytes(77 + n, k * n).reshape(k, n)
+        py = O.encode(k, m, list(data))
+        c = O.c_encode(c_oracle, k, m, list(data))
+        for a, b in zip(py, c):
+            assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("k,m", [(3, 2), (6, 3), (10, 4)])
+def test_decode_roundtrip_all_patterns(c_oracle, k, m):
+    n = 61
+    data = splitmix64_bytes(5 + k, k * n).reshape(k, n)
+    par = O.encode(k, m, list(data))
+    full = list(data) + par
+    for e in range(0, m + 2):
+        for miss in itertools.combinations(range(k + m), e):
+            shards = [None if i in miss else full[i] for i in range(k + m)]
+            n_present = k + m - e
+            data_missing = any(i < k for i in miss)
+            if data_missing and n_present < k:
+                with pytest.raises(O.NotEnoughShards):
+                    O.decode(k, m, shards)
+                with pytest.raises(O.NotEnoughShards):
+                    O.c_decode(c_oracle, k, m, shards)
+                continue
+            res = O.decode(k, m, shards)
+            resc = O.c_decode(c_oracle, k, m, shards)
+            for i in range(k):
+                assert np.array_equal(res[i], data[i])
+                assert np.array_equal(resc[i], data[i])
+            # missing parity is never regenerated (gf256.rs:96-97)
+            for i in range(k, k + m):
+                if i in miss:
+                    assert res[i] is None
+            if k == 10 and e >= 3:
+                break
+
+
+def test_decode_uses_first_k_present():
+    # gf256.rs:90-95: survivors are the first k present in index order
+    surv, miss, dm = O.decode_plan(3, 2, [False, True, True, True, True])
+    assert surv == [1, 2, 3] and miss == [0]
+
+
+def test_golden_vectors_match_oracle(golden, c_oracle):
+    manifest, arrays = golden
+    for case in manifest["cases"]:
+        key, k, m = case["key"], case["k"], case["m"]
+        data = arrays[key + "_data"]
+        par = arrays[key + "_parity"]
+        got = O.c_encode(c_oracle, k, m, list(data))
+        assert all(np.array_equal(a, b) for a, b in zip(got, par)), key
+    for k, m in [(3, 2), (6, 3), (10, 4)]:
+        for plan in manifest[f"rs{k}_{m}_decode_plans"][:50]:
+            present = [i not in plan["missing"] for i in range(k + m)]
+            surv, miss, dm = O.decode_plan(k, m, present)
+            assert surv == plan["survivors"] and dm == plan["matrix"]
+
+
+def test_bench_counter_fill():
+    # rust/benches/ec.rs:19-27 big-endian i32 counter
+    s = bench_counter_shards(2, 16)
+    assert s[0].tolist() == [0, 0, 0, 0, 0, 0, 0, 1, 0, 0, 0, 2, 0, 0, 0, 3]
+    assert s[1][:4].tolist() == [0, 0, 0, 16]
+
+
+def test_cell_buffer_and_ec_decode_semantics():
+    # block_writer.rs:817-851 pads to len(buffers[0]); mod.rs:62-89 splits cells
+    k, m, cell = 3, 2, 8
+    cells = [bytes(range(8)), bytes(range(10, 13)), b""]
+    out = O.cell_buffer_encode(k, m, cells)
+    assert [len(c) for c in out] == [8, 3, 0, 8, 8]
+    vertical = [out[0], None, None, out[3], out[4]]
+    # pad to cell size as CellReader::next_cell does (block_reader.rs:370-371)
+    vertical = [None if v is None else v + b"\0" * (cell - len(v)) for v in vertical]
+    cells_back = O.ec_decode(k, m, cell, "rs", vertical)
+    assert cells_back[0] == bytes(range(8))
+    assert cells_back[1][:3] == bytes(range(10, 13)) and cells_back[1][3:] == b"\0" * 5
+    assert cells_back[2] == b"\0" * 8
+    with pytest.raises(NotImplementedError):
+        O.ec_decode(2, 1, cell, "xor", [None, b"\0" * 8, b"\0" * 8])
