@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -23,6 +24,23 @@
 #include "gf256.hpp"
 
 namespace {
+
+thread_local char g_last_error[256] = "";
+
+// Records the failing HIP call for hec_last_error() and returns `status`.
+int fail(int status, const char* what, hipError_t err) {
+    std::snprintf(g_last_error, sizeof(g_last_error), "%s: %s (%d)", what, hipGetErrorString(err), int(err));
+    return status;
+}
+
+#define HEC_HIP(call, status)                                  \
+    do {                                                       \
+        hipError_t e_ = (call);                                \
+        if (e_ != hipSuccess) {                                \
+            (void)hipGetLastError();                           \
+            return fail((status), #call, e_);                  \
+        }                                                      \
+    } while (0)
 
 struct DecodePlan {
     int status = HEC_OK;
@@ -64,10 +82,11 @@ struct hec_coder {
 
 namespace {
 
+// launch_gf_matmul: 0 ok, -1 invalid sizes, >0 the hipError_t of the launch.
 int to_status(int kernel_rc) {
     if (kernel_rc == 0) return HEC_OK;
     if (kernel_rc == -1) return HEC_ERR_INVALID_ARG;
-    return HEC_ERR_DEVICE;
+    return fail(HEC_ERR_DEVICE, "kernel launch", hipError_t(kernel_rc));
 }
 
 DecodePlan compute_plan(size_t k, size_t m, const uint8_t* present) {
@@ -148,10 +167,7 @@ int ensure_dbuf(hec_coder* c, size_t bytes) {
     if (c->dbuf) (void)hipFree(c->dbuf);
     c->dbuf = nullptr;
     c->dbuf_bytes = 0;
-    if (hipMalloc(&c->dbuf, bytes) != hipSuccess) {
-        (void)hipGetLastError();
-        return HEC_ERR_NO_MEMORY;
-    }
+    HEC_HIP(hipMalloc(&c->dbuf, bytes), HEC_ERR_NO_MEMORY);
     c->dbuf_bytes = bytes;
     return HEC_OK;
 }
@@ -163,7 +179,7 @@ int guarded(F&& f) {
     } catch (const std::bad_alloc&) {
         return HEC_ERR_NO_MEMORY;
     } catch (...) {
-        return HEC_ERR_DEVICE;
+        return fail(HEC_ERR_DEVICE, "unexpected C++ exception", hipErrorUnknown);
     }
 }
 
@@ -185,6 +201,8 @@ const char* hec_strerror(int status) {
 }
 
 int hec_abi_version(void) { return HEC_ABI_VERSION; }
+
+const char* hec_last_error(void) { return g_last_error; }
 
 int hec_gen_rs_matrix(size_t data_units, size_t parity_units, uint8_t* out) {
     if (!out || data_units == 0 || data_units + parity_units > 256) return HEC_ERR_INVALID_ARG;
@@ -223,26 +241,25 @@ int hec_coder_create(size_t data_units, size_t parity_units, int device, hec_cod
         return HEC_ERR_INVALID_ARG;
     return guarded([&] {
         int ndev = 0;
-        if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) {
-            (void)hipGetLastError();
-            return HEC_ERR_DEVICE;
-        }
+        HEC_HIP(hipGetDeviceCount(&ndev), HEC_ERR_DEVICE);
+        if (device < 0 || device >= ndev) return fail(HEC_ERR_DEVICE, "device ordinal", hipErrorInvalidDevice);
         auto* c = new hec_coder();
         c->k = data_units;
         c->m = parity_units;
         c->device = device;
         c->enc = hec::gen_rs_matrix(data_units, parity_units);
-        DeviceGuard g(device);
-        bool ok = g.ok;
-        ok = ok && hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess;
-        for (int i = 0; i < 2 && ok; i++)
-            ok = hipStreamCreateWithFlags(&c->copy_stream[i], hipStreamNonBlocking) == hipSuccess;
-        for (int i = 0; i < 4 && ok; i++)
-            ok = hipEventCreateWithFlags(&c->ev[i], hipEventDisableTiming) == hipSuccess;
-        if (!ok) {
-            (void)hipGetLastError();
+        int rc = [&] {
+            DeviceGuard g(device);
+            if (!g.ok) return fail(HEC_ERR_DEVICE, "hipSetDevice", hipErrorInvalidDevice);
+            HEC_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), HEC_ERR_DEVICE);
+            for (int i = 0; i < 2; i++)
+                HEC_HIP(hipStreamCreateWithFlags(&c->copy_stream[i], hipStreamNonBlocking), HEC_ERR_DEVICE);
+            for (int i = 0; i < 4; i++) HEC_HIP(hipEventCreateWithFlags(&c->ev[i], hipEventDisableTiming), HEC_ERR_DEVICE);
+            return HEC_OK;
+        }();
+        if (rc != HEC_OK) {
             hec_coder_destroy(c);
-            return HEC_ERR_DEVICE;
+            return rc;
         }
         *out = c;
         return HEC_OK;
@@ -277,7 +294,7 @@ int hec_gf_matmul_device(hec_coder_t* c, const uint8_t* matrix, size_t rows, siz
     if (!c) return HEC_ERR_INVALID_ARG;
     return guarded([&] {
         DeviceGuard g(c->device);
-        if (!g.ok) return HEC_ERR_DEVICE;
+        if (!g.ok) return fail(HEC_ERR_DEVICE, "hipSetDevice", hipErrorInvalidDevice);
         return matmul_batch(c->device, matrix, rows, cols, d_in, in_strides, d_out, out_strides, cell_len, stripes,
                             static_cast<hipStream_t>(hip_stream));
     });
@@ -315,7 +332,7 @@ int hec_decode_device(hec_coder_t* c, const uint8_t* const* d_shards, const size
             ost[r] = out_strides[p.missing[r]];
         }
         DeviceGuard g(c->device);
-        if (!g.ok) return HEC_ERR_DEVICE;
+        if (!g.ok) return fail(HEC_ERR_DEVICE, "hipSetDevice", hipErrorInvalidDevice);
         return matmul_batch(c->device, p.matrix.data(), p.missing.size(), c->k, in, ist, out, ost, cell_len, stripes,
                             static_cast<hipStream_t>(hip_stream));
     });
@@ -330,7 +347,7 @@ int hec_encode(hec_coder_t* c, const uint8_t* const* data, size_t shard_len, uin
     return guarded([&] {
         std::lock_guard<std::mutex> lk(c->host_mu);
         DeviceGuard g(c->device);
-        if (!g.ok) return HEC_ERR_DEVICE;
+        if (!g.ok) return fail(HEC_ERR_DEVICE, "hipSetDevice", hipErrorInvalidDevice);
         const size_t pitch = (shard_len + 255) & ~size_t(255);
         int rc = ensure_dbuf(c, pitch * (c->k + c->m));
         if (rc != HEC_OK) return rc;
@@ -340,18 +357,16 @@ int hec_encode(hec_coder_t* c, const uint8_t* const* data, size_t shard_len, uin
         for (size_t i = 0; i < c->k + c->m; i++) strides[i] = pitch;
         for (size_t i = 0; i < c->k; i++) {
             din[i] = c->dbuf + i * pitch;
-            if (hipMemcpyAsync(c->dbuf + i * pitch, data[i], shard_len, hipMemcpyHostToDevice, c->stream) !=
-                hipSuccess)
-                return HEC_ERR_DEVICE;
+            HEC_HIP(hipMemcpyAsync(c->dbuf + i * pitch, data[i], shard_len, hipMemcpyHostToDevice, c->stream), HEC_ERR_DEVICE);
         }
         for (size_t j = 0; j < c->m; j++) dout[j] = c->dbuf + (c->k + j) * pitch;
         rc = matmul_batch(c->device, c->enc.data() + c->k * c->k, c->m, c->k, din, strides, dout, strides, shard_len,
                           1, c->stream);
         if (rc != HEC_OK) return rc;
         for (size_t j = 0; j < c->m; j++)
-            if (hipMemcpyAsync(parity[j], dout[j], shard_len, hipMemcpyDeviceToHost, c->stream) != hipSuccess)
-                return HEC_ERR_DEVICE;
-        return hipStreamSynchronize(c->stream) == hipSuccess ? HEC_OK : HEC_ERR_DEVICE;
+            HEC_HIP(hipMemcpyAsync(parity[j], dout[j], shard_len, hipMemcpyDeviceToHost, c->stream), HEC_ERR_DEVICE);
+        HEC_HIP(hipStreamSynchronize(c->stream), HEC_ERR_DEVICE);
+        return HEC_OK;
     });
 }
 
@@ -368,7 +383,7 @@ int hec_decode(hec_coder_t* c, const uint8_t* const* shards, size_t shard_len, u
             if (!out[i]) return HEC_ERR_INVALID_ARG;
         std::lock_guard<std::mutex> lk(c->host_mu);
         DeviceGuard g(c->device);
-        if (!g.ok) return HEC_ERR_DEVICE;
+        if (!g.ok) return fail(HEC_ERR_DEVICE, "hipSetDevice", hipErrorInvalidDevice);
         const size_t e = p.missing.size();
         const size_t pitch = (shard_len + 255) & ~size_t(255);
         int rc = ensure_dbuf(c, pitch * (c->k + e));
@@ -379,17 +394,15 @@ int hec_decode(hec_coder_t* c, const uint8_t* const* shards, size_t shard_len, u
         for (size_t i = 0; i < c->k + e; i++) strides[i] = pitch;
         for (size_t r = 0; r < c->k; r++) {
             din[r] = c->dbuf + r * pitch;
-            if (hipMemcpyAsync(c->dbuf + r * pitch, shards[p.survivors[r]], shard_len, hipMemcpyHostToDevice,
-                               c->stream) != hipSuccess)
-                return HEC_ERR_DEVICE;
+            HEC_HIP(hipMemcpyAsync(c->dbuf + r * pitch, shards[p.survivors[r]], shard_len, hipMemcpyHostToDevice, c->stream), HEC_ERR_DEVICE);
         }
         for (size_t r = 0; r < e; r++) dout[r] = c->dbuf + (c->k + r) * pitch;
         rc = matmul_batch(c->device, p.matrix.data(), e, c->k, din, strides, dout, strides, shard_len, 1, c->stream);
         if (rc != HEC_OK) return rc;
         for (size_t r = 0; r < e; r++)
-            if (hipMemcpyAsync(out[p.missing[r]], dout[r], shard_len, hipMemcpyDeviceToHost, c->stream) != hipSuccess)
-                return HEC_ERR_DEVICE;
-        return hipStreamSynchronize(c->stream) == hipSuccess ? HEC_OK : HEC_ERR_DEVICE;
+            HEC_HIP(hipMemcpyAsync(out[p.missing[r]], dout[r], shard_len, hipMemcpyDeviceToHost, c->stream), HEC_ERR_DEVICE);
+        HEC_HIP(hipStreamSynchronize(c->stream), HEC_ERR_DEVICE);
+        return HEC_OK;
     });
 }
 
@@ -403,7 +416,7 @@ int hec_encode_host_batch(hec_coder_t* c, const uint8_t* h_data, uint8_t* h_pari
     return guarded([&] {
         std::lock_guard<std::mutex> lk(c->host_mu);
         DeviceGuard g(c->device);
-        if (!g.ok) return HEC_ERR_DEVICE;
+        if (!g.ok) return fail(HEC_ERR_DEVICE, "hipSetDevice", hipErrorInvalidDevice);
         const size_t k = c->k, m = c->m;
         chunk_stripes = std::min(chunk_stripes, stripes);
         const size_t in_bytes = chunk_stripes * k * cell_len;
@@ -419,11 +432,9 @@ int hec_encode_host_batch(hec_coder_t* c, const uint8_t* h_data, uint8_t* h_pari
             uint8_t* dpar = din + in_bytes;
             const size_t s0 = q * chunk_stripes;
             const size_t ns = std::min(chunk_stripes, stripes - s0);
-            if (hipMemcpyAsync(din, h_data + s0 * k * cell_len, ns * k * cell_len, hipMemcpyHostToDevice, cs) !=
-                hipSuccess)
-                return HEC_ERR_DEVICE;
-            if (hipEventRecord(c->ev[slot], cs) != hipSuccess) return HEC_ERR_DEVICE;
-            if (hipStreamWaitEvent(c->stream, c->ev[slot], 0) != hipSuccess) return HEC_ERR_DEVICE;
+            HEC_HIP(hipMemcpyAsync(din, h_data + s0 * k * cell_len, ns * k * cell_len, hipMemcpyHostToDevice, cs), HEC_ERR_DEVICE);
+            HEC_HIP(hipEventRecord(c->ev[slot], cs), HEC_ERR_DEVICE);
+            HEC_HIP(hipStreamWaitEvent(c->stream, c->ev[slot], 0), HEC_ERR_DEVICE);
             const uint8_t* in[HEC_MAX_DATA_UNITS];
             uint8_t* out[HEC_MAX_PARITY_UNITS];
             size_t ist[HEC_MAX_DATA_UNITS], ost[HEC_MAX_PARITY_UNITS];
@@ -437,27 +448,36 @@ int hec_encode_host_batch(hec_coder_t* c, const uint8_t* h_data, uint8_t* h_pari
             }
             rc = matmul_batch(c->device, c->enc.data() + k * k, m, k, in, ist, out, ost, cell_len, ns, c->stream);
             if (rc != HEC_OK) return rc;
-            if (hipEventRecord(c->ev[2 + slot], c->stream) != hipSuccess) return HEC_ERR_DEVICE;
-            if (hipStreamWaitEvent(cs, c->ev[2 + slot], 0) != hipSuccess) return HEC_ERR_DEVICE;
-            if (hipMemcpyAsync(h_parity + s0 * m * cell_len, dpar, ns * m * cell_len, hipMemcpyDeviceToHost, cs) !=
-                hipSuccess)
-                return HEC_ERR_DEVICE;
+            HEC_HIP(hipEventRecord(c->ev[2 + slot], c->stream), HEC_ERR_DEVICE);
+            HEC_HIP(hipStreamWaitEvent(cs, c->ev[2 + slot], 0), HEC_ERR_DEVICE);
+            HEC_HIP(hipMemcpyAsync(h_parity + s0 * m * cell_len, dpar, ns * m * cell_len, hipMemcpyDeviceToHost, cs), HEC_ERR_DEVICE);
         }
-        bool ok = hipStreamSynchronize(c->copy_stream[0]) == hipSuccess;
-        ok = hipStreamSynchronize(c->copy_stream[1]) == hipSuccess && ok;
-        ok = hipStreamSynchronize(c->stream) == hipSuccess && ok;
-        return ok ? HEC_OK : HEC_ERR_DEVICE;
+        HEC_HIP(hipStreamSynchronize(c->copy_stream[0]), HEC_ERR_DEVICE);
+        HEC_HIP(hipStreamSynchronize(c->copy_stream[1]), HEC_ERR_DEVICE);
+        HEC_HIP(hipStreamSynchronize(c->stream), HEC_ERR_DEVICE);
+        return HEC_OK;
     });
 }
 
-// Tuning knobs for the measurement harness (not part of the reference API):
-// key 1 = column chunks per lane (1|2), 2 = non-temporal loads/stores (0|1),
-// 3 = blocks per CU (0 = occupancy-derived).
+// Tuning knobs for the measurement harness (not part of the reference API).
+// A value of 0 (-1 for key 2) restores the per-shape default.
+// key 1 = 16-B column chunks per lane (1|2|4), 2 = non-temporal loads/stores
+// (0|1), 3 = resident blocks per CU, 4 = threads per block (256|512).
 int hec_tune_set(int key, int value) {
     switch (key) {
-        case 1: hec::g_tune_unroll = value == 2 ? 2 : 1; return HEC_OK;
-        case 2: hec::g_tune_nt = value ? 1 : 0; return HEC_OK;
-        case 3: hec::g_tune_blocks_per_cu = value < 0 ? 0 : value; return HEC_OK;
+        case 1:
+            if (value != 0 && value != 1 && value != 2 && value != 4) return HEC_ERR_INVALID_ARG;
+            hec::g_tune_unroll = value;
+            return HEC_OK;
+        case 2: hec::g_tune_nt = value < 0 ? -1 : (value ? 1 : 0); return HEC_OK;
+        case 3:
+            if (value < 0 || value > 16) return HEC_ERR_INVALID_ARG;
+            hec::g_tune_blocks_per_cu = value;
+            return HEC_OK;
+        case 4:
+            if (value != 0 && value != 256 && value != 512) return HEC_ERR_INVALID_ARG;
+            hec::g_tune_block = value;
+            return HEC_OK;
         default: return HEC_ERR_INVALID_ARG;
     }
 }

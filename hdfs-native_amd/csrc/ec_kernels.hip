@@ -108,17 +108,19 @@ __device__ __forceinline__ void store16(uint8_t* p, u32x4 v) {
 }
 
 // Stage log/antilog + coefficient rows in LDS, build the perm tables.
-template <int R>
+template <int R, int BS>
 __device__ __forceinline__ void prologue(const MatmulArgs& a, int k, PermTable (*s_tab)[kMaxK], uint8_t* s_exp,
                                          uint8_t* s_log, uint8_t* s_coef) {
-    static_assert(kBlock == 256, "prologue assumes 256 threads");
+    static_assert(BS >= 256 && BS % 256 == 0, "prologue assumes >= 256 threads");
     const int tid = threadIdx.x;
-    s_exp[tid] = kDevGf.exp[tid];
-    s_exp[tid + 256] = kDevGf.exp[tid + 256];
-    s_log[tid] = kDevGf.log[tid];
+    if (tid < 256) {
+        s_exp[tid] = kDevGf.exp[tid];
+        s_exp[tid + 256] = kDevGf.exp[tid + 256];
+        s_log[tid] = kDevGf.log[tid];
+    }
     if (tid < R * kMaxK) s_coef[tid] = a.coef[tid];
     __syncthreads();
-    for (int t = tid; t < R * k; t += kBlock) {
+    for (int t = tid; t < R * k; t += BS) {
         int j = t / k, i = t - j * k;
         build_perm_table(&s_tab[j][i], s_coef[j * kMaxK + i], s_exp, s_log);
     }
@@ -129,19 +131,19 @@ __device__ __forceinline__ void prologue(const MatmulArgs& a, int k, PermTable (
 // Vector kernel: 16 B per lane per shard, U column chunks per lane.
 // K = compile-time input count (0 = runtime a.k), R = outputs (1..4).
 // ---------------------------------------------------------------------------
-template <int K, int R, int U, bool NT>
-__global__ __launch_bounds__(kBlock) void gf_matmul_v16(MatmulArgs a) {
+template <int K, int R, int U, bool NT, int BS>
+__global__ __launch_bounds__(BS) void gf_matmul_v16(MatmulArgs a) {
     __shared__ PermTable s_tab[R][kMaxK];
     __shared__ uint8_t s_exp[512];
     __shared__ uint8_t s_log[256];
     __shared__ uint8_t s_coef[R * kMaxK];
     const int k = K ? K : a.k;
-    prologue<R>(a, k, s_tab, s_exp, s_log, s_coef);
+    prologue<R, BS>(a, k, s_tab, s_exp, s_log, s_coef);
 
     const uint32_t chunks = a.chunks;  // 16-B chunks per cell
     const uint32_t tps = a.tiles_per_stripe;
     const uint32_t total = a.total_tiles;
-    constexpr uint32_t TILE = kBlock * U;
+    constexpr uint32_t TILE = BS * U;
 
     for (uint32_t tile = blockIdx.x; tile < total; tile += gridDim.x) {
         const uint32_t stripe = tile / tps;
@@ -149,36 +151,74 @@ __global__ __launch_bounds__(kBlock) void gf_matmul_v16(MatmulArgs a) {
         // Keep the per-coefficient table reads inside the loop (LDS broadcast
         // reads) instead of letting LICM pin R*K*5 VGPRs for the whole kernel.
         asm volatile("" ::: "memory");
+        if constexpr (K > 0) {
+            // Compile-time K: every shard's loads for all U chunks are issued
+            // before any arithmetic (K*U x 1 KiB in flight per wave).
+            u32x4 x[U][K];
+            bool live[U];
 #pragma unroll
-        for (int u = 0; u < U; u++) {
-            const uint32_t col = tcol * TILE + u * kBlock + threadIdx.x;
-            if (col >= chunks) continue;
-            const uint64_t off = uint64_t(col) * 16u;
-            u32x4 acc[R];
+            for (int u = 0; u < U; u++) {
+                const uint32_t col = tcol * TILE + u * BS + threadIdx.x;
+                live[u] = col < chunks;
+                const uint64_t off = uint64_t(live[u] ? col : 0) * 16u;
 #pragma unroll
-            for (int j = 0; j < R; j++) acc[j] = u32x4{0, 0, 0, 0};
-            if constexpr (K > 0) {
-                u32x4 x[K];
+                for (int i = 0; i < K; i++) x[u][i] = load16<NT>(a.in[i] + uint64_t(stripe) * a.in_stride[i] + off);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            u32x4 acc[U][R];
 #pragma unroll
-                for (int i = 0; i < K; i++) x[i] = load16<NT>(a.in[i] + uint64_t(stripe) * a.in_stride[i] + off);
-                // Issue every shard's load before any arithmetic: K x 1 KiB in
-                // flight per wave instead of the scheduler's 2.
-                __builtin_amdgcn_sched_barrier(0);
+            for (int u = 0; u < U; u++)
 #pragma unroll
-                for (int i = 0; i < K; i++) {
-                    Sel s[4];
+                for (int j = 0; j < R; j++) acc[u][j] = u32x4{0, 0, 0, 0};
 #pragma unroll
-                    for (int d = 0; d < 4; d++) s[d] = make_sel(x[i][d]);
+            for (int i = 0; i < K; i++) {
+                // Opaque per-input table offset: input i's coefficient-table
+                // reads cannot be hoisted above this point (otherwise the
+                // compiler front-loads all R*K tables = R*K*5 VGPRs).
+                uint32_t toff = uint32_t(i) * uint32_t(sizeof(PermTable));
+                asm volatile("" : "+v"(toff));
 #pragma unroll
-                    for (int j = 0; j < R; j++) {
-                        const PermTable& t = s_tab[j][i];
-                        const uint32_t t0lo = t.t0lo, t0hi = t.t0hi, t1lo = t.t1lo, t1hi = t.t1hi, t2 = t.t2;
+                for (int u = 0; u < U; u++)
+#pragma unroll
+                    for (int j = 0; j < R; j++) asm volatile("" : "+v"(acc[u][j]) : "v"(toff));
+                Sel s[U][4];
+#pragma unroll
+                for (int u = 0; u < U; u++)
+#pragma unroll
+                    for (int d = 0; d < 4; d++) s[u][d] = make_sel(x[u][i][d]);
+#pragma unroll
+                for (int j = 0; j < R; j++) {
+                    const PermTable& t =
+                        *reinterpret_cast<const PermTable*>(reinterpret_cast<const char*>(&s_tab[j][0]) + toff);
+                    const uint32_t t0lo = t.t0lo, t0hi = t.t0hi, t1lo = t.t1lo, t1hi = t.t1hi, t2 = t.t2;
+#pragma unroll
+                    for (int u = 0; u < U; u++)
 #pragma unroll
                         for (int d = 0; d < 4; d++)
-                            acc[j][d] ^= gf_mul4(t0lo, t0hi, t1lo, t1hi, t2, s[d].s0, s[d].s1, s[d].s2);
-                    }
+                            acc[u][j][d] ^= gf_mul4(t0lo, t0hi, t1lo, t1hi, t2, s[u][d].s0, s[u][d].s1, s[u][d].s2);
                 }
-            } else {
+                // one input at a time: stops the scheduler from hoisting every
+                // coefficient's table read (R*K*5 VGPRs) to the top
+                __builtin_amdgcn_sched_barrier(0);
+            }
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                if (!live[u]) continue;
+                const uint64_t off = uint64_t(tcol * TILE + u * BS + threadIdx.x) * 16u;
+#pragma unroll
+                for (int j = 0; j < R; j++)
+                    store16<NT>(a.out[j] + uint64_t(stripe) * a.out_stride[j] + off, acc[u][j]);
+            }
+        } else {
+            // Runtime K: one shard at a time, U chunks per lane.
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const uint32_t col = tcol * TILE + u * BS + threadIdx.x;
+                if (col >= chunks) continue;
+                const uint64_t off = uint64_t(col) * 16u;
+                u32x4 acc[R];
+#pragma unroll
+                for (int j = 0; j < R; j++) acc[j] = u32x4{0, 0, 0, 0};
                 for (int i = 0; i < k; i++) {
                     u32x4 x = load16<NT>(a.in[i] + uint64_t(stripe) * a.in_stride[i] + off);
                     Sel s[4];
@@ -193,9 +233,9 @@ __global__ __launch_bounds__(kBlock) void gf_matmul_v16(MatmulArgs a) {
                             acc[j][d] ^= gf_mul4(t0lo, t0hi, t1lo, t1hi, t2, s[d].s0, s[d].s1, s[d].s2);
                     }
                 }
-            }
 #pragma unroll
-            for (int j = 0; j < R; j++) store16<NT>(a.out[j] + uint64_t(stripe) * a.out_stride[j] + off, acc[j]);
+                for (int j = 0; j < R; j++) store16<NT>(a.out[j] + uint64_t(stripe) * a.out_stride[j] + off, acc[j]);
+            }
         }
     }
 }
@@ -248,35 +288,41 @@ struct KernelInfo {
     int blocks_per_cu = 0;
 };
 
-template <int K, int R, int U, bool NT>
+template <int K, int R, int U, bool NT, int BS>
 const void* vec_fn() {
-    return reinterpret_cast<const void*>(&gf_matmul_v16<K, R, U, NT>);
+    return reinterpret_cast<const void*>(&gf_matmul_v16<K, R, U, NT, BS>);
 }
 
-template <int R, int U, bool NT>
+template <int R, int U, bool NT, int BS>
 const void* pick_k(int k) {
     switch (k) {
-        case 2: return vec_fn<2, R, U, NT>();
-        case 3: return vec_fn<3, R, U, NT>();
-        case 6: return vec_fn<6, R, U, NT>();
-        case 10: return vec_fn<10, R, U, NT>();
-        default: return vec_fn<0, R, U, NT>();
+        case 2: return vec_fn<2, R, U, NT, BS>();
+        case 3: return vec_fn<3, R, U, NT, BS>();
+        case 6: return vec_fn<6, R, U, NT, BS>();
+        case 10: return vec_fn<10, R, U, NT, BS>();
+        default: return vec_fn<0, R, U, NT, BS>();
     }
 }
 
-template <int U, bool NT>
+template <int U, bool NT, int BS>
 const void* pick_r(int k, int r) {
     switch (r) {
-        case 1: return pick_k<1, U, NT>(k);
-        case 2: return pick_k<2, U, NT>(k);
-        case 3: return pick_k<3, U, NT>(k);
-        default: return pick_k<4, U, NT>(k);
+        case 1: return pick_k<1, U, NT, BS>(k);
+        case 2: return pick_k<2, U, NT, BS>(k);
+        case 3: return pick_k<3, U, NT, BS>(k);
+        default: return pick_k<4, U, NT, BS>(k);
     }
 }
 
-const void* pick_vec(int k, int r, int unroll, bool nt) {
-    if (unroll == 2) return nt ? pick_r<2, true>(k, r) : pick_r<2, false>(k, r);
-    return nt ? pick_r<1, true>(k, r) : pick_r<1, false>(k, r);
+// Shapes compiled: (chunks per lane U, block size BS) in
+// {(1,256),(2,256),(4,256),(1,512),(2,512)}, each with and without
+// non-temporal access.
+template <bool NT>
+const void* pick_shape(int k, int r, int unroll, int bs) {
+    if (bs == 512) return unroll >= 2 ? pick_r<2, NT, 512>(k, r) : pick_r<1, NT, 512>(k, r);
+    if (unroll == 4) return pick_r<4, NT, 256>(k, r);
+    if (unroll == 2) return pick_r<2, NT, 256>(k, r);
+    return pick_r<1, NT, 256>(k, r);
 }
 
 int g_num_cus[64] = {0};
@@ -291,17 +337,29 @@ int num_cus(int dev) {
     return g_num_cus[dev];
 }
 
-int occupancy(const void* fn) {
-    int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, kBlock, 0) != hipSuccess || nb <= 0) nb = 4;
-    return nb;
+}  // namespace
+
+int g_tune_unroll = 0;         // 0 = per-shape default
+int g_tune_nt = -1;            // -1 = default (non-temporal on)
+int g_tune_blocks_per_cu = 0;  // 0 = per-shape default
+int g_tune_block = 0;          // 0 = per-shape default
+
+namespace {
+
+// Launch shape chosen from the MI355X sweeps in DESIGN.md ("Tuning"): long
+// per-wave runs (4 x 1 KiB per stream) at one 256-thread block per CU keep
+// the fewest DRAM rows open for a given bytes-in-flight.
+struct Shape {
+    int unroll, block, blocks_per_cu;
+    bool nt;
+};
+
+Shape default_shape(int k) {
+    if (k > 6) return {2, 512, 2, true};  // RS(10,4): 20 x 1 KiB loads in flight per wave already
+    return {4, 256, 1, true};             // RS(3,2), RS(6,3): one wave per SIMD, 4 KiB per stream
 }
 
 }  // namespace
-
-int g_tune_unroll = 1;
-int g_tune_nt = 0;
-int g_tune_blocks_per_cu = 0;  // 0 = occupancy-derived
 
 int launch_gf_matmul(const MatmulArgs& in, int device, hipStream_t stream) {
     MatmulArgs a = in;
@@ -314,26 +372,26 @@ int launch_gf_matmul(const MatmulArgs& in, int device, hipStream_t stream) {
     const int cus = num_cus(device);
 
     if (chunks > 0) {
-        const int unroll = g_tune_unroll == 2 ? 2 : 1;
-        const uint64_t tile = uint64_t(kBlock) * unroll;
+        Shape sh = default_shape(a.k);
+        if (g_tune_unroll) sh.unroll = g_tune_unroll;
+        if (g_tune_block) sh.block = g_tune_block;
+        if (g_tune_nt >= 0) sh.nt = g_tune_nt != 0;
+        if (g_tune_blocks_per_cu) sh.blocks_per_cu = g_tune_blocks_per_cu;
+        if (sh.block == 512 && sh.unroll > 2) sh.unroll = 2;
+        const uint64_t tile = uint64_t(sh.block) * sh.unroll;
         const uint64_t tps = (chunks + tile - 1) / tile;
         const uint64_t total = tps * a.stripes;
         if (chunks > 0xFFFFFFFFull || total > 0xFFFFFFFFull) return -1;
         a.chunks = uint32_t(chunks);
         a.tiles_per_stripe = uint32_t(tps);
         a.total_tiles = uint32_t(total);
-        const void* fn = pick_vec(a.k, a.r, unroll, g_tune_nt != 0);
-        static thread_local const void* last_fn = nullptr;
-        static thread_local int last_occ = 0;
-        if (fn != last_fn) {
-            last_occ = occupancy(fn);
-            last_fn = fn;
-        }
-        const int bpc = g_tune_blocks_per_cu > 0 ? g_tune_blocks_per_cu : last_occ;
-        uint64_t grid = uint64_t(cus) * bpc;
+        const void* fn = sh.nt ? pick_shape<true>(a.k, a.r, sh.unroll, sh.block)
+                               : pick_shape<false>(a.k, a.r, sh.unroll, sh.block);
+        uint64_t grid = uint64_t(cus) * sh.blocks_per_cu;
         if (grid > total) grid = total;
         void* args[] = {&a};
-        if (hipLaunchKernel(fn, dim3(uint32_t(grid)), dim3(kBlock), args, 0, stream) != hipSuccess) return -4;
+        const hipError_t e = hipLaunchKernel(fn, dim3(uint32_t(grid)), dim3(sh.block), args, 0, stream);
+        if (e != hipSuccess) return int(e);
     }
     const uint64_t begin = chunks * 16;
     if (begin < a.cell_len) {
@@ -343,11 +401,12 @@ int launch_gf_matmul(const MatmulArgs& in, int device, hipStream_t stream) {
         const uint64_t cap = uint64_t(cus) * 8;
         if (grid > cap) grid = cap;
         void* args[] = {&a};
-        if (hipLaunchKernel(reinterpret_cast<const void*>(&gf_matmul_bytes), dim3(uint32_t(grid)), dim3(kBlock),
-                            args, 0, stream) != hipSuccess)
-            return -4;
+        const hipError_t e = hipLaunchKernel(reinterpret_cast<const void*>(&gf_matmul_bytes), dim3(uint32_t(grid)),
+                                             dim3(kBlock), args, 0, stream);
+        if (e != hipSuccess) return int(e);
     }
-    return hipGetLastError() == hipSuccess ? 0 : -4;
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : int(e);
 }
 
 }  // namespace hec

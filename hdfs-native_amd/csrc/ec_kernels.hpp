@@ -30,12 +30,13 @@ struct MatmulArgs {
 };
 
 // Launches the multiply for one group of <= kMaxR output rows.  0 on
-// success, -1 invalid sizes, -4 HIP failure.
+// success, -1 invalid sizes, otherwise the (positive) hipError_t.
 int launch_gf_matmul(const MatmulArgs& a, int device, hipStream_t stream);
 
 // Tuning knobs (set through hec_tune_set).
-extern int g_tune_unroll;
-extern int g_tune_nt;
-extern int g_tune_blocks_per_cu;
+extern int g_tune_unroll;         // 0 = default, else 1|2|4
+extern int g_tune_nt;             // -1 = default, else 0|1
+extern int g_tune_blocks_per_cu;  // 0 = default
+extern int g_tune_block;          // 0 = default, else 256|512
 
 }  // namespace hec

@@ -31,7 +31,7 @@ HEC_ERR_SINGULAR = -6
 
 # Every symbol include/hdfs_ec_amd.h declares (checked by tests/test_capi.py).
 EXPORTS = [
-    "hec_strerror", "hec_abi_version", "hec_gen_rs_matrix", "hec_matrix_invert",
+    "hec_strerror", "hec_abi_version", "hec_last_error", "hec_gen_rs_matrix", "hec_matrix_invert",
     "hec_decode_plan", "hec_coder_create", "hec_coder_destroy", "hec_coder_data_units",
     "hec_coder_parity_units", "hec_coder_device", "hec_encode", "hec_decode",
     "hec_encode_device", "hec_decode_device", "hec_gf_matmul_device",
@@ -55,7 +55,24 @@ class DeviceError(HdfsError):
     pass
 
 
+def _share_torch_hip_runtime() -> None:
+    """If PyTorch is installed, import it BEFORE loading the engine.
+
+    torch's wheel bundles its own libamdhip64 and links it by the unversioned
+    name; our .so links libamdhip64.so.7.  Loaded lib-first, the process ends
+    up with two HIP runtimes and whichever initialises first owns the GPU
+    (the other reports "no ROCm-capable device").  Loaded torch-first, our
+    DT_NEEDED libamdhip64.so.7 matches the SONAME of torch's copy and one
+    runtime serves both.  Set HEC_NO_TORCH_PRELOAD=1 to skip."""
+    import importlib.util
+    if os.environ.get("HEC_NO_TORCH_PRELOAD") == "1":
+        return
+    if importlib.util.find_spec("torch") is not None:
+        import torch  # noqa: F401
+
+
 def _load() -> ctypes.CDLL:
+    _share_torch_hip_runtime()
     if not os.path.exists(LIB_PATH):
         raise ImportError(
             f"{LIB_PATH} not built: run `make -C hdfs-native_amd` (or __graft_entry__.build()). "
@@ -67,6 +84,7 @@ def _load() -> ctypes.CDLL:
     sig = {
         "hec_strerror": ([I], ctypes.c_char_p),
         "hec_abi_version": ([], I),
+        "hec_last_error": ([], ctypes.c_char_p),
         "hec_gen_rs_matrix": ([S, S, P], I),
         "hec_matrix_invert": ([P, S], I),
         "hec_decode_plan": ([S, S, P, SP, SP, SP, P], I),
@@ -109,7 +127,7 @@ def _check(rc: int) -> None:
         raise ValueError(msg)
     if rc == HEC_ERR_NO_MEMORY:
         raise MemoryError(msg)
-    raise DeviceError(f"{msg} (status {rc})")
+    raise DeviceError(f"{msg} (status {rc}): {lib.hec_last_error().decode()}")
 
 
 def _pp(addrs: Sequence[int]):

@@ -55,6 +55,8 @@ typedef struct hec_coder hec_coder_t;
 /* Human-readable text for a status code (static storage). */
 const char *hec_strerror(int status);
 int hec_abi_version(void);
+/* Detail of the last failing HIP call made by this thread ("" if none). */
+const char *hec_last_error(void);
 
 /* ---- Field / matrix helpers (host only, no device needed) ------------- */
 
@@ -145,9 +147,10 @@ int hec_encode_host_batch(hec_coder_t *coder, const uint8_t *h_data, uint8_t *h_
                           size_t cell_len, size_t stripes, size_t chunk_stripes);
 
 /* ---- Measurement knobs (not part of the reference interface) ---------- *
- * key 1: 16-B column chunks per lane per tile (1 or 2)
- * key 2: non-temporal global loads/stores (0 or 1)
- * key 3: resident blocks per CU for the grid (0 = occupancy-derived)
+ * key 1: 16-B column chunks per lane per tile (1, 2 or 4; 0 = default)
+ * key 2: non-temporal global loads/stores (0 or 1; -1 = default on)
+ * key 3: resident blocks per CU for the grid (1..16; 0 = default)
+ * key 4: threads per block (256 or 512; 0 = default)
  * Process-wide; affects launches made after the call. */
 int hec_tune_set(int key, int value);
 

@@ -217,7 +217,8 @@ def test_gf_matmul_device_arbitrary_matrix(dev):
             assert np.array_equal(o[s, j], want[j])
 
 
-@pytest.mark.parametrize("knob", [(1, 2), (2, 1), (3, 1), (3, 2)])
+@pytest.mark.parametrize("knob", [((1, 1),), ((1, 2),), ((1, 4),), ((2, 0),), ((3, 2),), ((4, 512), (1, 1)),
+                                  ((4, 512), (1, 2)), ((1, 4), (2, 0), (3, 3))])
 def test_tuning_variants_bit_identical(dev, c_oracle, knob):
     k, m, S, cell = 6, 3, 5, 8192 + 16
     data = batch_data(S, k, cell, first=21)
@@ -225,14 +226,20 @@ def test_tuning_variants_bit_identical(dev, c_oracle, knob):
     d = torch.from_numpy(data).to(dev)
     p = torch.zeros((S, m, cell), dtype=torch.uint8, device=dev)
     try:
-        H.tune_set(*knob)
+        for kv in knob:
+            H.tune_set(*kv)
         H.encode_batch(coder(k, m), d, p)
+        out = torch.zeros_like(d)
+        H.decode_batch(coder(k, m), d, p, [0, 2, 4], out)
         torch.cuda.synchronize()
     finally:
-        H.tune_set(1, 1)
-        H.tune_set(2, 0)
+        H.tune_set(1, 0)
+        H.tune_set(2, -1)
         H.tune_set(3, 0)
+        H.tune_set(4, 0)
     assert np.array_equal(p.cpu().numpy(), want)
+    for i in (0, 2, 4):
+        assert torch.equal(out[:, i], d[:, i])
 
 
 def test_encode_host_batch_pinned(c_oracle):
