@@ -44,13 +44,16 @@ def parse():
     ap.add_argument("--k", type=int, default=6)
     ap.add_argument("--m", type=int, default=3)
     ap.add_argument("--cell", type=int, default=1 << 20)
-    ap.add_argument("--stripes", type=int, default=1024, help="stripes per GPU")
+    ap.add_argument("--stripes", type=int, default=1024, help="stripes per GPU (weak scaling)")
+    ap.add_argument("--global-stripes", type=int, default=0,
+                    help="split this many stripes across the ranks instead (strong scaling)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="also time the oracle stripe-parallel on T threads")
     ap.add_argument("--host-path", action="store_true", help="also measure the pinned H2D+encode+D2H pipeline")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--tune", default="", help="key=value,... passed to hec_tune_set (measurement)")
     ap.add_argument("--encode-only", action="store_true")
+    ap.add_argument("--backend", default="nccl", help="process-group backend (nccl = RCCL; gloo for rehearsals)")
     ap.add_argument("--spinup", type=float, default=0.5, help="untimed seconds of steps before warmup")
     return ap.parse_args()
 
@@ -104,23 +107,35 @@ def main():
     import torch.distributed as dist
 
     import hdfs_native_ec as H
+    from hdfs_native_ec.dist import max_over_ranks, shard_range, sum_over_ranks
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = torch.cuda.device_count()
+    local = local % max(1, ndev)  # rehearsal: several ranks may share one GPU (gloo only)
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     for kv in filter(None, args.tune.split(",")):
         key, val = kv.split("=")
         H.tune_set(int(key), int(val))
 
-    k, m, cell, S = args.k, args.m, args.cell, args.stripes
+    k, m, cell = args.k, args.m, args.cell
+    if args.global_stripes:
+        first, S = shard_range(args.global_stripes, world, rank)
+        scaling = "strong"
+    else:
+        first, S = rank * args.stripes, args.stripes
+        scaling = "weak"
     coder = H.Coder(k, m, local)
     g = torch.Generator(device=dev)
-    g.manual_seed(0x5EED_EC00 + rank)
+    g.manual_seed(0x5EED_EC00 + first)
     data = torch.randint(0, 256, (S, k, cell), dtype=torch.uint8, device=dev, generator=g)
     parity = torch.empty((S, m, cell), dtype=torch.uint8, device=dev)
     rec = torch.empty((S, m, cell), dtype=torch.uint8, device=dev)  # reconstructed data 0..m-1
@@ -173,11 +188,7 @@ def main():
     t1 = time.perf_counter()
     if world > 1:
         dist.barrier()
-    elapsed = t1 - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(t1 - t0, dev)
 
     # correctness gate (after the timed region): decode reconstructs the erased shards and
     # one stripe matches the oracle bit for bit
@@ -194,7 +205,7 @@ def main():
     launch_ms = enc_ms + dec_ms
     avg_launch_ms = sum(launch_ms) / len(launch_ms)
     ops = 1 if args.encode_only else 2
-    bytes_per_step = ops * k * cell * S * world
+    bytes_per_step = sum_over_ranks(float(ops * k * cell * S), dev)
     value = bytes_per_step * args.steps / elapsed / GIB
     algo_bytes = (k + m) * cell * S  # per launch: k inputs read + m outputs written
     achieved = algo_bytes / (avg_launch_ms * 1e-3) / 1e9
@@ -215,15 +226,18 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic: seeded uniform random bytes (torch.randint on device, seed 0x5EED_EC00+rank)",
+        "data": "synthetic: seeded uniform random bytes (torch.randint on device, seed 0x5EED_EC00 + first stripe)",
         "config": {
             "workload": f"RS({k},{m}) {cell >> 10} KiB cells: encode + decode with data shards "
-                        f"{{{','.join(map(str, miss))}}} missing, {S} stripes per GPU"
+                        f"{{{','.join(map(str, miss))}}} missing, "
+                        + (f"{args.global_stripes} stripes split over {world} GPU(s)" if args.global_stripes
+                           else f"{S} stripes per GPU")
                         + (" (encode only)" if args.encode_only else ""),
             "k": k, "m": m, "cell_bytes": cell, "stripes_per_gpu": S,
+            "global_stripes": args.global_stripes or S * world,
             "parallelism": f"stripe-sharded x{world}, no collectives",
         },
         "roofline": {

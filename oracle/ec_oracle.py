@@ -198,6 +198,23 @@ POLICIES = {  # mod.rs:93-144
 }
 
 
+def max_offset(k: int, cell: int, index: int, block_size: int) -> int:
+    """mod.rs:40-60: bytes of block `index` (parity -> as block 0) in a block
+    group holding block_size bytes of file data."""
+    if index >= k:
+        index = 0
+    row = cell * k
+    full_rows = block_size // row
+    remaining = block_size - full_rows * row
+    if remaining < index * cell:
+        last = 0
+    elif remaining > (index + 1) * cell:
+        last = cell
+    else:
+        last = remaining - index * cell
+    return full_rows * cell + last
+
+
 def cell_buffer_encode(k: int, m: int, cells: Sequence[bytes]) -> List[bytes]:
     """block_writer.rs:817-851: pad every buffer to len(buffers[0]) with 0,
     encode, truncate data back, append parity."""

@@ -1,0 +1,89 @@
+"""Multi-rank path on CPU: world_size-2 gloo process groups exercising the
+stripe sharding and max-over-ranks timing used by bench.py (the data path
+itself has no collective; each rank codes its own stripe range)."""
+import hashlib
+import json
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+from hdfs_native_ec.dist import shard_range
+
+torch = pytest.importorskip("torch")
+import torch.distributed as dist  # noqa: E402
+import torch.multiprocessing as mp  # noqa: E402
+
+
+@pytest.mark.parametrize("total", [0, 1, 7, 8, 1024, 2049])
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_shard_range_tiles_batch(total, world):
+    ranges = [shard_range(total, world, r) for r in range(world)]
+    pos = 0
+    for start, count in ranges:
+        assert start == pos
+        pos += count
+    assert pos == total
+    counts = [c for _, c in ranges]
+    assert max(counts) - min(counts) <= 1
+
+
+def test_shard_range_rejects_bad_rank():
+    with pytest.raises(ValueError):
+        shard_range(10, 2, 2)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, total, k, m, cell, out_path, root):
+    sys.path[:0] = [os.path.join(root, "hdfs-native_amd"), os.path.join(root, "oracle")]
+    import ec_oracle as O
+    from hdfs_native_ec.dist import max_over_ranks, shard_range, sum_over_ranks
+    from hdfs_native_ec.synth import batch_data
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        lib = O.load_c_oracle()
+        first, count = shard_range(total, world, rank)
+        data = batch_data(count, k, cell, first=first)
+        digests = []
+        for s in range(count):
+            par = O.c_encode(lib, k, m, list(data[s]))
+            digests.append(hashlib.sha256(b"".join(p.tobytes() for p in par)).hexdigest())
+        gathered = [None] * world
+        dist.all_gather_object(gathered, (first, digests))
+        tmax = max_over_ranks(float(rank + 1))
+        nbytes = sum_over_ranks(float(count * k * cell))
+        dist.barrier()
+        if rank == 0:
+            with open(out_path, "w") as f:
+                json.dump({"gathered": gathered, "tmax": tmax, "bytes": nbytes}, f)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_gloo_sharded_encode_matches_single_process(tmp_path, world):
+    import ec_oracle as O
+    from hdfs_native_ec.synth import batch_data
+    from conftest import ROOT
+    total, k, m, cell = 7, 6, 3, 4096
+    out = tmp_path / "res.json"
+    mp.spawn(_worker, args=(world, _free_port(), total, k, m, cell, str(out), ROOT), nprocs=world, join=True)
+    res = json.loads(out.read_text())
+    assert res["tmax"] == float(world)
+    assert res["bytes"] == float(total * k * cell)
+    lib = O.load_c_oracle()
+    data = batch_data(total, k, cell)
+    want = [hashlib.sha256(b"".join(p.tobytes() for p in O.c_encode(lib, k, m, list(data[s])))).hexdigest()
+            for s in range(total)]
+    got = []
+    for first, digests in sorted(res["gathered"], key=lambda t: t[0]):
+        assert first == len(got)
+        got.extend(digests)
+    assert got == want

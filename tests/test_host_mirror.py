@@ -1,0 +1,42 @@
+"""The C++ host mirror (hdfs-native_amd/csrc/hdfs_ec.hpp) of the reference's
+EcSchema / resolve_ec_policy / CellBuffer / Coder callers, driven by
+tests/cpp/test_host_mirror.cpp."""
+import json
+import os
+import subprocess
+
+import pytest
+
+import ec_oracle as O
+from conftest import PKG_DIR
+
+BIN = os.path.join(PKG_DIR, "build", "test_host_mirror")
+
+
+@pytest.fixture(scope="module")
+def binary():
+    subprocess.check_call(["make", "-s", "-C", PKG_DIR, "tests"])
+    return BIN
+
+
+def test_cpu_side_matches_oracle(binary):
+    out = subprocess.run([binary, "cpu"], capture_output=True, text=True, check=True, timeout=60).stdout
+    rows = [json.loads(l) for l in out.splitlines() if l.startswith("{")]
+    pol = {r["policy"]: r for r in rows if "policy" in r}
+    for pid, (codec, k, m, cell) in O.POLICIES.items():  # mod.rs:93-144
+        assert (pol[pid]["codec"], pol[pid]["k"], pol[pid]["m"], pol[pid]["cell"]) == (codec, k, m, cell)
+    assert "error" in pol[6]
+    assert (pol[99]["codec"], pol[99]["k"], pol[99]["m"], pol[99]["cell"]) == ("rs", 4, 2, 65536)
+    grid = [r["max_offset"] for r in rows if "max_offset" in r]
+    assert len(grid) > 100
+    for index, bs, got in grid:
+        assert got == O.max_offset(3, 16, index, bs), (index, bs)
+    row6 = next(r["rs63_row6"] for r in rows if "rs63_row6" in r)
+    assert row6 == O.gen_rs_matrix(6, 3)[6]
+
+
+@pytest.mark.gpu
+def test_striped_write_faulty_read_roundtrip(binary):
+    r = subprocess.run([binary, "gpu"], capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "ALL OK" in r.stdout
