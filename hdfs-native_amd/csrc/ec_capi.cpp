@@ -462,7 +462,9 @@ int hec_encode_host_batch(hec_coder_t* c, const uint8_t* h_data, uint8_t* h_pari
 // Tuning knobs for the measurement harness (not part of the reference API).
 // A value of 0 (-1 for key 2) restores the per-shape default.
 // key 1 = 16-B column chunks per lane (1|2|4), 2 = non-temporal loads/stores
-// (0|1), 3 = resident blocks per CU, 4 = threads per block (256|512).
+// (0|1), 3 = resident blocks per CU, 4 = threads per block (256|512),
+// 5 = pipeline (1 = register kernel, 2 = LDS-DMA prefetch kernel),
+// 6 = chunk mapping (1 = block slabs, 2 = wave-contiguous runs), 7 = grid size.
 int hec_tune_set(int key, int value) {
     switch (key) {
         case 1:
@@ -477,6 +479,18 @@ int hec_tune_set(int key, int value) {
         case 4:
             if (value != 0 && value != 256 && value != 512) return HEC_ERR_INVALID_ARG;
             hec::g_tune_block = value;
+            return HEC_OK;
+        case 5:
+            if (value < 0 || value > 2) return HEC_ERR_INVALID_ARG;
+            hec::g_tune_pipeline = value;
+            return HEC_OK;
+        case 6:
+            if (value < 0 || value > 2) return HEC_ERR_INVALID_ARG;
+            hec::g_tune_map = value;
+            return HEC_OK;
+        case 7:
+            if (value < 0 || value > 65536) return HEC_ERR_INVALID_ARG;
+            hec::g_tune_grid = value;
             return HEC_OK;
         default: return HEC_ERR_INVALID_ARG;
     }

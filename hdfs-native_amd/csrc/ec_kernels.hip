@@ -131,7 +131,19 @@ __device__ __forceinline__ void prologue(const MatmulArgs& a, int k, PermTable (
 // Vector kernel: 16 B per lane per shard, U column chunks per lane.
 // K = compile-time input count (0 = runtime a.k), R = outputs (1..4).
 // ---------------------------------------------------------------------------
-template <int K, int R, int U, bool NT, int BS>
+// Column of chunk u of this lane within a tile.  MAP 0: chunk u of the
+// block is a contiguous BS-lane slab (a wave's U pieces are BS*16 B apart);
+// MAP 1: each wave owns U*64 contiguous chunks (one 4 KiB run per stream at
+// U=4) and issues a stream's pieces back to back.
+template <int U, int BS, int MAP>
+__device__ __forceinline__ uint32_t chunk_col(uint32_t tile_base, int u, uint32_t tid) {
+    if constexpr (MAP == 0)
+        return tile_base + u * BS + tid;
+    else
+        return tile_base + (tid / 64) * (U * 64) + u * 64 + (tid & 63);
+}
+
+template <int K, int R, int U, bool NT, int BS, int MAP = 0>
 __global__ __launch_bounds__(BS) void gf_matmul_v16(MatmulArgs a) {
     __shared__ PermTable s_tab[R][kMaxK];
     __shared__ uint8_t s_exp[512];
@@ -156,13 +168,25 @@ __global__ __launch_bounds__(BS) void gf_matmul_v16(MatmulArgs a) {
             // before any arithmetic (K*U x 1 KiB in flight per wave).
             u32x4 x[U][K];
             bool live[U];
+            uint64_t offs[U];
 #pragma unroll
             for (int u = 0; u < U; u++) {
-                const uint32_t col = tcol * TILE + u * BS + threadIdx.x;
+                const uint32_t col = chunk_col<U, BS, MAP>(tcol * TILE, u, threadIdx.x);
                 live[u] = col < chunks;
-                const uint64_t off = uint64_t(live[u] ? col : 0) * 16u;
+                offs[u] = uint64_t(live[u] ? col : 0) * 16u;
+            }
+            if constexpr (MAP == 0) {
 #pragma unroll
-                for (int i = 0; i < K; i++) x[u][i] = load16<NT>(a.in[i] + uint64_t(stripe) * a.in_stride[i] + off);
+                for (int u = 0; u < U; u++)
+#pragma unroll
+                    for (int i = 0; i < K; i++)
+                        x[u][i] = load16<NT>(a.in[i] + uint64_t(stripe) * a.in_stride[i] + offs[u]);
+            } else {
+#pragma unroll
+                for (int i = 0; i < K; i++)
+#pragma unroll
+                    for (int u = 0; u < U; u++)
+                        x[u][i] = load16<NT>(a.in[i] + uint64_t(stripe) * a.in_stride[i] + offs[u]);
             }
             __builtin_amdgcn_sched_barrier(0);
             u32x4 acc[U][R];
@@ -201,19 +225,28 @@ __global__ __launch_bounds__(BS) void gf_matmul_v16(MatmulArgs a) {
                 // coefficient's table read (R*K*5 VGPRs) to the top
                 __builtin_amdgcn_sched_barrier(0);
             }
+            if constexpr (MAP == 0) {
 #pragma unroll
-            for (int u = 0; u < U; u++) {
-                if (!live[u]) continue;
-                const uint64_t off = uint64_t(tcol * TILE + u * BS + threadIdx.x) * 16u;
+                for (int u = 0; u < U; u++) {
+                    if (!live[u]) continue;
+#pragma unroll
+                    for (int j = 0; j < R; j++)
+                        store16<NT>(a.out[j] + uint64_t(stripe) * a.out_stride[j] + offs[u], acc[u][j]);
+                }
+            } else {
 #pragma unroll
                 for (int j = 0; j < R; j++)
-                    store16<NT>(a.out[j] + uint64_t(stripe) * a.out_stride[j] + off, acc[u][j]);
+#pragma unroll
+                    for (int u = 0; u < U; u++) {
+                        if (!live[u]) continue;
+                        store16<NT>(a.out[j] + uint64_t(stripe) * a.out_stride[j] + offs[u], acc[u][j]);
+                    }
             }
         } else {
             // Runtime K: one shard at a time, U chunks per lane.
 #pragma unroll
             for (int u = 0; u < U; u++) {
-                const uint32_t col = tcol * TILE + u * BS + threadIdx.x;
+                const uint32_t col = chunk_col<U, BS, MAP>(tcol * TILE, u, threadIdx.x);
                 if (col >= chunks) continue;
                 const uint64_t off = uint64_t(col) * 16u;
                 u32x4 acc[R];
@@ -238,6 +271,142 @@ __global__ __launch_bounds__(BS) void gf_matmul_v16(MatmulArgs a) {
             }
         }
     }
+}
+
+// ---------------------------------------------------------------------------
+// LDS-DMA pipelined vector kernel (compile-time K only).  Each wave streams
+// its part of tile t+1 straight into LDS with global_load_lds_dwordx4 while
+// it computes tile t from registers, so at one wave per SIMD the HBM queue
+// never drains during the GF math.  LDS image per wave: [K][U] pieces of
+// 1 KiB (one wave-instruction each, lane-linear), read back by the SAME wave
+// (ds_read_b128 at lane*16) -- no cross-wave hand-off, no barrier.
+// ---------------------------------------------------------------------------
+template <int K, int R, int U, int BS>
+__global__ __launch_bounds__(BS) void gf_matmul_dma(MatmulArgs a) {
+    static_assert(K > 0, "DMA kernel needs a compile-time input count");
+    constexpr int WAVES = BS / 64;
+    constexpr int PIECE = 1024;  // one wave-instruction: 64 lanes x 16 B
+    // One LDS array for everything (a second __shared__ object next to the
+    // DMA image can make hipcc add vmcnt(0) waits; cdna guide §5 item 4a).
+    constexpr int STAGE = WAVES * K * U * PIECE;
+    constexpr int TAB = R * kMaxK * int(sizeof(PermTable));
+    __shared__ __attribute__((aligned(16))) uint8_t s_mem[STAGE + TAB + 512 + 256 + R * kMaxK];
+    PermTable(*s_tab)[kMaxK] = reinterpret_cast<PermTable(*)[kMaxK]>(s_mem + STAGE);
+    uint8_t* s_exp = s_mem + STAGE + TAB;
+    uint8_t* s_log = s_exp + 512;
+    uint8_t* s_coef = s_log + 256;
+    prologue<R, BS>(a, K, s_tab, s_exp, s_log, s_coef);
+
+    const uint32_t chunks = a.chunks;
+    const uint32_t tps = a.tiles_per_stripe;
+    const uint32_t total = a.total_tiles;
+    constexpr uint32_t TILE = BS * U;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / 64);
+    const int lane = threadIdx.x & 63;
+    uint8_t* stage = s_mem + wave * (K * U * PIECE);
+
+    auto issue = [&](uint32_t tile) {
+        const uint32_t stripe = tile / tps;
+        const uint32_t tcol = tile - stripe * tps;
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            uint32_t col = tcol * TILE + u * BS + wave * 64 + lane;
+            col = col < chunks ? col : chunks - 1;  // dead lanes fetch a valid chunk, never stored
+            const uint64_t off = uint64_t(col) * 16u;
+#pragma unroll
+            for (int i = 0; i < K; i++) {
+                const uint8_t* src = a.in[i] + uint64_t(stripe) * a.in_stride[i] + off;
+                __builtin_amdgcn_global_load_lds(
+                    reinterpret_cast<const void*>(src),
+                    (__attribute__((address_space(3))) void*)(stage + (i * U + u) * PIECE), 16, 0,
+                    2 /* nt */);
+            }
+        }
+    };
+
+    uint32_t tile = blockIdx.x;
+    if (tile < total) issue(tile);
+    bool prev_full = false;  // previous iteration issued exactly R*U stores
+    for (; tile < total; tile += gridDim.x) {
+        // This tile's K*U pieces are the oldest vector-memory ops of the
+        // wave.  After a full tile exactly R*U stores are younger and may
+        // stay in flight; otherwise (first tile, or a partial tile whose
+        // dead-lane stores were skipped) drain everything.
+        if (prev_full)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(R * U) : "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        u32x4 x[U][K];
+#pragma unroll
+        for (int u = 0; u < U; u++)
+#pragma unroll
+            for (int i = 0; i < K; i++)
+                x[u][i] = *reinterpret_cast<const u32x4*>(stage + (i * U + u) * PIECE + lane * 16);
+        // every read of the image has landed in VGPRs before it is refilled
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        const uint32_t next = tile + gridDim.x;
+        if (next < total) issue(next);
+        __builtin_amdgcn_sched_barrier(0);
+
+        const uint32_t stripe = tile / tps;
+        const uint32_t tcol = tile - stripe * tps;
+        u32x4 acc[U][R];
+#pragma unroll
+        for (int u = 0; u < U; u++)
+#pragma unroll
+            for (int j = 0; j < R; j++) acc[u][j] = u32x4{0, 0, 0, 0};
+#pragma unroll
+        for (int i = 0; i < K; i++) {
+            uint32_t toff = uint32_t(i) * uint32_t(sizeof(PermTable));
+            asm volatile("" : "+v"(toff));
+#pragma unroll
+            for (int u = 0; u < U; u++)
+#pragma unroll
+                for (int j = 0; j < R; j++) asm volatile("" : "+v"(acc[u][j]) : "v"(toff));
+            Sel sl[U][4];
+#pragma unroll
+            for (int u = 0; u < U; u++)
+#pragma unroll
+                for (int d = 0; d < 4; d++) sl[u][d] = make_sel(x[u][i][d]);
+#pragma unroll
+            for (int j = 0; j < R; j++) {
+                const PermTable& t =
+                    *reinterpret_cast<const PermTable*>(reinterpret_cast<const char*>(&s_tab[j][0]) + toff);
+                const uint32_t t0lo = t.t0lo, t0hi = t.t0hi, t1lo = t.t1lo, t1hi = t.t1hi, t2 = t.t2;
+#pragma unroll
+                for (int u = 0; u < U; u++)
+#pragma unroll
+                    for (int d = 0; d < 4; d++)
+                        acc[u][j][d] ^= gf_mul4(t0lo, t0hi, t1lo, t1hi, t2, sl[u][d].s0, sl[u][d].s1, sl[u][d].s2);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        // wave-uniform: every lane of every chunk of this wave is live
+        const bool full = __builtin_amdgcn_readfirstlane(
+                              int(tcol * TILE + (U - 1) * BS + wave * 64 + 63 < chunks)) != 0;
+        if (full) {
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const uint64_t off = uint64_t(tcol * TILE + u * BS + threadIdx.x) * 16u;
+#pragma unroll
+                for (int j = 0; j < R; j++)
+                    store16<true>(a.out[j] + uint64_t(stripe) * a.out_stride[j] + off, acc[u][j]);
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const uint32_t col = tcol * TILE + u * BS + threadIdx.x;
+                if (col >= chunks) continue;
+                const uint64_t off = uint64_t(col) * 16u;
+#pragma unroll
+                for (int j = 0; j < R; j++)
+                    store16<true>(a.out[j] + uint64_t(stripe) * a.out_stride[j] + off, acc[u][j]);
+            }
+        }
+        prev_full = full;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // ---------------------------------------------------------------------------
@@ -288,29 +457,29 @@ struct KernelInfo {
     int blocks_per_cu = 0;
 };
 
-template <int K, int R, int U, bool NT, int BS>
+template <int K, int R, int U, bool NT, int BS, int MAP>
 const void* vec_fn() {
-    return reinterpret_cast<const void*>(&gf_matmul_v16<K, R, U, NT, BS>);
+    return reinterpret_cast<const void*>(&gf_matmul_v16<K, R, U, NT, BS, MAP>);
 }
 
-template <int R, int U, bool NT, int BS>
+template <int R, int U, bool NT, int BS, int MAP>
 const void* pick_k(int k) {
     switch (k) {
-        case 2: return vec_fn<2, R, U, NT, BS>();
-        case 3: return vec_fn<3, R, U, NT, BS>();
-        case 6: return vec_fn<6, R, U, NT, BS>();
-        case 10: return vec_fn<10, R, U, NT, BS>();
-        default: return vec_fn<0, R, U, NT, BS>();
+        case 2: return vec_fn<2, R, U, NT, BS, MAP>();
+        case 3: return vec_fn<3, R, U, NT, BS, MAP>();
+        case 6: return vec_fn<6, R, U, NT, BS, MAP>();
+        case 10: return vec_fn<10, R, U, NT, BS, MAP>();
+        default: return vec_fn<0, R, U, NT, BS, MAP>();
     }
 }
 
-template <int U, bool NT, int BS>
+template <int U, bool NT, int BS, int MAP = 0>
 const void* pick_r(int k, int r) {
     switch (r) {
-        case 1: return pick_k<1, U, NT, BS>(k);
-        case 2: return pick_k<2, U, NT, BS>(k);
-        case 3: return pick_k<3, U, NT, BS>(k);
-        default: return pick_k<4, U, NT, BS>(k);
+        case 1: return pick_k<1, U, NT, BS, MAP>(k);
+        case 2: return pick_k<2, U, NT, BS, MAP>(k);
+        case 3: return pick_k<3, U, NT, BS, MAP>(k);
+        default: return pick_k<4, U, NT, BS, MAP>(k);
     }
 }
 
@@ -318,11 +487,47 @@ const void* pick_r(int k, int r) {
 // {(1,256),(2,256),(4,256),(1,512),(2,512)}, each with and without
 // non-temporal access.
 template <bool NT>
-const void* pick_shape(int k, int r, int unroll, int bs) {
+const void* pick_shape(int k, int r, int unroll, int bs, int map) {
     if (bs == 512) return unroll >= 2 ? pick_r<2, NT, 512>(k, r) : pick_r<1, NT, 512>(k, r);
-    if (unroll == 4) return pick_r<4, NT, 256>(k, r);
+    if (unroll == 4) return map ? pick_r<4, NT, 256, 1>(k, r) : pick_r<4, NT, 256>(k, r);
     if (unroll == 2) return pick_r<2, NT, 256>(k, r);
     return pick_r<1, NT, 256>(k, r);
+}
+
+template <int R, int U, int BS>
+const void* dma_pick_k(int k) {
+    switch (k) {
+        case 2: return reinterpret_cast<const void*>(&gf_matmul_dma<2, R, U, BS>);
+        case 3: return reinterpret_cast<const void*>(&gf_matmul_dma<3, R, U, BS>);
+        case 6: return reinterpret_cast<const void*>(&gf_matmul_dma<6, R, U, BS>);
+        default: return nullptr;
+    }
+}
+
+template <int U, int BS>
+const void* dma_pick(int k, int r) {
+    switch (r) {
+        case 1: return dma_pick_k<1, U, BS>(k);
+        case 2: return dma_pick_k<2, U, BS>(k);
+        case 3: return dma_pick_k<3, U, BS>(k);
+        default: return dma_pick_k<4, U, BS>(k);
+    }
+}
+
+// LDS-DMA pipelined kernel: (U, BS) in {(4,256), (2,256), (2,512)} for k <= 6;
+// k = 10 only at (2,256) (10 x 2 x 4 waves x 1 KiB = 80 KiB of LDS).
+const void* pick_dma(int k, int r, int unroll, int bs) {
+    if (k == 10) {
+        switch (r) {
+            case 1: return reinterpret_cast<const void*>(&gf_matmul_dma<10, 1, 2, 256>);
+            case 2: return reinterpret_cast<const void*>(&gf_matmul_dma<10, 2, 2, 256>);
+            case 3: return reinterpret_cast<const void*>(&gf_matmul_dma<10, 3, 2, 256>);
+            default: return reinterpret_cast<const void*>(&gf_matmul_dma<10, 4, 2, 256>);
+        }
+    }
+    if (bs == 512) return dma_pick<2, 512>(k, r);
+    if (unroll == 4) return dma_pick<4, 256>(k, r);
+    return dma_pick<2, 256>(k, r);
 }
 
 int g_num_cus[64] = {0};
@@ -343,6 +548,9 @@ int g_tune_unroll = 0;         // 0 = per-shape default
 int g_tune_nt = -1;            // -1 = default (non-temporal on)
 int g_tune_blocks_per_cu = 0;  // 0 = per-shape default
 int g_tune_block = 0;          // 0 = per-shape default
+int g_tune_pipeline = 0;       // 0 = per-shape default, 1 = register kernel, 2 = LDS-DMA kernel
+int g_tune_map = 0;            // 0 = default, 1 = MAP 0, 2 = MAP 1
+int g_tune_grid = 0;           // 0 = blocks_per_cu * CUs, else absolute block count
 
 namespace {
 
@@ -352,11 +560,13 @@ namespace {
 struct Shape {
     int unroll, block, blocks_per_cu;
     bool nt;
+    bool dma;
+    int map;  // chunk_col mapping (U=4, 256 threads only)
 };
 
 Shape default_shape(int k) {
-    if (k > 6) return {2, 512, 2, true};  // RS(10,4): 20 x 1 KiB loads in flight per wave already
-    return {4, 256, 1, true};             // RS(3,2), RS(6,3): one wave per SIMD, 4 KiB per stream
+    if (k > 6) return {2, 512, 2, true, false, 0};  // RS(10,4): 20 x 1 KiB loads in flight per wave already
+    return {4, 256, 1, true, false, 0};             // RS(3,2), RS(6,3): one wave per SIMD, 4 KiB per stream
 }
 
 }  // namespace
@@ -377,7 +587,22 @@ int launch_gf_matmul(const MatmulArgs& in, int device, hipStream_t stream) {
         if (g_tune_block) sh.block = g_tune_block;
         if (g_tune_nt >= 0) sh.nt = g_tune_nt != 0;
         if (g_tune_blocks_per_cu) sh.blocks_per_cu = g_tune_blocks_per_cu;
+        if (g_tune_pipeline) sh.dma = g_tune_pipeline == 2;
+        if (g_tune_map) sh.map = g_tune_map - 1;
+        if (g_tune_grid) sh.blocks_per_cu = 0;
         if (sh.block == 512 && sh.unroll > 2) sh.unroll = 2;
+        const bool dma_ok = (a.k == 2 || a.k == 3 || a.k == 6 || a.k == 10);
+        if (sh.dma && !dma_ok) sh.dma = false;
+        if (sh.dma) {
+            if (a.k == 10) {
+                sh.unroll = 2;
+                sh.block = 256;
+            } else if (sh.block == 512) {
+                sh.unroll = 2;
+            } else if (sh.unroll < 2) {
+                sh.unroll = 2;
+            }
+        }
         const uint64_t tile = uint64_t(sh.block) * sh.unroll;
         const uint64_t tps = (chunks + tile - 1) / tile;
         const uint64_t total = tps * a.stripes;
@@ -385,9 +610,10 @@ int launch_gf_matmul(const MatmulArgs& in, int device, hipStream_t stream) {
         a.chunks = uint32_t(chunks);
         a.tiles_per_stripe = uint32_t(tps);
         a.total_tiles = uint32_t(total);
-        const void* fn = sh.nt ? pick_shape<true>(a.k, a.r, sh.unroll, sh.block)
-                               : pick_shape<false>(a.k, a.r, sh.unroll, sh.block);
-        uint64_t grid = uint64_t(cus) * sh.blocks_per_cu;
+        const void* fn = sh.dma ? pick_dma(a.k, a.r, sh.unroll, sh.block)
+                                : (sh.nt ? pick_shape<true>(a.k, a.r, sh.unroll, sh.block, sh.map)
+                                         : pick_shape<false>(a.k, a.r, sh.unroll, sh.block, sh.map));
+        uint64_t grid = g_tune_grid ? uint64_t(g_tune_grid) : uint64_t(cus) * sh.blocks_per_cu;
         if (grid > total) grid = total;
         void* args[] = {&a};
         const hipError_t e = hipLaunchKernel(fn, dim3(uint32_t(grid)), dim3(sh.block), args, 0, stream);

@@ -38,5 +38,8 @@ extern int g_tune_unroll;         // 0 = default, else 1|2|4
 extern int g_tune_nt;             // -1 = default, else 0|1
 extern int g_tune_blocks_per_cu;  // 0 = default
 extern int g_tune_block;          // 0 = default, else 256|512
+extern int g_tune_pipeline;       // 0 = default, 1 = register kernel, 2 = LDS-DMA kernel
+extern int g_tune_map;            // 0 = default, 1|2 = chunk mapping 0|1
+extern int g_tune_grid;           // 0 = default, else absolute grid size
 
 }  // namespace hec

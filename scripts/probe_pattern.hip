@@ -185,24 +185,15 @@ int main() {
     const size_t n = bytes / 16;
     const size_t n_copy = S * 9 * cell / 2 / 16;  // 4.5 GiB each way
 
-#define COPYB(U, NL, NS, BS)                                                                                  \
-    for (int g : {1024, 2048, 4096, 8192, 16384}) {                                                              \
-        float ms = time_ms([&] { copyb_k<U, NL, NS, BS><<<g * 256 / BS, BS, 0, s>>>((const u32x4*)din, (u32x4*)dout, n_copy); }, s); \
-        std::printf("copyb U=%d ntl=%d nts=%d bs=%d grid256eq=%d: %.1f GB/s\n", U, NL, NS, BS, g, 2.0 * n_copy * 16 / ms / 1e6); \
+    const uint32_t chunks = cell / 16;
+#define EC(U, NL, NS, O)                                                                                       \
+    for (int g : {256}) {                                                                                      \
+        uint32_t tps = chunks / (256 * U), total = tps * S;                                                    \
+        float ms = time_ms([&] { ec_k<U, NL, NS, O><<<g, 256, 0, s>>>(din, dout, chunks, tps, total, cell); }, s); \
+        std::printf("ec63 U=%d ntl=%d nts=%d order=%d grid=%d: %.1f GB/s\n", U, NL, NS, O, g,                 \
+                    9.0 * cell * S / ms / 1e6);                                                                \
     }
-    COPYB(1, 1, 1, 256) COPYB(2, 1, 1, 256) COPYB(4, 1, 1, 256) COPYB(2, 1, 1, 512) COPYB(2, 1, 1, 1024) COPYB(1, 0, 0, 1024)
-#define COPYR(U, NL, NS)                                                                                       \
-    for (int g : {256, 512, 1024, 2048, 4096}) {                                                               \
-        float ms = time_ms([&] { copyr_k<U, NL, NS><<<g, 256, 0, s>>>((const u32x4*)din, (u32x4*)dout, n_copy); }, s); \
-        std::printf("copyr U=%d ntl=%d nts=%d grid=%d: %.1f GB/s\n", U, NL, NS, g, 2.0 * n_copy * 16 / ms / 1e6); \
-    }
-    COPYR(2, 1, 1) COPYR(4, 1, 1)
-    // in-place style: read and write the SAME addresses (x ^= 1)
-    {
-        for (int g : {1024, 2048, 4096}) {
-            float ms = time_ms([&] { copyb_k<2, true, true, 256><<<g, 256, 0, s>>>((const u32x4*)din, (u32x4*)din, n_copy); }, s);
-            std::printf("inplace U=2 nt grid=%d: %.1f GB/s\n", g, 2.0 * n_copy * 16 / ms / 1e6);
-        }
-    }
+    EC(4, 1, 1, 0) EC(4, 1, 0, 0) EC(4, 0, 1, 0) EC(4, 0, 0, 0) EC(4, 1, 1, 0) EC(4, 1, 0, 0)
+    EC(2, 1, 1, 0) EC(2, 1, 0, 0)
     return 0;
 }

@@ -218,7 +218,9 @@ def test_gf_matmul_device_arbitrary_matrix(dev):
 
 
 @pytest.mark.parametrize("knob", [((1, 1),), ((1, 2),), ((1, 4),), ((2, 0),), ((3, 2),), ((4, 512), (1, 1)),
-                                  ((4, 512), (1, 2)), ((1, 4), (2, 0), (3, 3))])
+                                  ((4, 512), (1, 2)), ((1, 4), (2, 0), (3, 3)), ((5, 2),), ((5, 2), (1, 2)),
+                                  ((5, 2), (4, 512)), ((5, 2), (3, 2)), ((5, 1),), ((6, 2),), ((6, 2), (7, 100)),
+                                  ((7, 3),)])
 def test_tuning_variants_bit_identical(dev, c_oracle, knob):
     k, m, S, cell = 6, 3, 5, 8192 + 16
     data = batch_data(S, k, cell, first=21)
@@ -237,9 +239,39 @@ def test_tuning_variants_bit_identical(dev, c_oracle, knob):
         H.tune_set(2, -1)
         H.tune_set(3, 0)
         H.tune_set(4, 0)
+        H.tune_set(5, 0)
+        H.tune_set(6, 0)
+        H.tune_set(7, 0)
     assert np.array_equal(p.cpu().numpy(), want)
     for i in (0, 2, 4):
         assert torch.equal(out[:, i], d[:, i])
+
+
+@pytest.mark.parametrize("pipeline", [1, 2, 3])
+@pytest.mark.parametrize("k,m", [(2, 1), (3, 2), (6, 3), (10, 4)])
+@pytest.mark.parametrize("cell", [4096, 4096 + 16, 3 * 65536 + 48])
+def test_pipelines_vs_oracle(dev, c_oracle, pipeline, k, m, cell):
+    # register kernel and LDS-DMA kernel, full and partial tiles
+    S = 3
+    data = batch_data(S, k, cell, first=cell + k)
+    want = oracle_batch_encode(c_oracle, k, m, data)
+    d = torch.from_numpy(data).to(dev)
+    p = torch.zeros((S, m, cell), dtype=torch.uint8, device=dev)
+    try:
+        if pipeline == 3:  # register kernel, wave-contiguous chunk mapping
+            H.tune_set(5, 1)
+            H.tune_set(6, 2)
+        else:
+            H.tune_set(5, pipeline)
+        H.encode_batch(coder(k, m), d, p)
+        out = torch.zeros_like(d)
+        H.decode_batch(coder(k, m), d, p, list(range(m)), out)
+        torch.cuda.synchronize()
+    finally:
+        H.tune_set(5, 0)
+        H.tune_set(6, 0)
+    assert np.array_equal(p.cpu().numpy(), want)
+    assert torch.equal(out[:, :m], d[:, :m])
 
 
 def test_encode_host_batch_pinned(c_oracle):
