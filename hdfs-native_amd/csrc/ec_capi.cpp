@@ -464,7 +464,8 @@ int hec_encode_host_batch(hec_coder_t* c, const uint8_t* h_data, uint8_t* h_pari
 // key 1 = 16-B column chunks per lane (1|2|4), 2 = non-temporal loads/stores
 // (0|1), 3 = resident blocks per CU, 4 = threads per block (256|512),
 // 5 = pipeline (1 = register kernel, 2 = LDS-DMA prefetch kernel),
-// 6 = chunk mapping (1 = block slabs, 2 = wave-contiguous runs), 7 = grid size.
+// 6 = chunk mapping (1 = block slabs, 2 = wave-contiguous runs), 7 = grid size,
+// 8 = tile-order group (stripes interleaved column-major; 1 = stripe-major).
 int hec_tune_set(int key, int value) {
     switch (key) {
         case 1:
@@ -491,6 +492,10 @@ int hec_tune_set(int key, int value) {
         case 7:
             if (value < 0 || value > 65536) return HEC_ERR_INVALID_ARG;
             hec::g_tune_grid = value;
+            return HEC_OK;
+        case 8:
+            if (value < 0 || value > 65536) return HEC_ERR_INVALID_ARG;
+            hec::g_tune_group = value;
             return HEC_OK;
         default: return HEC_ERR_INVALID_ARG;
     }

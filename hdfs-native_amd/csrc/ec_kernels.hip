@@ -83,6 +83,28 @@ struct Sel {
     uint32_t s0, s1, s2;
 };
 
+// Tile order: stripes are taken G at a time and, inside a group, tiles go
+// column-major (tile-column c of all G stripes, then c+1), so the blocks in
+// flight together touch G stripes x (grid/G) columns.  G = 1 is plain
+// stripe-major order.
+__device__ __forceinline__ void tile_coords(uint32_t tile, const MatmulArgs& a, uint32_t& stripe, uint32_t& tcol) {
+    const uint32_t tps = a.tiles_per_stripe;
+    const uint32_t G = a.group;
+    if (G <= 1) {
+        stripe = tile / tps;
+        tcol = tile - stripe * tps;
+        return;
+    }
+    const uint32_t per_group = G * tps;
+    const uint32_t g = tile / per_group;
+    const uint32_t r = tile - g * per_group;
+    const uint32_t first = g * G;
+    const uint32_t rem = uint32_t(a.stripes) - first;
+    const uint32_t gs = rem < G ? rem : G;  // last group may be short
+    tcol = r / gs;
+    stripe = first + (r - tcol * gs);
+}
+
 __device__ __forceinline__ Sel make_sel(uint32_t x) {
     Sel s;
     s.s0 = x & 0x07070707u;
@@ -153,13 +175,12 @@ __global__ __launch_bounds__(BS) void gf_matmul_v16(MatmulArgs a) {
     prologue<R, BS>(a, k, s_tab, s_exp, s_log, s_coef);
 
     const uint32_t chunks = a.chunks;  // 16-B chunks per cell
-    const uint32_t tps = a.tiles_per_stripe;
     const uint32_t total = a.total_tiles;
     constexpr uint32_t TILE = BS * U;
 
     for (uint32_t tile = blockIdx.x; tile < total; tile += gridDim.x) {
-        const uint32_t stripe = tile / tps;
-        const uint32_t tcol = tile - stripe * tps;
+        uint32_t stripe, tcol;
+        tile_coords(tile, a, stripe, tcol);
         // Keep the per-coefficient table reads inside the loop (LDS broadcast
         // reads) instead of letting LICM pin R*K*5 VGPRs for the whole kernel.
         asm volatile("" ::: "memory");
@@ -298,7 +319,6 @@ __global__ __launch_bounds__(BS) void gf_matmul_dma(MatmulArgs a) {
     prologue<R, BS>(a, K, s_tab, s_exp, s_log, s_coef);
 
     const uint32_t chunks = a.chunks;
-    const uint32_t tps = a.tiles_per_stripe;
     const uint32_t total = a.total_tiles;
     constexpr uint32_t TILE = BS * U;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / 64);
@@ -306,8 +326,8 @@ __global__ __launch_bounds__(BS) void gf_matmul_dma(MatmulArgs a) {
     uint8_t* stage = s_mem + wave * (K * U * PIECE);
 
     auto issue = [&](uint32_t tile) {
-        const uint32_t stripe = tile / tps;
-        const uint32_t tcol = tile - stripe * tps;
+        uint32_t stripe, tcol;
+        tile_coords(tile, a, stripe, tcol);
 #pragma unroll
         for (int u = 0; u < U; u++) {
             uint32_t col = tcol * TILE + u * BS + wave * 64 + lane;
@@ -349,8 +369,8 @@ __global__ __launch_bounds__(BS) void gf_matmul_dma(MatmulArgs a) {
         if (next < total) issue(next);
         __builtin_amdgcn_sched_barrier(0);
 
-        const uint32_t stripe = tile / tps;
-        const uint32_t tcol = tile - stripe * tps;
+        uint32_t stripe, tcol;
+        tile_coords(tile, a, stripe, tcol);
         u32x4 acc[U][R];
 #pragma unroll
         for (int u = 0; u < U; u++)
@@ -551,6 +571,7 @@ int g_tune_block = 0;          // 0 = per-shape default
 int g_tune_pipeline = 0;       // 0 = per-shape default, 1 = register kernel, 2 = LDS-DMA kernel
 int g_tune_map = 0;            // 0 = default, 1 = MAP 0, 2 = MAP 1
 int g_tune_grid = 0;           // 0 = blocks_per_cu * CUs, else absolute block count
+int g_tune_group = 0;          // 0 = default (1), else stripes per tile-order group
 
 namespace {
 
@@ -564,9 +585,13 @@ struct Shape {
     int map;  // chunk_col mapping (U=4, 256 threads only)
 };
 
-Shape default_shape(int k) {
+Shape default_shape(int k, uint64_t cell_len) {
     if (k > 6) return {2, 512, 2, true, false, 0};  // RS(10,4): 20 x 1 KiB loads in flight per wave already
-    return {4, 256, 1, true, false, 0};             // RS(3,2), RS(6,3): one wave per SIMD, 4 KiB per stream
+    // RS(3,2), RS(6,3): one wave per SIMD, 4 x 1 KiB per stream per wave.
+    // Small cells (many short stripes) gain 2-3 % from the LDS-DMA prefetch;
+    // 1 MiB cells lose ~5 % with it (profiles/r01_probe_dma_pipeline.log).
+    const bool small = cell_len <= (256u << 10);
+    return {4, 256, 1, true, small && (k == 2 || k == 3 || k == 6), 0};
 }
 
 }  // namespace
@@ -582,7 +607,7 @@ int launch_gf_matmul(const MatmulArgs& in, int device, hipStream_t stream) {
     const int cus = num_cus(device);
 
     if (chunks > 0) {
-        Shape sh = default_shape(a.k);
+        Shape sh = default_shape(a.k, a.cell_len);
         if (g_tune_unroll) sh.unroll = g_tune_unroll;
         if (g_tune_block) sh.block = g_tune_block;
         if (g_tune_nt >= 0) sh.nt = g_tune_nt != 0;
@@ -610,6 +635,9 @@ int launch_gf_matmul(const MatmulArgs& in, int device, hipStream_t stream) {
         a.chunks = uint32_t(chunks);
         a.tiles_per_stripe = uint32_t(tps);
         a.total_tiles = uint32_t(total);
+        // 4 stripes column-interleaved: +1-4 % over stripe-major at 1 MiB
+        // cells (profiles/r01_probe_tile_order.log)
+        a.group = g_tune_group > 0 ? uint32_t(g_tune_group) : 4u;
         const void* fn = sh.dma ? pick_dma(a.k, a.r, sh.unroll, sh.block)
                                 : (sh.nt ? pick_shape<true>(a.k, a.r, sh.unroll, sh.block, sh.map)
                                          : pick_shape<false>(a.k, a.r, sh.unroll, sh.block, sh.map));

@@ -27,6 +27,7 @@ struct MatmulArgs {
     uint32_t chunks;              // vec kernel: 16-B chunks per cell
     uint32_t tiles_per_stripe;
     uint32_t total_tiles;
+    uint32_t group;               // tile order: G stripes column-interleaved (1 = stripe-major)
 };
 
 // Launches the multiply for one group of <= kMaxR output rows.  0 on
@@ -41,5 +42,6 @@ extern int g_tune_block;          // 0 = default, else 256|512
 extern int g_tune_pipeline;       // 0 = default, 1 = register kernel, 2 = LDS-DMA kernel
 extern int g_tune_map;            // 0 = default, 1|2 = chunk mapping 0|1
 extern int g_tune_grid;           // 0 = default, else absolute grid size
+extern int g_tune_group;          // 0 = default, else stripes per tile-order group
 
 }  // namespace hec

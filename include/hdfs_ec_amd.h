@@ -154,6 +154,7 @@ int hec_encode_host_batch(hec_coder_t *coder, const uint8_t *h_data, uint8_t *h_
  * key 5: kernel pipeline (1 = register, 2 = LDS-DMA prefetch; 0 = default)
  * key 6: chunk mapping (1 = block slabs, 2 = wave-contiguous runs; 0 = default)
  * key 7: absolute grid size in blocks (0 = default)
+ * key 8: tile order, stripes interleaved per group (1 = stripe-major; 0 = default)
  * Process-wide; affects launches made after the call. */
 int hec_tune_set(int key, int value);
 

@@ -134,12 +134,13 @@ int main(int argc, char** argv) {
         ps[j] = R * pitch;
     }
     const bool quick = pad != 0 || (argc > 6);
-    struct V { int u, bs, bpc, pipe, map, grid; };
-    const V vs[] = {{4, 256, 1, 1, 1, 0}, {4, 256, 1, 1, 1, 0}, {4, 256, 1, 1, 2, 0}, {4, 256, 1, 1, 1, 192},
-                    {4, 256, 1, 1, 2, 192}, {4, 256, 1, 1, 1, 224}, {4, 256, 1, 1, 2, 224}, {4, 256, 1, 1, 1, 128},
-                    {4, 256, 1, 1, 2, 128}, {4, 256, 1, 1, 2, 320}, {4, 256, 1, 1, 2, 384}, {4, 256, 1, 1, 1, 0},
-                    {4, 256, 1, 1, 2, 0}};
+    struct V { int u, bs, bpc, pipe, map, grid, group; };
+    const V vs[] = {{0, 0, 0, 0, 0, 0, 1}, {0, 0, 0, 0, 0, 0, 1}, {0, 0, 0, 0, 0, 0, 2}, {0, 0, 0, 0, 0, 0, 4},
+                    {0, 0, 0, 0, 0, 0, 8}, {0, 0, 0, 0, 0, 0, 16}, {0, 0, 0, 0, 0, 0, 32}, {0, 0, 0, 0, 0, 0, 64},
+                    {0, 0, 0, 0, 0, 0, 256}, {0, 0, 0, 0, 0, 0, 1024}, {0, 0, 0, 2, 0, 0, 1}, {0, 0, 0, 2, 0, 0, 16},
+                    {0, 0, 0, 2, 0, 0, 64}, {0, 0, 0, 0, 0, 0, 1}};
     for (const V& v : vs) {
+        hec_tune_set(8, v.group);
         hec_tune_set(1, v.u);
         hec_tune_set(4, v.bs);
         hec_tune_set(3, v.bpc);
@@ -147,8 +148,8 @@ int main(int argc, char** argv) {
         hec_tune_set(6, v.map);
         hec_tune_set(7, v.grid);
         float ms = time_ms([&] { hec_encode_device(c, dp, ds, pp, ps, cell, S, s); }, reps, s);
-        std::printf("engine pad=%zu pipe=%d map=%d grid=%d u=%d bs=%d bpc=%d: %.1f GB/s (%.3f ms)\n", pad, v.pipe,
-                    v.map, v.grid, v.u, v.bs, v.bpc,
+        std::printf("engine pipe=%d group=%d u=%d bs=%d bpc=%d: %.1f GB/s (%.3f ms)\n", v.pipe, v.group, v.u,
+                    v.bs, v.bpc,
                     algo / (ms * 1e-3) / 1e9, ms);
     }
     hec_coder_destroy(c);
