@@ -73,9 +73,10 @@ struct hec_coder {
     std::unordered_map<uint64_t, DecodePlan> plans;  // key: presence bitmask (k+m <= 48)
 
     std::mutex host_mu;  // serialises the host-buffer API (staging buffers)
-    hipStream_t stream = nullptr;
-    hipStream_t copy_stream[2] = {nullptr, nullptr};
-    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    static constexpr int kSlots = 3;
+    hipStream_t stream = nullptr;                       // compute
+    hipStream_t copy_stream[2] = {nullptr, nullptr};    // [0] H2D, [1] D2H
+    hipEvent_t ev_in[kSlots] = {}, ev_k[kSlots] = {}, ev_out[kSlots] = {};
     uint8_t* dbuf = nullptr;
     size_t dbuf_bytes = 0;
 };
@@ -254,7 +255,11 @@ int hec_coder_create(size_t data_units, size_t parity_units, int device, hec_cod
             HEC_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), HEC_ERR_DEVICE);
             for (int i = 0; i < 2; i++)
                 HEC_HIP(hipStreamCreateWithFlags(&c->copy_stream[i], hipStreamNonBlocking), HEC_ERR_DEVICE);
-            for (int i = 0; i < 4; i++) HEC_HIP(hipEventCreateWithFlags(&c->ev[i], hipEventDisableTiming), HEC_ERR_DEVICE);
+            for (int i = 0; i < hec_coder::kSlots; i++) {
+                HEC_HIP(hipEventCreateWithFlags(&c->ev_in[i], hipEventDisableTiming), HEC_ERR_DEVICE);
+                HEC_HIP(hipEventCreateWithFlags(&c->ev_k[i], hipEventDisableTiming), HEC_ERR_DEVICE);
+                HEC_HIP(hipEventCreateWithFlags(&c->ev_out[i], hipEventDisableTiming), HEC_ERR_DEVICE);
+            }
             return HEC_OK;
         }();
         if (rc != HEC_OK) {
@@ -274,8 +279,9 @@ void hec_coder_destroy(hec_coder_t* c) {
         for (auto s : c->copy_stream)
             if (s) (void)hipStreamSynchronize(s);
         if (c->dbuf) (void)hipFree(c->dbuf);
-        for (auto e : c->ev)
-            if (e) (void)hipEventDestroy(e);
+        for (int i = 0; i < hec_coder::kSlots; i++)
+            for (hipEvent_t e : {c->ev_in[i], c->ev_k[i], c->ev_out[i]})
+                if (e) (void)hipEventDestroy(e);
         for (auto s : c->copy_stream)
             if (s) (void)hipStreamDestroy(s);
         if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -406,9 +412,12 @@ int hec_decode(hec_coder_t* c, const uint8_t* const* shards, size_t shard_len, u
     });
 }
 
-// Pipelined pinned-host batch: chunk q uses device slot q%2; H2D on
-// copy_stream[slot], encode on stream, D2H on copy_stream[slot] after the
-// encode's event; slot reuse waits on the previous D2H through stream order.
+// Pipelined pinned-host batch, 3 device slots and 3 streams:
+//   h2d stream:     [wait kernel(q-3) done: input slot free] H2D(q)  -> ev_in[slot]
+//   compute stream: [wait ev_in[slot], D2H(q-3) done: output slot free] encode(q) -> ev_k[slot]
+//   d2h stream:     [wait ev_k[slot]] D2H(q) -> ev_out[slot]
+// so chunk q+1's H2D, chunk q's encode and chunk q-1's D2H run concurrently
+// (PCIe is full duplex; the SDMA engines serve both directions at once).
 int hec_encode_host_batch(hec_coder_t* c, const uint8_t* h_data, uint8_t* h_parity, size_t cell_len,
                           size_t stripes, size_t chunk_stripes) {
     if (!c || !h_data || !h_parity || cell_len == 0 || chunk_stripes == 0) return HEC_ERR_INVALID_ARG;
@@ -418,23 +427,27 @@ int hec_encode_host_batch(hec_coder_t* c, const uint8_t* h_data, uint8_t* h_pari
         DeviceGuard g(c->device);
         if (!g.ok) return fail(HEC_ERR_DEVICE, "hipSetDevice", hipErrorInvalidDevice);
         const size_t k = c->k, m = c->m;
+        constexpr int kSlots = hec_coder::kSlots;
         chunk_stripes = std::min(chunk_stripes, stripes);
         const size_t in_bytes = chunk_stripes * k * cell_len;
         const size_t out_bytes = chunk_stripes * m * cell_len;
         const size_t slot_bytes = in_bytes + out_bytes;
-        int rc = ensure_dbuf(c, 2 * slot_bytes);
+        int rc = ensure_dbuf(c, kSlots * slot_bytes);
         if (rc != HEC_OK) return rc;
+        hipStream_t h2d = c->copy_stream[0], d2h = c->copy_stream[1];
         const size_t nchunks = (stripes + chunk_stripes - 1) / chunk_stripes;
         for (size_t q = 0; q < nchunks; q++) {
-            const int slot = int(q & 1);
-            hipStream_t cs = c->copy_stream[slot];
+            const int slot = int(q % kSlots);
             uint8_t* din = c->dbuf + slot * slot_bytes;
             uint8_t* dpar = din + in_bytes;
             const size_t s0 = q * chunk_stripes;
             const size_t ns = std::min(chunk_stripes, stripes - s0);
-            HEC_HIP(hipMemcpyAsync(din, h_data + s0 * k * cell_len, ns * k * cell_len, hipMemcpyHostToDevice, cs), HEC_ERR_DEVICE);
-            HEC_HIP(hipEventRecord(c->ev[slot], cs), HEC_ERR_DEVICE);
-            HEC_HIP(hipStreamWaitEvent(c->stream, c->ev[slot], 0), HEC_ERR_DEVICE);
+            if (q >= size_t(kSlots)) HEC_HIP(hipStreamWaitEvent(h2d, c->ev_k[slot], 0), HEC_ERR_DEVICE);
+            HEC_HIP(hipMemcpyAsync(din, h_data + s0 * k * cell_len, ns * k * cell_len, hipMemcpyHostToDevice, h2d),
+                    HEC_ERR_DEVICE);
+            HEC_HIP(hipEventRecord(c->ev_in[slot], h2d), HEC_ERR_DEVICE);
+            HEC_HIP(hipStreamWaitEvent(c->stream, c->ev_in[slot], 0), HEC_ERR_DEVICE);
+            if (q >= size_t(kSlots)) HEC_HIP(hipStreamWaitEvent(c->stream, c->ev_out[slot], 0), HEC_ERR_DEVICE);
             const uint8_t* in[HEC_MAX_DATA_UNITS];
             uint8_t* out[HEC_MAX_PARITY_UNITS];
             size_t ist[HEC_MAX_DATA_UNITS], ost[HEC_MAX_PARITY_UNITS];
@@ -448,13 +461,15 @@ int hec_encode_host_batch(hec_coder_t* c, const uint8_t* h_data, uint8_t* h_pari
             }
             rc = matmul_batch(c->device, c->enc.data() + k * k, m, k, in, ist, out, ost, cell_len, ns, c->stream);
             if (rc != HEC_OK) return rc;
-            HEC_HIP(hipEventRecord(c->ev[2 + slot], c->stream), HEC_ERR_DEVICE);
-            HEC_HIP(hipStreamWaitEvent(cs, c->ev[2 + slot], 0), HEC_ERR_DEVICE);
-            HEC_HIP(hipMemcpyAsync(h_parity + s0 * m * cell_len, dpar, ns * m * cell_len, hipMemcpyDeviceToHost, cs), HEC_ERR_DEVICE);
+            HEC_HIP(hipEventRecord(c->ev_k[slot], c->stream), HEC_ERR_DEVICE);
+            HEC_HIP(hipStreamWaitEvent(d2h, c->ev_k[slot], 0), HEC_ERR_DEVICE);
+            HEC_HIP(hipMemcpyAsync(h_parity + s0 * m * cell_len, dpar, ns * m * cell_len, hipMemcpyDeviceToHost, d2h),
+                    HEC_ERR_DEVICE);
+            HEC_HIP(hipEventRecord(c->ev_out[slot], d2h), HEC_ERR_DEVICE);
         }
-        HEC_HIP(hipStreamSynchronize(c->copy_stream[0]), HEC_ERR_DEVICE);
-        HEC_HIP(hipStreamSynchronize(c->copy_stream[1]), HEC_ERR_DEVICE);
+        HEC_HIP(hipStreamSynchronize(h2d), HEC_ERR_DEVICE);
         HEC_HIP(hipStreamSynchronize(c->stream), HEC_ERR_DEVICE);
+        HEC_HIP(hipStreamSynchronize(d2h), HEC_ERR_DEVICE);
         return HEC_OK;
     });
 }

@@ -141,7 +141,8 @@ int hec_gf_matmul_device(hec_coder_t *coder, const uint8_t *matrix, size_t rows,
 /* ---- Pinned-host pipelined batch (PCIe-inclusive path) ----------------- *
  * Encodes a [stripe][k][cell] host batch into a [stripe][m][cell] host batch,
  * streaming chunks of `chunk_stripes` stripes H2D -> encode -> D2H with
- * copy/compute overlap on the coder's own streams.  Host buffers should be
+ * copy/compute overlap on the coder's own streams (3 device slots; H2D,
+ * compute and D2H of consecutive chunks run concurrently).  Host buffers should be
  * pinned (hipHostMalloc / registered) for full PCIe rate.  Synchronous. */
 int hec_encode_host_batch(hec_coder_t *coder, const uint8_t *h_data, uint8_t *h_parity,
                           size_t cell_len, size_t stripes, size_t chunk_stripes);

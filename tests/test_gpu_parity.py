@@ -275,14 +275,18 @@ def test_pipelines_vs_oracle(dev, c_oracle, pipeline, k, m, cell):
     assert torch.equal(out[:, :m], d[:, :m])
 
 
-def test_encode_host_batch_pinned(c_oracle):
-    k, m, S, cell = 6, 3, 9, 65536
+@pytest.mark.parametrize("S,chunk,cell", [(9, 4, 65536), (23, 2, 65536), (7, 7, 4096 + 16), (5, 1, 1000)])
+def test_encode_host_batch_pinned(c_oracle, S, chunk, cell):
+    # more chunks than device slots, partial last chunk, tails
+    k, m = 6, 3
     data = batch_data(S, k, cell, first=40)
     want = oracle_batch_encode(c_oracle, k, m, data)
     h_in = torch.from_numpy(data).pin_memory()
     h_out = torch.zeros((S, m, cell), dtype=torch.uint8).pin_memory()
-    coder(k, m).encode_host_batch(h_in.data_ptr(), h_out.data_ptr(), cell, S, 4)
-    assert np.array_equal(h_out.numpy(), want)
+    for _ in range(2):  # second pass reuses the slots/events
+        coder(k, m).encode_host_batch(h_in.data_ptr(), h_out.data_ptr(), cell, S, chunk)
+        assert np.array_equal(h_out.numpy(), want)
+        h_out.zero_()
 
 
 # ---- full-size configs (BASELINE.json) via size-independent properties ---
