@@ -53,6 +53,9 @@ def parse():
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--tune", default="", help="key=value,... passed to hec_tune_set (measurement)")
     ap.add_argument("--encode-only", action="store_true")
+    ap.add_argument("--decode-mode", default="uniform", choices=["uniform", "mixed"],
+                    help="uniform: data shards 0..m-1 missing in every stripe; mixed: a random pattern of "
+                         "1..m missing data shards per stripe (hec_decode_device_mixed)")
     ap.add_argument("--backend", default="nccl", help="process-group backend (nccl = RCCL; gloo for rehearsals)")
     ap.add_argument("--spinup", type=float, default=0.5, help="untimed seconds of steps before warmup")
     return ap.parse_args()
@@ -138,23 +141,41 @@ def main():
     g.manual_seed(0x5EED_EC00 + first)
     data = torch.randint(0, 256, (S, k, cell), dtype=torch.uint8, device=dev, generator=g)
     parity = torch.empty((S, m, cell), dtype=torch.uint8, device=dev)
-    rec = torch.empty((S, m, cell), dtype=torch.uint8, device=dev)  # reconstructed data 0..m-1
+    mixed = args.decode_mode == "mixed"
+    # reconstructed data: [S, m, cell] for the uniform worst case (shards
+    # 0..m-1), [S, k, cell] when every stripe has its own pattern
+    rec = torch.empty((S, k if mixed else m, cell), dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
     sp = stream.cuda_stream
 
     dp, ds = H.stripe_layout_ptrs(data, k)
     pp, ps = H.stripe_layout_ptrs(parity, m)
-    rp, rs = H.stripe_layout_ptrs(rec, m)
+    rp, rs = H.stripe_layout_ptrs(rec, k if mixed else m)
     miss = list(range(m))  # worst case: m data shards missing
     shard_ptrs = [None if i in miss else dp[i] for i in range(k)] + pp
     out_ptrs = [rp[i] if i in miss else 0 for i in range(k)]
     out_strides = [rs[0]] * k
+    if mixed:
+        rng = np.random.default_rng(0x5EED_EC00 + first)
+        full = (1 << (k + m)) - 1
+        masks, erased = [], 0
+        for _ in range(S):
+            e = int(rng.integers(1, m + 1))
+            lost = rng.choice(k, size=e, replace=False)
+            masks.append(full & ~sum(1 << int(i) for i in lost))
+            erased += e
+        ws = torch.empty(coder.decode_mixed_workspace_size(S), dtype=torch.uint8, device=dev)
+        mixed_ptrs, mixed_strides = dp + pp, ds + ps
 
     def encode():
         coder.encode_device(dp, ds, pp, ps, cell, S, sp)
 
     def decode():
-        coder.decode_device(shard_ptrs, ds + ps, out_ptrs, out_strides, cell, S, sp)
+        if mixed:
+            coder.decode_device_mixed(mixed_ptrs, mixed_strides, rp, rs, masks, cell, S, ws.data_ptr(), ws.numel(),
+                                      sp)
+        else:
+            coder.decode_device(shard_ptrs, ds + ps, out_ptrs, out_strides, cell, S, sp)
 
     def step(events=None):
         if events is not None:
@@ -192,8 +213,13 @@ def main():
 
     # correctness gate (after the timed region): decode reconstructs the erased shards and
     # one stripe matches the oracle bit for bit
-    if not args.encode_only:
+    if not args.encode_only and not mixed:
         assert torch.equal(rec, data[:, :m]), "decode != original"
+    if not args.encode_only and mixed:
+        for s_ in range(0, S, max(1, S // 8)):
+            for i in range(k):
+                if not (masks[s_] >> i) & 1:
+                    assert torch.equal(rec[s_, i], data[s_, i]), "mixed decode != original"
     import ec_oracle
     clib = ec_oracle.load_c_oracle()
     s0 = data[0].cpu().numpy()
@@ -209,12 +235,17 @@ def main():
     value = bytes_per_step * args.steps / elapsed / GIB
     algo_bytes = (k + m) * cell * S  # per launch: k inputs read + m outputs written
     achieved = algo_bytes / (avg_launch_ms * 1e-3) / 1e9
+    if mixed:  # decode launches move (k + e_s) cells per stripe
+        dec_bytes = (k * S + erased) * cell
+        enc_avg = sum(enc_ms) / len(enc_ms) * 1e-3
+        dec_avg = sum(dec_ms) / len(dec_ms) * 1e-3 if dec_ms else enc_avg
+        achieved = (algo_bytes + dec_bytes) / (enc_avg + dec_avg) / 1e9
 
     traffic = None
     if os.path.exists(args.traffic):
         with open(args.traffic) as f:
             tr = json.load(f)
-        if tr.get("config") == {"k": k, "m": m, "cell": cell, "stripes": S}:
+        if tr.get("config") == {"k": k, "m": m, "cell": cell, "stripes": S} and not mixed:
             traffic = tr.get("hbm_bytes_per_launch")
 
     result = {
@@ -231,14 +262,17 @@ def main():
         "dtype": "u8",
         "data": "synthetic: seeded uniform random bytes (torch.randint on device, seed 0x5EED_EC00 + first stripe)",
         "config": {
-            "workload": f"RS({k},{m}) {cell >> 10} KiB cells: encode + decode with data shards "
-                        f"{{{','.join(map(str, miss))}}} missing, "
+            "workload": f"RS({k},{m}) {cell >> 10} KiB cells: encode + decode with "
+                        + ("data shards " if not mixed else "")
+                        + (f"{{{','.join(map(str, miss))}}} missing, " if not mixed else
+                           f"a random 1..{m} data shards missing per stripe, ")
                         + (f"{args.global_stripes} stripes split over {world} GPU(s)" if args.global_stripes
                            else f"{S} stripes per GPU")
                         + (" (encode only)" if args.encode_only else ""),
             "k": k, "m": m, "cell_bytes": cell, "stripes_per_gpu": S,
             "global_stripes": args.global_stripes or S * world,
             "parallelism": f"stripe-sharded x{world}, no collectives",
+            "decode_mode": args.decode_mode,
         },
         "roofline": {
             "bound": "hbm",

@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <map>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -408,6 +409,194 @@ int hec_decode(hec_coder_t* c, const uint8_t* const* shards, size_t shard_len, u
         for (size_t r = 0; r < e; r++)
             HEC_HIP(hipMemcpyAsync(out[p.missing[r]], dout[r], shard_len, hipMemcpyDeviceToHost, c->stream), HEC_ERR_DEVICE);
         HEC_HIP(hipStreamSynchronize(c->stream), HEC_ERR_DEVICE);
+        return HEC_OK;
+    });
+}
+
+// ---- heterogeneous per-stripe erasure patterns ---------------------------
+
+namespace {
+
+constexpr size_t kAlign = 256;
+inline size_t align_up(size_t v) { return (v + kAlign - 1) & ~(kAlign - 1); }
+
+size_t max_plans(size_t k, size_t m, size_t stripes) {
+    // presence masks with >= 1 missing data shard and >= k present: at most
+    // sum_{j=1..m} C(k+m, j)
+    double total = 0, c = 1;
+    for (size_t j = 1; j <= m; j++) {
+        c = c * double(k + m - j + 1) / double(j);
+        total += c;
+    }
+    return std::min(stripes, size_t(total));
+}
+
+size_t plan_bytes(size_t k, size_t m) {
+    return sizeof(hec::DevPlanHeader) + std::min(k, m) * k * sizeof(hec::PermTable);
+}
+
+size_t mixed_workspace(size_t k, size_t m, size_t stripes) {
+    const size_t p = max_plans(k, m, stripes);
+    return align_up(stripes * sizeof(uint16_t)) + align_up(p * sizeof(uint32_t)) + p * plan_bytes(k, m);
+}
+
+void free_host_buffer(void* p) { delete[] static_cast<uint8_t*>(p); }
+
+}  // namespace
+
+size_t hec_decode_mixed_workspace_size(const hec_coder_t* c, size_t stripes) {
+    if (!c) return 0;
+    return mixed_workspace(c->k, c->m, stripes);
+}
+
+int hec_decode_device_mixed(hec_coder_t* c, const uint8_t* const* d_shards, const size_t* shard_strides,
+                            uint8_t* const* d_out, const size_t* out_strides, const uint64_t* present,
+                            size_t cell_len, size_t stripes, void* d_workspace, size_t workspace_bytes,
+                            void* hip_stream) {
+    if (!c || !d_shards || !shard_strides || !d_out || !out_strides || !present || cell_len == 0)
+        return HEC_ERR_INVALID_ARG;
+    if (stripes == 0) return HEC_OK;
+    if (stripes > 0xFFFFFFFFull) return HEC_ERR_INVALID_ARG;
+    return guarded([&] {
+        const size_t k = c->k, m = c->m, n = k + m;
+        const uint64_t all = n >= 64 ? ~uint64_t(0) : ((uint64_t(1) << n) - 1);
+        // 1. plan per distinct mask (host), fail before launching anything
+        std::map<uint64_t, uint16_t> ids;
+        std::vector<const DecodePlan*> plans;
+        std::vector<uint16_t> stripe_plan(stripes);
+        size_t max_e = 0;
+        for (size_t s = 0; s < stripes; s++) {
+            const uint64_t mask = present[s] & all;
+            auto it = ids.find(mask);
+            if (it == ids.end()) {
+                uint8_t pres[HEC_MAX_DATA_UNITS + HEC_MAX_PARITY_UNITS];
+                for (size_t i = 0; i < n; i++) pres[i] = (mask >> i) & 1;
+                const DecodePlan& p = cached_plan(c, pres);
+                if (p.status != HEC_OK) return p.status;
+                uint16_t id = 0xFFFF;
+                if (!p.missing.empty()) {
+                    if (plans.size() >= 0xFFFF) return HEC_ERR_INVALID_ARG;
+                    id = uint16_t(plans.size());
+                    plans.push_back(&p);
+                    max_e = std::max(max_e, p.missing.size());
+                }
+                it = ids.emplace(mask, id).first;
+            }
+            stripe_plan[s] = it->second;
+        }
+        if (plans.empty()) return HEC_OK;
+        for (const DecodePlan* p : plans)
+            for (size_t i : p->missing)
+                if (!d_out[i]) return HEC_ERR_INVALID_ARG;
+        for (size_t i = 0; i < n; i++)
+            if (!d_shards[i]) return HEC_ERR_INVALID_ARG;  // every shard needs storage (present in some stripe)
+
+        DeviceGuard g(c->device);
+        if (!g.ok) return fail(HEC_ERR_DEVICE, "hipSetDevice", hipErrorInvalidDevice);
+        hipStream_t stream = static_cast<hipStream_t>(hip_stream);
+
+        bool aligned = cell_len % 16 == 0;
+        for (size_t i = 0; i < n; i++)
+            aligned &= ((reinterpret_cast<uintptr_t>(d_shards[i]) | shard_strides[i]) & 15u) == 0;
+        for (size_t i = 0; i < k; i++)
+            aligned &= ((reinterpret_cast<uintptr_t>(d_out[i]) | out_strides[i]) & 15u) == 0;
+        const bool fused = aligned && (k == 2 || k == 3 || k == 6 || k == 10);
+
+        if (!fused) {
+            // Correct for any shape: one uniform-pattern launch per run of
+            // consecutive stripes sharing a plan.
+            size_t s0 = 0;
+            while (s0 < stripes) {
+                size_t s1 = s0 + 1;
+                while (s1 < stripes && stripe_plan[s1] == stripe_plan[s0]) s1++;
+                if (stripe_plan[s0] != 0xFFFF) {
+                    const DecodePlan& p = *plans[stripe_plan[s0]];
+                    const uint8_t* in[HEC_MAX_DATA_UNITS];
+                    size_t ist[HEC_MAX_DATA_UNITS];
+                    uint8_t* out[HEC_MAX_DATA_UNITS];
+                    size_t ost[HEC_MAX_DATA_UNITS];
+                    for (size_t r = 0; r < k; r++) {
+                        in[r] = d_shards[p.survivors[r]] + s0 * shard_strides[p.survivors[r]];
+                        ist[r] = shard_strides[p.survivors[r]];
+                    }
+                    for (size_t r = 0; r < p.missing.size(); r++) {
+                        out[r] = d_out[p.missing[r]] + s0 * out_strides[p.missing[r]];
+                        ost[r] = out_strides[p.missing[r]];
+                    }
+                    const int rc = matmul_batch(c->device, p.matrix.data(), p.missing.size(), k, in, ist, out, ost,
+                                                cell_len, s1 - s0, stream);
+                    if (rc != HEC_OK) return rc;
+                }
+                s0 = s1;
+            }
+            return HEC_OK;
+        }
+
+        // 2. workspace image: stripe_plan | plan_off | plan blobs
+        const size_t need = align_up(stripes * sizeof(uint16_t)) + align_up(plans.size() * sizeof(uint32_t)) +
+                            plans.size() * plan_bytes(k, m);
+        if (!d_workspace || workspace_bytes < need) return HEC_ERR_INVALID_ARG;
+        uint8_t* host = new uint8_t[need]();
+        std::memcpy(host, stripe_plan.data(), stripes * sizeof(uint16_t));
+        const size_t off_pos = align_up(stripes * sizeof(uint16_t));
+        const size_t blob_pos = off_pos + align_up(plans.size() * sizeof(uint32_t));
+        uint32_t* offs = reinterpret_cast<uint32_t*>(host + off_pos);
+        size_t cur = 0;
+        for (size_t pi = 0; pi < plans.size(); pi++) {
+            const DecodePlan& p = *plans[pi];
+            offs[pi] = uint32_t(cur);
+            auto* hdr = reinterpret_cast<hec::DevPlanHeader*>(host + blob_pos + cur);
+            hdr->e = uint32_t(p.missing.size());
+            for (size_t r = 0; r < k; r++) hdr->surv[r] = uint8_t(p.survivors[r]);
+            for (size_t r = 0; r < p.missing.size(); r++) hdr->miss[r] = uint8_t(p.missing[r]);
+            auto* tab = reinterpret_cast<uint32_t*>(host + blob_pos + cur + sizeof(hec::DevPlanHeader));
+            for (size_t r = 0; r < p.missing.size(); r++)
+                for (size_t i = 0; i < k; i++) {
+                    const auto w = hec::perm_table_words(p.matrix[r * k + i]);
+                    std::memcpy(tab + (r * k + i) * 8, w.data(), sizeof(uint32_t) * 8);
+                }
+            cur += sizeof(hec::DevPlanHeader) + p.missing.size() * k * sizeof(hec::PermTable);
+        }
+        const hipError_t ce = hipMemcpyAsync(d_workspace, host, need, hipMemcpyHostToDevice, stream);
+        if (ce != hipSuccess) {
+            delete[] host;
+            (void)hipGetLastError();
+            return fail(HEC_ERR_DEVICE, "hipMemcpyAsync(workspace)", ce);
+        }
+        // the staging image is freed once the copy has run
+        const hipError_t he = hipLaunchHostFunc(stream, free_host_buffer, host);
+        if (he != hipSuccess) {
+            (void)hipStreamSynchronize(stream);
+            delete[] host;
+            (void)hipGetLastError();
+            return fail(HEC_ERR_DEVICE, "hipLaunchHostFunc", he);
+        }
+
+        // 3. one launch per group of <= 4 missing rows
+        hec::MixedArgs a;
+        std::memset(&a, 0, sizeof(a));
+        for (size_t i = 0; i < n; i++) {
+            a.base[i] = d_shards[i];
+            a.stride[i] = shard_strides[i];
+        }
+        for (size_t i = 0; i < k; i++) {
+            a.out[i] = d_out[i];
+            a.out_stride[i] = out_strides[i];
+        }
+        uint8_t* ws = static_cast<uint8_t*>(d_workspace);
+        a.stripe_plan = reinterpret_cast<const uint16_t*>(ws);
+        a.plan_off = reinterpret_cast<const uint32_t*>(ws + off_pos);
+        a.plans = ws + blob_pos;
+        a.blob_bytes = uint32_t(cur);
+        a.k = int32_t(k);
+        a.cell_len = cell_len;
+        a.stripes = stripes;
+        for (size_t r0 = 0; r0 < max_e; r0 += hec::kMaxR) {
+            a.row0 = int32_t(r0);
+            const int rows = int(std::min(max_e - r0, size_t(hec::kMaxR)));
+            const int rc = hec::launch_decode_mixed(a, rows, c->device, stream);
+            if (rc != 0) return to_status(rc);
+        }
         return HEC_OK;
     });
 }

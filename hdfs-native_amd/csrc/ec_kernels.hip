@@ -34,12 +34,9 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 __constant__ GfTables kDevGf = GfTables();
 
-// One coefficient's product tables, 8 dwords (32 B) per entry so that a
+// PermTable (ec_kernels.hpp): 8 dwords (32 B) per coefficient so that a
 // ds_read_b128 + ds_read_b32 pair fetches it (broadcast: all lanes read the
 // same address, so no bank conflicts).
-struct PermTable {
-    uint32_t t0lo, t0hi, t1lo, t1hi, t2, pad0, pad1, pad2;
-};
 
 __device__ __forceinline__ uint8_t lds_gf_mul(const uint8_t* s_exp, const uint8_t* s_log, uint8_t a,
                                               uint8_t b) {
@@ -430,6 +427,144 @@ __global__ __launch_bounds__(BS) void gf_matmul_dma(MatmulArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Mixed-pattern decode: every stripe carries its own erasure pattern (plan
+// index), as a striped read over many block groups does.  Same register
+// kernel shape as gf_matmul_v16; per tile the block looks up the stripe's
+// plan, re-stages its header + coefficient tables into LDS when the plan
+// changes (block-uniform), and gathers the survivors by shard index.
+// ---------------------------------------------------------------------------
+template <int K, int R, int U, int BS, bool RESIDENT>
+__global__ __launch_bounds__(BS) void gf_decode_mixed(MixedArgs a) {
+    static_assert(K > 0, "compile-time k");
+    __shared__ PermTable s_tab[R][K];
+    __shared__ DevPlanHeader s_hdr;
+    // RESIDENT: the whole plan blob (a.blob_bytes) is copied to dynamic LDS
+    // once per block, so per-tile plan switches need no barrier.
+    extern __shared__ __attribute__((aligned(16))) uint8_t s_blob[];
+    if constexpr (RESIDENT) {
+        const uint32_t words = a.blob_bytes / 4;
+        for (uint32_t t = threadIdx.x; t < words; t += BS)
+            reinterpret_cast<uint32_t*>(s_blob)[t] = reinterpret_cast<const uint32_t*>(a.plans)[t];
+        __syncthreads();
+    }
+    const uint32_t chunks = a.chunks;
+    const uint32_t total = a.total_tiles;
+    constexpr uint32_t TILE = BS * U;
+    uint32_t cur_plan = 0xFFFFFFFFu;
+    MatmulArgs dummy;  // tile_coords only reads tiles_per_stripe/group/stripes
+    dummy.tiles_per_stripe = a.tiles_per_stripe;
+    dummy.group = a.group;
+    dummy.stripes = a.stripes;
+
+    // RESIDENT: grouped interleaved order (best DRAM locality).  Otherwise
+    // each block walks a contiguous range of whole stripes, so its plan
+    // changes (and LDS restaging with two barriers) once per stripe, not once
+    // per tile.
+    uint32_t t_begin = blockIdx.x, t_end = total, t_step = gridDim.x;
+    if constexpr (!RESIDENT) {
+        const uint32_t per = (total + gridDim.x - 1) / gridDim.x;
+        t_begin = blockIdx.x * per;
+        t_end = min(total, t_begin + per);
+        t_step = 1;
+        dummy.group = 1;
+    }
+    for (uint32_t tile = t_begin; tile < t_end; tile += t_step) {
+        uint32_t stripe, tcol;
+        tile_coords(tile, dummy, stripe, tcol);
+        const uint32_t p = a.stripe_plan[stripe];
+        if (p == 0xFFFFu) continue;
+        const DevPlanHeader* hdr = &s_hdr;
+        const PermTable* tab_base = &s_tab[0][0];
+        int tab_row0 = 0;  // row of tab_base[0]
+        if constexpr (RESIDENT) {
+            hdr = reinterpret_cast<const DevPlanHeader*>(s_blob + a.plan_off[p]);
+            tab_base = reinterpret_cast<const PermTable*>(s_blob + a.plan_off[p] + sizeof(DevPlanHeader));
+            tab_row0 = a.row0;
+        } else if (p != cur_plan) {  // block-uniform: every thread sees the same tile
+            __syncthreads();
+            const uint8_t* blob = a.plans + a.plan_off[p];
+            const int tid = threadIdx.x;
+            if (tid < 16) reinterpret_cast<uint32_t*>(&s_hdr)[tid] = reinterpret_cast<const uint32_t*>(blob)[tid];
+            const uint32_t e_all = reinterpret_cast<const DevPlanHeader*>(blob)->e;
+            const PermTable* tabs = reinterpret_cast<const PermTable*>(blob + sizeof(DevPlanHeader));
+            for (int t = tid; t < R * K * 8; t += BS) {
+                const int j = t / (K * 8), rem = t - j * (K * 8), i = rem / 8, w = rem - i * 8;
+                const int row = a.row0 + j;
+                reinterpret_cast<uint32_t*>(&s_tab[j][i])[w] =
+                    row < int(e_all) ? reinterpret_cast<const uint32_t*>(&tabs[row * K + i])[w] : 0u;
+            }
+            __syncthreads();
+            cur_plan = p;
+        }
+        const int e_all = int(hdr->e);
+        const int nrows = e_all - a.row0;  // rows of this launch that exist for this plan
+        if (nrows <= 0) continue;
+        asm volatile("" ::: "memory");
+
+        u32x4 x[U][K];
+        bool live[U];
+        uint64_t offs[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint32_t col = tcol * TILE + u * BS + threadIdx.x;
+            live[u] = col < chunks;
+            offs[u] = uint64_t(live[u] ? col : 0) * 16u;
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++)
+#pragma unroll
+            for (int i = 0; i < K; i++) {
+                const int sh = hdr->surv[i];
+                x[u][i] = load16<true>(a.base[sh] + uint64_t(stripe) * a.stride[sh] + offs[u]);
+            }
+        __builtin_amdgcn_sched_barrier(0);
+        u32x4 acc[U][R];
+#pragma unroll
+        for (int u = 0; u < U; u++)
+#pragma unroll
+            for (int j = 0; j < R; j++) acc[u][j] = u32x4{0, 0, 0, 0};
+#pragma unroll
+        for (int i = 0; i < K; i++) {
+            uint32_t toff = uint32_t(i) * uint32_t(sizeof(PermTable));
+            asm volatile("" : "+v"(toff));
+#pragma unroll
+            for (int u = 0; u < U; u++)
+#pragma unroll
+                for (int j = 0; j < R; j++) asm volatile("" : "+v"(acc[u][j]) : "v"(toff));
+            Sel sl[U][4];
+#pragma unroll
+            for (int u = 0; u < U; u++)
+#pragma unroll
+                for (int d = 0; d < 4; d++) sl[u][d] = make_sel(x[u][i][d]);
+#pragma unroll
+            for (int j = 0; j < R; j++) {
+                if (j >= nrows) break;  // block-uniform
+                const PermTable& t = *reinterpret_cast<const PermTable*>(
+                    reinterpret_cast<const char*>(tab_base + (tab_row0 + j) * K) + toff);
+                const uint32_t t0lo = t.t0lo, t0hi = t.t0hi, t1lo = t.t1lo, t1hi = t.t1hi, t2 = t.t2;
+#pragma unroll
+                for (int u = 0; u < U; u++)
+#pragma unroll
+                    for (int d = 0; d < 4; d++)
+                        acc[u][j][d] ^= gf_mul4(t0lo, t0hi, t1lo, t1hi, t2, sl[u][d].s0, sl[u][d].s1, sl[u][d].s2);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int j = 0; j < R; j++) {
+            if (j >= nrows) break;
+            const int mi = hdr->miss[a.row0 + j];
+            uint8_t* ob = a.out[mi] + uint64_t(stripe) * a.out_stride[mi];
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                if (!live[u]) continue;
+                store16<true>(ob + offs[u], acc[u][j]);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Byte kernel: tails and unaligned layouts.  One thread per (stripe, byte) in
 // [a.byte_begin, a.cell_len); LDS log/antilog lookups.
 // ---------------------------------------------------------------------------
@@ -660,6 +795,60 @@ int launch_gf_matmul(const MatmulArgs& in, int device, hipStream_t stream) {
         if (e != hipSuccess) return int(e);
     }
     const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : int(e);
+}
+
+namespace {
+
+template <int K, int R, bool RES>
+const void* mixed_fn() {
+    if constexpr (K > 6)
+        return reinterpret_cast<const void*>(&gf_decode_mixed<K, R, 2, 512, RES>);
+    else
+        return reinterpret_cast<const void*>(&gf_decode_mixed<K, R, 4, 256, RES>);
+}
+
+template <int K>
+const void* mixed_pick_r(int r, bool res) {
+    switch (r) {
+        case 1: return res ? mixed_fn<K, 1, true>() : mixed_fn<K, 1, false>();
+        case 2: return res ? mixed_fn<K, 2, true>() : mixed_fn<K, 2, false>();
+        case 3: return res ? mixed_fn<K, 3, true>() : mixed_fn<K, 3, false>();
+        default: return res ? mixed_fn<K, 4, true>() : mixed_fn<K, 4, false>();
+    }
+}
+
+constexpr uint32_t kResidentBlobMax = 64u << 10;  // LDS budget for resident plans
+
+}  // namespace
+
+int launch_decode_mixed(const MixedArgs& in, int rows, int device, hipStream_t stream) {
+    MixedArgs a = in;
+    if (a.cell_len % 16 != 0 || a.cell_len / 16 > 0xFFFFFFFFull) return -1;
+    const bool res = a.blob_bytes <= kResidentBlobMax && a.blob_bytes % 4 == 0;
+    const void* fn = nullptr;
+    switch (a.k) {
+        case 2: fn = mixed_pick_r<2>(rows, res); break;
+        case 3: fn = mixed_pick_r<3>(rows, res); break;
+        case 6: fn = mixed_pick_r<6>(rows, res); break;
+        case 10: fn = mixed_pick_r<10>(rows, res); break;
+        default: return -1;
+    }
+    const int U = a.k > 6 ? 2 : 4, BS = a.k > 6 ? 512 : 256, bpc = a.k > 6 ? 2 : 1;
+    const uint64_t chunks = a.cell_len / 16;
+    const uint64_t tile = uint64_t(BS) * U;
+    const uint64_t tps = (chunks + tile - 1) / tile;
+    const uint64_t total = tps * a.stripes;
+    if (total > 0xFFFFFFFFull) return -1;
+    if (total == 0) return 0;
+    a.chunks = uint32_t(chunks);
+    a.tiles_per_stripe = uint32_t(tps);
+    a.total_tiles = uint32_t(total);
+    a.group = g_tune_group > 0 ? uint32_t(g_tune_group) : 4u;
+    uint64_t grid = uint64_t(num_cus(device)) * bpc;
+    if (grid > total) grid = total;
+    void* args[] = {&a};
+    const hipError_t e = hipLaunchKernel(fn, dim3(uint32_t(grid)), dim3(BS), args, res ? a.blob_bytes : 0, stream);
     return e == hipSuccess ? 0 : int(e);
 }
 

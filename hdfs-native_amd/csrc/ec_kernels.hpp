@@ -30,6 +30,45 @@ struct MatmulArgs {
     uint32_t group;               // tile order: G stripes column-interleaved (1 = stripe-major)
 };
 
+// One coefficient's v_perm_b32 product tables (see ec_kernels.hip): c*x =
+// perm(t0hi,t0lo,x&7) ^ perm(t1hi,t1lo,(x>>3)&7) ^ perm(t2,t2,x>>6), 32 B.
+struct PermTable {
+    uint32_t t0lo, t0hi, t1lo, t1hi, t2, pad0, pad1, pad2;
+};
+
+// ---- heterogeneous per-stripe erasure patterns ---------------------------
+constexpr int kMaxShards = kMaxK + 16;  // k + m <= 48
+
+// Plan blob entry (device workspace): header, then e x k PermTables.
+struct DevPlanHeader {
+    uint32_t e;              // missing data shards
+    uint8_t surv[kMaxK];     // survivor shard indices (first k present)
+    uint8_t miss[16];        // missing data indices, ascending
+    uint8_t pad[12];
+};
+static_assert(sizeof(DevPlanHeader) == 64, "plan header is 64 B");
+
+struct MixedArgs {
+    const uint8_t* base[kMaxShards];  // all k+m shard bases
+    uint64_t stride[kMaxShards];
+    uint8_t* out[kMaxK];              // reconstructed data shard i -> out[i]
+    uint64_t out_stride[kMaxK];
+    const uint8_t* plans;             // blob: plan p at plans + plan_off[p]
+    uint32_t blob_bytes;              // size of the blob (LDS-resident when <= 64 KiB)
+    const uint32_t* plan_off;
+    const uint16_t* stripe_plan;      // per stripe; 0xFFFF = nothing missing
+    int32_t k;
+    int32_t row0;                     // first missing row handled by this launch
+    uint64_t cell_len;
+    uint64_t stripes;
+    uint32_t chunks, tiles_per_stripe, total_tiles, group;
+};
+
+// Mixed-pattern decode of one group of missing rows row0 .. row0+rows-1
+// (rows <= kMaxR).  Requires k in {2,3,6,10}, 16-B aligned bases/strides
+// and cell_len % 16 == 0.  0 ok, -1 unsupported, >0 hipError_t.
+int launch_decode_mixed(const MixedArgs& a, int rows, int device, hipStream_t stream);
+
 // Launches the multiply for one group of <= kMaxR output rows.  0 on
 // success, -1 invalid sizes, otherwise the (positive) hipError_t.
 int launch_gf_matmul(const MatmulArgs& a, int device, hipStream_t stream);

@@ -81,4 +81,21 @@ inline bool invert(uint8_t* mat, size_t n) {
     return true;
 }
 
+// The 3-3-2 v_perm_b32 product tables for coefficient c (layout of
+// hec::PermTable): words {t0lo, t0hi, t1lo, t1hi, t2, 0, 0, 0}.
+inline std::array<uint32_t, 8> perm_table_words(uint8_t c) {
+    auto pack = [](uint8_t a, uint8_t b, uint8_t d, uint8_t e) {
+        return uint32_t(a) | (uint32_t(b) << 8) | (uint32_t(d) << 16) | (uint32_t(e) << 24);
+    };
+    uint8_t p0[8], p1[8], p2[4];
+    for (int e = 0; e < 8; e++) {
+        p0[e] = gf_mul(c, uint8_t(e));
+        p1[e] = gf_mul(c, uint8_t(e << 3));
+    }
+    for (int e = 0; e < 4; e++) p2[e] = gf_mul(c, uint8_t(e << 6));
+    return {pack(p0[0], p0[1], p0[2], p0[3]), pack(p0[4], p0[5], p0[6], p0[7]),
+            pack(p1[0], p1[1], p1[2], p1[3]), pack(p1[4], p1[5], p1[6], p1[7]),
+            pack(p2[0], p2[1], p2[2], p2[3]), 0u, 0u, 0u};
+}
+
 }  // namespace hec

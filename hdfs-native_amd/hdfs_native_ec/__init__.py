@@ -35,7 +35,8 @@ EXPORTS = [
     "hec_decode_plan", "hec_coder_create", "hec_coder_destroy", "hec_coder_data_units",
     "hec_coder_parity_units", "hec_coder_device", "hec_encode", "hec_decode",
     "hec_encode_device", "hec_decode_device", "hec_gf_matmul_device",
-    "hec_encode_host_batch", "hec_tune_set",
+    "hec_encode_host_batch", "hec_tune_set", "hec_decode_mixed_workspace_size",
+    "hec_decode_device_mixed",
 ]
 
 
@@ -100,6 +101,8 @@ def _load() -> ctypes.CDLL:
         "hec_gf_matmul_device": ([P, P, S, S, PP, SP, PP, SP, S, S, P], I),
         "hec_encode_host_batch": ([P, P, P, S, S, S], I),
         "hec_tune_set": ([I, I], I),
+        "hec_decode_mixed_workspace_size": ([P, S], S),
+        "hec_decode_device_mixed": ([P, PP, SP, PP, SP, ctypes.POINTER(ctypes.c_uint64), S, S, P, S, P], I),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)
@@ -252,6 +255,17 @@ class Coder:
                                      _pp([p or 0 for p in out_ptrs]), _sp(out_strides), cell_len, stripes,
                                      ctypes.c_void_p(stream)))
 
+    def decode_mixed_workspace_size(self, stripes: int) -> int:
+        return lib.hec_decode_mixed_workspace_size(self._h, stripes)
+
+    def decode_device_mixed(self, shard_ptrs, shard_strides, out_ptrs, out_strides, present_masks, cell_len,
+                            stripes, workspace_ptr, workspace_bytes, stream: int = 0) -> None:
+        masks = (ctypes.c_uint64 * stripes)(*present_masks)
+        _check(lib.hec_decode_device_mixed(self._h, _pp(shard_ptrs), _sp(shard_strides), _pp(out_ptrs),
+                                           _sp(out_strides), masks, cell_len, stripes,
+                                           ctypes.c_void_p(workspace_ptr), workspace_bytes,
+                                           ctypes.c_void_p(stream)))
+
     def gf_matmul_device(self, matrix: List[List[int]], in_ptrs, in_strides, out_ptrs, out_strides, cell_len,
                          stripes, stream: int = 0) -> None:
         rows, cols = len(matrix), len(matrix[0])
@@ -282,6 +296,25 @@ def encode_batch(coder: Coder, data, parity, stream=None) -> None:
     dp, ds = stripe_layout_ptrs(data, coder.data_units)
     pp, ps = stripe_layout_ptrs(parity, coder.parity_units)
     coder.encode_device(dp, ds, pp, ps, data.shape[2], data.shape[0], s.cuda_stream)
+
+
+def decode_batch_mixed(coder: Coder, data, parity, present_masks: Sequence[int], out, stream=None,
+                       workspace=None) -> None:
+    """Per-stripe erasure patterns: present_masks[s] bit i = shard i present.
+    Rebuilt data shards land in out [S,k,cell] where missing."""
+    import torch
+    k, m = coder.data_units, coder.parity_units
+    S = data.shape[0]
+    s = stream if stream is not None else torch.cuda.current_stream(data.device)
+    dp, ds = stripe_layout_ptrs(data, k)
+    pp, ps = stripe_layout_ptrs(parity, m)
+    op, os_ = stripe_layout_ptrs(out, k)
+    nbytes = coder.decode_mixed_workspace_size(S)
+    if workspace is None:
+        workspace = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=data.device)
+    coder.decode_device_mixed(dp + pp, ds + ps, op, os_, list(present_masks), data.shape[2], S,
+                              workspace.data_ptr(), workspace.numel(), s.cuda_stream)
+    return workspace
 
 
 def decode_batch(coder: Coder, data, parity, missing: Sequence[int], out, stream=None) -> None:

@@ -130,6 +130,24 @@ int hec_decode_device(hec_coder_t *coder, const uint8_t *const *d_shards, const 
                       uint8_t *const *d_out, const size_t *out_strides, size_t cell_len,
                       size_t stripes, void *hip_stream);
 
+/* Batched Coder::decode where every stripe has its OWN erasure pattern, as a
+ * striped read over many block groups sees (ec/mod.rs:71 decodes row by
+ * row).  d_shards[k+m]/shard_strides[k+m]: storage of every shard index
+ * (never NULL; slots a stripe lacks are not read).  present[stripes] (host):
+ * bit i set = shard i of that stripe is available.  Reconstructed data shard
+ * i of stripe s goes to d_out[i] + s*out_strides[i], only where it is
+ * missing.  One plan per distinct pattern (first-k-present survivors, as
+ * gf256.rs:84-126) is built on the host, cached in the coder and uploaded to
+ * d_workspace (hec_decode_mixed_workspace_size bytes; keep it untouched
+ * until the stream reaches the work).  If any stripe lacks data shards and
+ * has fewer than k present, HEC_ERR_NOT_ENOUGH_SHARDS is returned and
+ * nothing is launched. */
+size_t hec_decode_mixed_workspace_size(const hec_coder_t *coder, size_t stripes);
+int hec_decode_device_mixed(hec_coder_t *coder, const uint8_t *const *d_shards, const size_t *shard_strides,
+                            uint8_t *const *d_out, const size_t *out_strides, const uint64_t *present,
+                            size_t cell_len, size_t stripes, void *d_workspace, size_t workspace_bytes,
+                            void *hip_stream);
+
 /* The raw hot loop, Mul<&[&[u8]]> (matrix.rs:204-231), batched:
  * out[j] = sum_i matrix[j*cols + i] * in[i] for j < rows, i < cols.
  * Any rows >= 1 (launched 4 output rows at a time), 1 <= cols <=

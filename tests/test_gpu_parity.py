@@ -339,3 +339,81 @@ def test_repeatable(dev):
     H.encode_batch(coder(k, m), d, p2)
     torch.cuda.synchronize()
     assert torch.equal(p1, p2)
+
+
+# ---- heterogeneous per-stripe erasure patterns --------
+
+def _random_masks(k, m, S, seed, allow_fail=False):
+    rng = np.random.default_rng(seed)
+    masks = []
+    for s in range(S):
+        n_missing = int(rng.integers(0, m + (2 if allow_fail else 1)))
+        missing = rng.choice(k + m, size=n_missing, replace=False)
+        mask = sum(1 << i for i in range(k + m) if i not in set(missing.tolist()))
+        masks.append(mask)
+    return masks
+
+
+@pytest.mark.parametrize("k,m,cell", [(6, 3, 4096), (6, 3, 65536 + 64), (10, 4, 8192), (3, 2, 4096 + 16),
+                                      (2, 1, 1024), (4, 2, 4096), (6, 3, 1000)])
+def test_device_decode_mixed_patterns(dev, c_oracle, k, m, cell):
+    S = 40
+    data = batch_data(S, k, cell, first=900 + k)
+    par = oracle_batch_encode(c_oracle, k, m, data)
+    masks = _random_masks(k, m, S, seed=k * 31 + cell)
+    masks[0] = (1 << (k + m)) - 1          # nothing missing
+    masks[1] = (1 << k) - 1                # only parity missing: no work
+    masks[2] = ((1 << (k + m)) - 1) & ~((1 << m) - 1)  # worst case: data 0..m-1
+    d = torch.from_numpy(data).to(dev)
+    p = torch.from_numpy(par).to(dev)
+    # scribble over the erased slots so a wrong survivor choice shows up
+    for s, mask in enumerate(masks):
+        for i in range(k + m):
+            if not (mask >> i) & 1:
+                (d[s, i] if i < k else p[s, i - k]).fill_(0xEE)
+    out = torch.full_like(d, 0x5A)
+    H.decode_batch_mixed(coder(k, m), d, p, masks, out)
+    torch.cuda.synchronize()
+    o = out.cpu().numpy()
+    for s, mask in enumerate(masks):
+        for i in range(k):
+            if (mask >> i) & 1:
+                assert (o[s, i] == 0x5A).all(), (s, i)  # untouched
+            else:
+                assert np.array_equal(o[s, i], data[s, i]), (s, i, bin(mask))
+
+
+def test_device_decode_mixed_not_enough_shards_launches_nothing(dev):
+    k, m, S, cell = 6, 3, 4, 4096
+    d = torch.zeros((S, k, cell), dtype=torch.uint8, device=dev)
+    p = torch.zeros((S, m, cell), dtype=torch.uint8, device=dev)
+    full = (1 << 9) - 1
+    masks = [full & ~1, full, full & ~0b1111, full]  # stripe 2 lost 4 shards
+    out = torch.full_like(d, 7)
+    with pytest.raises(H.ErasureCodingError):
+        H.decode_batch_mixed(coder(k, m), d, p, masks, out)
+    torch.cuda.synchronize()
+    assert (out == 7).all()
+
+
+def test_device_decode_mixed_matches_uniform_decode(dev, c_oracle):
+    # same pattern on every stripe == hec_decode_device, at a full-size cell
+    k, m, S, cell = 6, 3, 16, 1 << 20
+    g = torch.Generator(device=dev)
+    g.manual_seed(77)
+    d = torch.randint(0, 256, (S, k, cell), dtype=torch.uint8, device=dev, generator=g)
+    p = torch.empty((S, m, cell), dtype=torch.uint8, device=dev)
+    H.encode_batch(coder(k, m), d, p)
+    full = (1 << 9) - 1
+    masks = [full & ~0b101 & ~(1 << 7)] * S  # data 0,2 and parity 7 missing
+    o1 = torch.zeros_like(d)
+    o2 = torch.zeros_like(d)
+    H.decode_batch_mixed(coder(k, m), d, p, masks, o1)
+    dp, ds = H.stripe_layout_ptrs(d, k)
+    pp, ps = H.stripe_layout_ptrs(p, m)
+    op, os_ = H.stripe_layout_ptrs(o2, k)
+    ptrs = [None, dp[1], None, dp[3], dp[4], dp[5], pp[0], None, pp[2]]
+    coder(k, m).decode_device(ptrs, ds + ps, op, os_, cell, S, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert torch.equal(o1, o2)
+    assert torch.equal(o1[:, 0], d[:, 0]) and torch.equal(o1[:, 2], d[:, 2])
