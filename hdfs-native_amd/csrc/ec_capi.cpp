@@ -16,6 +16,7 @@
 #include <cstdio>
 #include <cstring>
 #include <mutex>
+#include <string>
 #include <new>
 #include <unordered_map>
 #include <vector>
@@ -68,6 +69,7 @@ struct DeviceGuard {
 struct hec_coder {
     size_t k = 0, m = 0;
     int device = 0;
+    bool xor_codec = false;
     std::vector<uint8_t> enc;  // (k+m) x k
 
     std::mutex plan_mu;
@@ -91,7 +93,7 @@ int to_status(int kernel_rc) {
     return fail(HEC_ERR_DEVICE, "kernel launch", hipError_t(kernel_rc));
 }
 
-DecodePlan compute_plan(size_t k, size_t m, const uint8_t* present) {
+DecodePlan compute_plan(size_t k, size_t m, const uint8_t* present, const std::vector<uint8_t>& enc) {
     DecodePlan p;
     std::vector<size_t> valid;
     for (size_t i = 0; i < k + m; i++) {
@@ -106,7 +108,6 @@ DecodePlan compute_plan(size_t k, size_t m, const uint8_t* present) {
         return p;
     }
     p.survivors.assign(valid.begin(), valid.begin() + k);  // first k present, ascending
-    const std::vector<uint8_t> enc = hec::gen_rs_matrix(k, m);
     std::vector<uint8_t> sub(k * k);
     for (size_t r = 0; r < k; r++) std::memcpy(&sub[r * k], &enc[p.survivors[r] * k], k);  // select_rows
     if (!hec::invert(sub.data(), k)) {
@@ -126,7 +127,7 @@ const DecodePlan& cached_plan(hec_coder* c, const uint8_t* present) {
     std::lock_guard<std::mutex> lk(c->plan_mu);
     auto it = c->plans.find(key);
     if (it != c->plans.end()) return it->second;
-    return c->plans.emplace(key, compute_plan(c->k, c->m, present)).first->second;
+    return c->plans.emplace(key, compute_plan(c->k, c->m, present, c->enc)).first->second;
 }
 
 // Runs out[j] = sum_i mat[j*cols+i] * in[i] over a batch, <= 4 rows per launch.
@@ -225,7 +226,7 @@ int hec_decode_plan(size_t data_units, size_t parity_units, const uint8_t* prese
     if (!present || !n_missing || data_units == 0 || parity_units == 0 || data_units + parity_units > 256)
         return HEC_ERR_INVALID_ARG;
     return guarded([&] {
-        DecodePlan p = compute_plan(data_units, parity_units, present);
+        DecodePlan p = compute_plan(data_units, parity_units, present, hec::gen_rs_matrix(data_units, parity_units));
         *n_missing = p.missing.size();
         if (p.status != HEC_OK) return p.status;
         if (survivors) std::copy(p.survivors.begin(), p.survivors.end(), survivors);
@@ -235,12 +236,16 @@ int hec_decode_plan(size_t data_units, size_t parity_units, const uint8_t* prese
     });
 }
 
-int hec_coder_create(size_t data_units, size_t parity_units, int device, hec_coder_t** out) {
+int hec_coder_create_codec(const char* codec, size_t data_units, size_t parity_units, int device,
+                           hec_coder_t** out) {
     if (!out) return HEC_ERR_INVALID_ARG;
     *out = nullptr;
     if (data_units == 0 || data_units > HEC_MAX_DATA_UNITS || parity_units == 0 ||
         parity_units > HEC_MAX_PARITY_UNITS)
         return HEC_ERR_INVALID_ARG;
+    const std::string name = codec ? codec : "rs";
+    if (name != "rs" && name != "xor") return HEC_ERR_UNSUPPORTED_CODEC;  // e.g. "rs-legacy"
+    if (name == "xor" && parity_units != 1) return HEC_ERR_INVALID_ARG;  // XOR-k-1 only
     return guarded([&] {
         int ndev = 0;
         HEC_HIP(hipGetDeviceCount(&ndev), HEC_ERR_DEVICE);
@@ -249,7 +254,8 @@ int hec_coder_create(size_t data_units, size_t parity_units, int device, hec_cod
         c->k = data_units;
         c->m = parity_units;
         c->device = device;
-        c->enc = hec::gen_rs_matrix(data_units, parity_units);
+        c->xor_codec = name == "xor";
+        c->enc = c->xor_codec ? hec::gen_xor_matrix(data_units) : hec::gen_rs_matrix(data_units, parity_units);
         int rc = [&] {
             DeviceGuard g(device);
             if (!g.ok) return fail(HEC_ERR_DEVICE, "hipSetDevice", hipErrorInvalidDevice);
@@ -270,6 +276,10 @@ int hec_coder_create(size_t data_units, size_t parity_units, int device, hec_cod
         *out = c;
         return HEC_OK;
     });
+}
+
+int hec_coder_create(size_t data_units, size_t parity_units, int device, hec_coder_t** out) {
+    return hec_coder_create_codec("rs", data_units, parity_units, device, out);
 }
 
 void hec_coder_destroy(hec_coder_t* c) {
@@ -653,6 +663,86 @@ int hec_encode_host_batch(hec_coder_t* c, const uint8_t* h_data, uint8_t* h_pari
             HEC_HIP(hipEventRecord(c->ev_k[slot], c->stream), HEC_ERR_DEVICE);
             HEC_HIP(hipStreamWaitEvent(d2h, c->ev_k[slot], 0), HEC_ERR_DEVICE);
             HEC_HIP(hipMemcpyAsync(h_parity + s0 * m * cell_len, dpar, ns * m * cell_len, hipMemcpyDeviceToHost, d2h),
+                    HEC_ERR_DEVICE);
+            HEC_HIP(hipEventRecord(c->ev_out[slot], d2h), HEC_ERR_DEVICE);
+        }
+        HEC_HIP(hipStreamSynchronize(h2d), HEC_ERR_DEVICE);
+        HEC_HIP(hipStreamSynchronize(c->stream), HEC_ERR_DEVICE);
+        HEC_HIP(hipStreamSynchronize(d2h), HEC_ERR_DEVICE);
+        return HEC_OK;
+    });
+}
+
+// Pipelined pinned-host decode straight into file order (the reader's
+// ec_decode + cell split + concatenation, ec/mod.rs:62-89 and
+// block_reader.rs:480-554, in one pass).  Slot layout: file region
+// [chunk][k][cell] + parity region [m][chunk][cell].  Present data cells are
+// copied H2D straight into their file-order slots (2D copies), missing ones
+// are written there by the decode kernel, and the file region goes back D2H
+// in one contiguous copy.
+int hec_decode_host_batch(hec_coder_t* c, const uint8_t* const* h_vertical, size_t cell_len, size_t rows,
+                          uint8_t* h_file, size_t chunk_rows) {
+    if (!c || !h_vertical || !h_file || cell_len == 0 || chunk_rows == 0) return HEC_ERR_INVALID_ARG;
+    if (rows == 0) return HEC_OK;
+    return guarded([&] {
+        const size_t k = c->k, m = c->m;
+        uint8_t present[HEC_MAX_DATA_UNITS + HEC_MAX_PARITY_UNITS];
+        for (size_t i = 0; i < k + m; i++) present[i] = h_vertical[i] != nullptr;
+        const DecodePlan& p = cached_plan(c, present);
+        if (p.status != HEC_OK) return p.status;
+        std::lock_guard<std::mutex> lk(c->host_mu);
+        DeviceGuard g(c->device);
+        if (!g.ok) return fail(HEC_ERR_DEVICE, "hipSetDevice", hipErrorInvalidDevice);
+        constexpr int kSlots = hec_coder::kSlots;
+        chunk_rows = std::min(chunk_rows, rows);
+        const size_t file_bytes = chunk_rows * k * cell_len;
+        const size_t par_bytes = chunk_rows * m * cell_len;
+        const size_t slot_bytes = file_bytes + par_bytes;
+        int rc = ensure_dbuf(c, kSlots * slot_bytes);
+        if (rc != HEC_OK) return rc;
+        hipStream_t h2d = c->copy_stream[0], d2h = c->copy_stream[1];
+        const size_t nchunks = (rows + chunk_rows - 1) / chunk_rows;
+        for (size_t q = 0; q < nchunks; q++) {
+            const int slot = int(q % kSlots);
+            uint8_t* dfile = c->dbuf + slot * slot_bytes;
+            uint8_t* dpar = dfile + file_bytes;
+            const size_t r0 = q * chunk_rows;
+            const size_t nr = std::min(chunk_rows, rows - r0);
+            // slot reuse: the D2H of chunk q-3 (which follows its kernel) is done
+            if (q >= size_t(kSlots)) HEC_HIP(hipStreamWaitEvent(h2d, c->ev_out[slot], 0), HEC_ERR_DEVICE);
+            for (size_t i = 0; i < k; i++)
+                if (h_vertical[i])
+                    HEC_HIP(hipMemcpy2DAsync(dfile + i * cell_len, k * cell_len, h_vertical[i] + r0 * cell_len,
+                                             cell_len, cell_len, nr, hipMemcpyHostToDevice, h2d),
+                            HEC_ERR_DEVICE);
+            for (size_t j = 0; j < m; j++)
+                if (h_vertical[k + j] && std::find(p.survivors.begin(), p.survivors.end(), k + j) != p.survivors.end())
+                    HEC_HIP(hipMemcpyAsync(dpar + j * chunk_rows * cell_len, h_vertical[k + j] + r0 * cell_len,
+                                           nr * cell_len, hipMemcpyHostToDevice, h2d),
+                            HEC_ERR_DEVICE);
+            HEC_HIP(hipEventRecord(c->ev_in[slot], h2d), HEC_ERR_DEVICE);
+            HEC_HIP(hipStreamWaitEvent(c->stream, c->ev_in[slot], 0), HEC_ERR_DEVICE);
+            if (!p.missing.empty()) {
+                const uint8_t* in[HEC_MAX_DATA_UNITS];
+                size_t ist[HEC_MAX_DATA_UNITS];
+                uint8_t* out[HEC_MAX_DATA_UNITS];
+                size_t ost[HEC_MAX_DATA_UNITS];
+                for (size_t r = 0; r < k; r++) {
+                    const size_t sh = p.survivors[r];
+                    in[r] = sh < k ? dfile + sh * cell_len : dpar + (sh - k) * chunk_rows * cell_len;
+                    ist[r] = sh < k ? k * cell_len : cell_len;
+                }
+                for (size_t r = 0; r < p.missing.size(); r++) {
+                    out[r] = dfile + p.missing[r] * cell_len;
+                    ost[r] = k * cell_len;
+                }
+                rc = matmul_batch(c->device, p.matrix.data(), p.missing.size(), k, in, ist, out, ost, cell_len, nr,
+                                  c->stream);
+                if (rc != HEC_OK) return rc;
+            }
+            HEC_HIP(hipEventRecord(c->ev_k[slot], c->stream), HEC_ERR_DEVICE);
+            HEC_HIP(hipStreamWaitEvent(d2h, c->ev_k[slot], 0), HEC_ERR_DEVICE);
+            HEC_HIP(hipMemcpyAsync(h_file + r0 * k * cell_len, dfile, nr * k * cell_len, hipMemcpyDeviceToHost, d2h),
                     HEC_ERR_DEVICE);
             HEC_HIP(hipEventRecord(c->ev_out[slot], d2h), HEC_ERR_DEVICE);
         }

@@ -51,6 +51,16 @@ inline std::vector<uint8_t> gen_rs_matrix(size_t k, size_t m) {
     return mat;
 }
 
+// Hadoop's XOR-k-1 codec (XORRawEncoder): identity on top, one all-ones
+// parity row (parity = XOR of the data units).  The reference names the
+// codec (ec/mod.rs:9-11, policy 4 = XOR-2-1) but rejects it on read.
+inline std::vector<uint8_t> gen_xor_matrix(size_t k) {
+    std::vector<uint8_t> mat((k + 1) * k, 0);
+    for (size_t r = 0; r < k; r++) mat[r * k + r] = 1;
+    for (size_t c = 0; c < k; c++) mat[k * k + c] = 1;
+    return mat;
+}
+
 // Matrix::invert (rust/src/ec/matrix.rs:101-162): Gauss-Jordan over GF(2^8)
 // on [M | I].  The inverse is unique, so any pivoting gives the reference's
 // result; we pick the first non-zero pivot below.  Returns false where the

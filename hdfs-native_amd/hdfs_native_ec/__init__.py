@@ -36,7 +36,7 @@ EXPORTS = [
     "hec_coder_parity_units", "hec_coder_device", "hec_encode", "hec_decode",
     "hec_encode_device", "hec_decode_device", "hec_gf_matmul_device",
     "hec_encode_host_batch", "hec_tune_set", "hec_decode_mixed_workspace_size",
-    "hec_decode_device_mixed",
+    "hec_decode_device_mixed", "hec_coder_create_codec", "hec_decode_host_batch",
 ]
 
 
@@ -90,6 +90,7 @@ def _load() -> ctypes.CDLL:
         "hec_matrix_invert": ([P, S], I),
         "hec_decode_plan": ([S, S, P, SP, SP, SP, P], I),
         "hec_coder_create": ([S, S, I, ctypes.POINTER(P)], I),
+        "hec_coder_create_codec": ([ctypes.c_char_p, S, S, I, ctypes.POINTER(P)], I),
         "hec_coder_destroy": ([P], None),
         "hec_coder_data_units": ([P], S),
         "hec_coder_parity_units": ([P], S),
@@ -100,6 +101,7 @@ def _load() -> ctypes.CDLL:
         "hec_decode_device": ([P, PP, SP, PP, SP, S, S, P], I),
         "hec_gf_matmul_device": ([P, P, S, S, PP, SP, PP, SP, S, S, P], I),
         "hec_encode_host_batch": ([P, P, P, S, S, S], I),
+        "hec_decode_host_batch": ([P, PP, S, S, P, S], I),
         "hec_tune_set": ([I, I], I),
         "hec_decode_mixed_workspace_size": ([P, S], S),
         "hec_decode_device_mixed": ([P, PP, SP, PP, SP, ctypes.POINTER(ctypes.c_uint64), S, S, P, S, P], I),
@@ -185,9 +187,10 @@ def _addr(buf) -> int:
 class Coder:
     """Drop-in for hdfs_native::ec::gf256::Coder on one MI355X."""
 
-    def __init__(self, data_units: int, parity_units: int, device: int = 0):
+    def __init__(self, data_units: int, parity_units: int, device: int = 0, codec: str = "rs"):
         h = ctypes.c_void_p()
-        _check(lib.hec_coder_create(data_units, parity_units, device, ctypes.byref(h)))
+        _check(lib.hec_coder_create_codec(codec.encode(), data_units, parity_units, device, ctypes.byref(h)))
+        self.codec = codec
         self._h = h
         self.data_units = data_units
         self.parity_units = parity_units
@@ -272,6 +275,12 @@ class Coder:
         mat = (ctypes.c_uint8 * (rows * cols))(*[v for r in matrix for v in r])
         _check(lib.hec_gf_matmul_device(self._h, mat, rows, cols, _pp(in_ptrs), _sp(in_strides), _pp(out_ptrs),
                                         _sp(out_strides), cell_len, stripes, ctypes.c_void_p(stream)))
+
+    def decode_host_batch(self, vertical_addrs, cell_len: int, rows: int, h_file_addr: int, chunk_rows: int) -> None:
+        """vertical_addrs[k+m]: host addresses of the per-shard vertical
+        buffers (0/None = missing) -> file-order bytes at h_file_addr."""
+        _check(lib.hec_decode_host_batch(self._h, _pp([a or 0 for a in vertical_addrs]), cell_len, rows,
+                                         ctypes.c_void_p(h_file_addr), chunk_rows))
 
     def encode_host_batch(self, h_data_addr: int, h_parity_addr: int, cell_len: int, stripes: int,
                           chunk_stripes: int) -> None:

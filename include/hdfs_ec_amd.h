@@ -84,6 +84,13 @@ int hec_decode_plan(size_t data_units, size_t parity_units, const uint8_t *prese
 /* Creates a coder for RS(data_units, parity_units) on HIP device `device`.
  * 1 <= data_units <= HEC_MAX_DATA_UNITS, 1 <= parity_units <= HEC_MAX_PARITY_UNITS. */
 int hec_coder_create(size_t data_units, size_t parity_units, int device, hec_coder_t **out);
+/* Same with a codec name: "rs" (the default above) or "xor" (Hadoop XOR-k-1:
+ * parity = XOR of the data units; parity_units must be 1).  The reference
+ * names XOR-2-1 (policy 4, ec/mod.rs:119-125) but rejects it on read
+ * (mod.rs:74-78); this engine codes it on the same kernels.  Any other name
+ * (e.g. "rs-legacy") -> HEC_ERR_UNSUPPORTED_CODEC. */
+int hec_coder_create_codec(const char *codec, size_t data_units, size_t parity_units, int device,
+                           hec_coder_t **out);
 void hec_coder_destroy(hec_coder_t *coder);
 size_t hec_coder_data_units(const hec_coder_t *coder);
 size_t hec_coder_parity_units(const hec_coder_t *coder);
@@ -164,6 +171,17 @@ int hec_gf_matmul_device(hec_coder_t *coder, const uint8_t *matrix, size_t rows,
  * pinned (hipHostMalloc / registered) for full PCIe rate.  Synchronous. */
 int hec_encode_host_batch(hec_coder_t *coder, const uint8_t *h_data, uint8_t *h_parity,
                           size_t cell_len, size_t stripes, size_t chunk_stripes);
+
+/* The read side, fused with the cell split (ec/mod.rs:62-89): h_vertical[k+m]
+ * are the per-shard "vertical" buffers a striped reader accumulates (shard i
+ * = its cells of `rows` consecutive rows, rows*cell_len bytes; NULL =
+ * missing).  Writes the k*cell_len*rows file bytes, in file (row) order, to
+ * h_file: present data cells are copied, missing ones reconstructed
+ * (first-k-present survivors).  Same 3-slot pipeline as the encode;
+ * HEC_ERR_NOT_ENOUGH_SHARDS when a data shard is missing and fewer than k
+ * shards are present.  Synchronous. */
+int hec_decode_host_batch(hec_coder_t *coder, const uint8_t *const *h_vertical, size_t cell_len, size_t rows,
+                          uint8_t *h_file, size_t chunk_rows);
 
 /* ---- Measurement knobs (not part of the reference interface) ---------- *
  * key 1: 16-B column chunks per lane per tile (1, 2 or 4; 0 = default)

@@ -76,6 +76,11 @@ def gen_rs_matrix(k: int, m: int) -> List[List[int]]:
     return mat
 
 
+def gen_xor_matrix(k: int) -> List[List[int]]:
+    """Hadoop XOR-k-1 (XORRawEncoder): parity = XOR of the data units."""
+    return [[1 if i == j else 0 for j in range(k)] for i in range(k)] + [[1] * k]
+
+
 def select_rows(mat: List[List[int]], rows) -> List[List[int]]:
     """matrix.rs:74-84 -- HashSet filter: rows come out in ORIGINAL order."""
     keep = set(rows)
@@ -156,7 +161,7 @@ class NotEnoughShards(Exception):
     """HdfsError::ErasureCodingError("Not enough valid shards") (gf256.rs:107-111)."""
 
 
-def decode_plan(k: int, m: int, present: Sequence[bool]):
+def decode_plan(k: int, m: int, present: Sequence[bool], codec: str = "rs"):
     """Returns (survivors, missing_data, decode_matrix) per gf256.rs:84-126."""
     valid, invalid = [], []
     for i, p in enumerate(present):
@@ -169,7 +174,8 @@ def decode_plan(k: int, m: int, present: Sequence[bool]):
     if len(valid) < k:
         raise NotEnoughShards("Not enough valid shards")
     surv = valid[:k]
-    dm = invert(select_rows(gen_rs_matrix(k, m), surv))
+    enc = gen_xor_matrix(k) if codec == "xor" else gen_rs_matrix(k, m)
+    dm = invert(select_rows(enc, surv))
     dm = select_rows(dm, invalid)
     return surv, invalid, dm
 

@@ -94,3 +94,10 @@ def test_coder_create_without_device_is_clean_error():
     h = ctypes.c_void_p()
     assert H.lib.hec_coder_create(6, 3, 0, ctypes.byref(h)) == H.HEC_ERR_DEVICE
     assert not h.value
+
+
+def test_codec_names_validated():
+    h = ctypes.c_void_p()
+    assert H.lib.hec_coder_create_codec(b"rs-legacy", 6, 3, 0, ctypes.byref(h)) == H.HEC_ERR_UNSUPPORTED_CODEC
+    assert H.lib.hec_coder_create_codec(b"xor", 2, 2, 0, ctypes.byref(h)) == H.HEC_ERR_INVALID_ARG
+    assert not h.value

@@ -417,3 +417,84 @@ def test_device_decode_mixed_matches_uniform_decode(dev, c_oracle):
     torch.cuda.synchronize()
     assert torch.equal(o1, o2)
     assert torch.equal(o1[:, 0], d[:, 0]) and torch.equal(o1[:, 2], d[:, 2])
+
+
+# ---- XOR-k-1 codec ------------------------------------
+
+@pytest.mark.parametrize("k", [2, 3, 6])
+def test_xor_codec_encode_decode(dev, k):
+    cell, S = 4096 + 16, 5
+    c = H.Coder(k, 1, 0, codec="xor")
+    data = batch_data(S, k, cell, first=5000 + k)
+    d = torch.from_numpy(data).to(dev)
+    p = torch.zeros((S, 1, cell), dtype=torch.uint8, device=dev)
+    H.encode_batch(c, d, p)
+    torch.cuda.synchronize()
+    want = np.bitwise_xor.reduce(data, axis=1)
+    assert np.array_equal(p[:, 0].cpu().numpy(), want)
+    for lost in range(k):
+        out = torch.zeros_like(d)
+        H.decode_batch(c, d, p, [lost], out)
+        torch.cuda.synchronize()
+        assert torch.equal(out[:, lost], d[:, lost])
+    # host API too
+    shards = [bytes(x) for x in data[0]] + [want[0].tobytes()]
+    shards[1] = None
+    c.decode(shards)
+    assert shards[1] == data[0, 1].tobytes()
+    c.close()
+
+
+# ---- fused striping: vertical shard buffers -> file-order rows (§8f row 2) -
+
+@pytest.mark.parametrize("k,m,lost", [(6, 3, (0, 1, 2)), (6, 3, (4, 7)), (3, 2, ()), (10, 4, (1, 5, 9, 12)),
+                                      (3, 2, (2, 3))])
+@pytest.mark.parametrize("rows,chunk,cell", [(7, 2, 65536), (5, 5, 4096 + 16), (9, 4, 1000)])
+def test_decode_host_batch_file_order(c_oracle, k, m, lost, rows, chunk, cell):
+    # file bytes striped into rows of k cells (CellBuffer::write), parity per
+    # row, then the reader's vertical buffers: shard i = its cells in row order
+    file = splitmix64_bytes(rows * 1000 + k, rows * k * cell)
+    data = file.reshape(rows, k, cell)
+    par = oracle_batch_encode(c_oracle, k, m, data)
+    vertical = [np.ascontiguousarray(data[:, i, :]).ravel() for i in range(k)] + \
+               [np.ascontiguousarray(par[:, j, :]).ravel() for j in range(m)]
+    hv = [None if i in lost else torch.from_numpy(vertical[i]).pin_memory() for i in range(k + m)]
+    out = torch.zeros(rows * k * cell, dtype=torch.uint8).pin_memory()
+    coder(k, m).decode_host_batch([None if t is None else t.data_ptr() for t in hv], cell, rows, out.data_ptr(),
+                                  chunk)
+    assert np.array_equal(out.numpy(), file)
+
+
+def test_decode_host_batch_too_many_losses():
+    k, m, cell, rows = 6, 3, 4096, 2
+    hv = [torch.zeros(rows * cell, dtype=torch.uint8).pin_memory() for _ in range(k + m)]
+    ptrs = [t.data_ptr() for t in hv]
+    for i in (0, 1, 2, 3):
+        ptrs[i] = None
+    out = torch.zeros(rows * k * cell, dtype=torch.uint8).pin_memory()
+    with pytest.raises(H.ErasureCodingError):
+        coder(k, m).decode_host_batch(ptrs, cell, rows, out.data_ptr(), 1)
+
+
+@pytest.mark.parametrize("k,m", [(6, 3), (10, 4)])
+def test_device_vertical_in_file_order_out(dev, c_oracle, k, m):
+    # device API strides express the reader's layout directly: shard-major
+    # vertical inputs, row-major (file order) outputs
+    rows, cell = 6, 8192
+    file = splitmix64_bytes(7 + k, rows * k * cell)
+    data = file.reshape(rows, k, cell)
+    par = oracle_batch_encode(c_oracle, k, m, data)
+    vert_d = torch.from_numpy(np.ascontiguousarray(data.transpose(1, 0, 2))).to(dev)  # [k][rows][cell]
+    vert_p = torch.from_numpy(np.ascontiguousarray(par.transpose(1, 0, 2))).to(dev)  # [m][rows][cell]
+    out = torch.zeros(rows * k * cell, dtype=torch.uint8, device=dev)
+    miss = set(range(m))
+    shard_ptrs = [None if i in miss else vert_d[i].data_ptr() for i in range(k)] + \
+                 [vert_p[j].data_ptr() for j in range(m)]
+    strides = [cell] * (k + m)
+    out_ptrs = [out.data_ptr() + i * cell for i in range(k)]
+    coder(k, m).decode_device(shard_ptrs, strides, out_ptrs, [k * cell] * k, cell, rows,
+                              torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    o = out.cpu().numpy().reshape(rows, k, cell)
+    for i in range(m):
+        assert np.array_equal(o[:, i], data[:, i])

@@ -178,3 +178,17 @@ def test_cell_buffer_and_ec_decode_semantics():
     assert cells_back[2] == b"\0" * 8
     with pytest.raises(NotImplementedError):
         O.ec_decode(2, 1, cell, "xor", [None, b"\0" * 8, b"\0" * 8])
+
+
+def test_xor_codec_oracle():
+    # Hadoop XOR-2-1: parity = d0 ^ d1; any single loss is the XOR of the rest
+    k = 2
+    data = [np.array([1, 2, 250], dtype=np.uint8), np.array([7, 9, 5], dtype=np.uint8)]
+    par = O.matmul_shards(O.gen_xor_matrix(k)[k:], data)[0]
+    assert par.tolist() == [1 ^ 7, 2 ^ 9, 250 ^ 5]
+    for lost in range(k):
+        present = [i != lost for i in range(k + 1)]
+        surv, miss, dm = O.decode_plan(k, 1, present, codec="xor")
+        shards = data + [par]
+        rec = O.matmul_shards(dm, [shards[i] for i in surv])[0]
+        assert np.array_equal(rec, data[lost])
