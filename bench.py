@@ -56,6 +56,8 @@ def parse():
     ap.add_argument("--decode-mode", default="uniform", choices=["uniform", "mixed"],
                     help="uniform: data shards 0..m-1 missing in every stripe; mixed: a random pattern of "
                          "1..m missing data shards per stripe (hec_decode_device_mixed)")
+    ap.add_argument("--crc", action="store_true",
+                    help="also time encode + CRC32C per 512-B chunk of all k+m cells (hec_encode_crc_device)")
     ap.add_argument("--backend", default="nccl", help="process-group backend (nccl = RCCL; gloo for rehearsals)")
     ap.add_argument("--spinup", type=float, default=0.5, help="untimed seconds of steps before warmup")
     return ap.parse_args()
@@ -290,6 +292,46 @@ def main():
         "decode_GiBps": round(k * cell * S / (sum(dec_ms) / len(dec_ms) * 1e-3) / GIB, 2) if dec_ms else None,
         "parity_check": "ok",
     }
+
+    if args.crc:
+        bpc = 512
+        nch = (cell + bpc - 1) // bpc
+        sums = torch.empty((S, k + m, nch, 4), dtype=torch.uint8, device=dev)
+        cells_ptrs, cells_strides = dp + pp, ds + ps
+
+        def enc_crc():
+            coder.encode_crc_device(dp, ds, pp, ps, cell, S, bpc, sums.data_ptr(), sp)
+
+        def crc_only():
+            coder.crc32c_device(cells_ptrs, cells_strides, cell, S, bpc, sums.data_ptr(), sp)
+
+        for fn in (enc_crc, crc_only):
+            fn()
+        torch.cuda.synchronize(dev)
+        reps = max(3, args.steps // 2)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        ev[0].record(stream)
+        for _ in range(reps):
+            enc_crc()
+        ev[1].record(stream)
+        for _ in range(reps):
+            crc_only()
+        ev[2].record(stream)
+        torch.cuda.synchronize(dev)
+        t_ec = ev[0].elapsed_time(ev[1]) / reps * 1e-3
+        t_c = ev[1].elapsed_time(ev[2]) / reps * 1e-3
+        # spot-check one stripe's sums against the oracle
+        s0_cells = torch.cat([data[0], parity[0]]).cpu().numpy()
+        want = b"".join(ec_oracle.chunk_crc32c(s0_cells[i].tobytes(), bpc) for i in range(k + m))
+        assert sums[0].cpu().numpy().tobytes() == want, "crc32c != oracle"
+        result["crc32c"] = {
+            "bytes_per_checksum": bpc,
+            "encode_crc_GiBps": round(k * cell * S / t_ec / GIB, 2),
+            "crc_only_GBps": round((k + m) * cell * S / t_c / 1e9, 1),
+            "crc_only_ms": round(t_c * 1e3, 3),
+            "encode_crc_ms": round(t_ec * 1e3, 3),
+            "note": "CRC32C of all k+m cells per 512-B chunk (WritePacket::calculate_checksum), big-endian",
+        }
 
     if args.host_path and rank == 0:
         hs = min(S, 256)

@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "../../include/hdfs_ec_amd.h"
+#include "crc32c.hpp"
 #include "ec_kernels.hpp"
 #include "gf256.hpp"
 
@@ -751,6 +752,54 @@ int hec_decode_host_batch(hec_coder_t* c, const uint8_t* const* h_vertical, size
         HEC_HIP(hipStreamSynchronize(d2h), HEC_ERR_DEVICE);
         return HEC_OK;
     });
+}
+
+// ---- CRC32C per checksum chunk -------------------------
+
+int hec_crc32c_device(hec_coder_t* c, const uint8_t* const* d_bases, const size_t* strides, size_t n_shards,
+                      size_t cell_len, size_t stripes, size_t bytes_per_checksum, uint8_t* d_out, void* hip_stream) {
+    if (!c || !d_bases || !strides || !d_out || n_shards == 0 || n_shards > size_t(hec::kCrcMaxShards) ||
+        cell_len == 0 || bytes_per_checksum == 0)
+        return HEC_ERR_INVALID_ARG;
+    for (size_t i = 0; i < n_shards; i++)
+        if (!d_bases[i]) return HEC_ERR_INVALID_ARG;
+    if (stripes == 0) return HEC_OK;
+    return guarded([&] {
+        DeviceGuard g(c->device);
+        if (!g.ok) return fail(HEC_ERR_DEVICE, "hipSetDevice", hipErrorInvalidDevice);
+        hec::CrcArgs a;
+        std::memset(&a, 0, sizeof(a));
+        for (size_t i = 0; i < n_shards; i++) {
+            a.base[i] = d_bases[i];
+            a.stride[i] = strides[i];
+        }
+        a.out = d_out;
+        a.n_shards = uint32_t(n_shards);
+        a.cell_len = cell_len;
+        a.stripes = stripes;
+        a.bytes_per_checksum = bytes_per_checksum;
+        const int rc = hec::launch_crc32c(a, c->device, static_cast<hipStream_t>(hip_stream));
+        return rc == 0 ? HEC_OK : to_status(rc);
+    });
+}
+
+int hec_encode_crc_device(hec_coder_t* c, const uint8_t* const* d_data, const size_t* data_strides,
+                          uint8_t* const* d_parity, const size_t* parity_strides, size_t cell_len, size_t stripes,
+                          size_t bytes_per_checksum, uint8_t* d_sums, void* hip_stream) {
+    if (!c || !d_data || !data_strides || !d_parity || !parity_strides || !d_sums) return HEC_ERR_INVALID_ARG;
+    int rc = hec_encode_device(c, d_data, data_strides, d_parity, parity_strides, cell_len, stripes, hip_stream);
+    if (rc != HEC_OK) return rc;
+    const uint8_t* bases[HEC_MAX_DATA_UNITS + HEC_MAX_PARITY_UNITS];
+    size_t st[HEC_MAX_DATA_UNITS + HEC_MAX_PARITY_UNITS];
+    for (size_t i = 0; i < c->k; i++) {
+        bases[i] = d_data[i];
+        st[i] = data_strides[i];
+    }
+    for (size_t j = 0; j < c->m; j++) {
+        bases[c->k + j] = d_parity[j];
+        st[c->k + j] = parity_strides[j];
+    }
+    return hec_crc32c_device(c, bases, st, c->k + c->m, cell_len, stripes, bytes_per_checksum, d_sums, hip_stream);
 }
 
 // Tuning knobs for the measurement harness (not part of the reference API).

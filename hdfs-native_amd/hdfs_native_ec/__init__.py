@@ -37,6 +37,7 @@ EXPORTS = [
     "hec_encode_device", "hec_decode_device", "hec_gf_matmul_device",
     "hec_encode_host_batch", "hec_tune_set", "hec_decode_mixed_workspace_size",
     "hec_decode_device_mixed", "hec_coder_create_codec", "hec_decode_host_batch",
+    "hec_crc32c_device", "hec_encode_crc_device",
 ]
 
 
@@ -102,6 +103,8 @@ def _load() -> ctypes.CDLL:
         "hec_gf_matmul_device": ([P, P, S, S, PP, SP, PP, SP, S, S, P], I),
         "hec_encode_host_batch": ([P, P, P, S, S, S], I),
         "hec_decode_host_batch": ([P, PP, S, S, P, S], I),
+        "hec_crc32c_device": ([P, PP, SP, S, S, S, S, P, P], I),
+        "hec_encode_crc_device": ([P, PP, SP, PP, SP, S, S, S, P, P], I),
         "hec_tune_set": ([I, I], I),
         "hec_decode_mixed_workspace_size": ([P, S], S),
         "hec_decode_device_mixed": ([P, PP, SP, PP, SP, ctypes.POINTER(ctypes.c_uint64), S, S, P, S, P], I),
@@ -258,6 +261,16 @@ class Coder:
                                      _pp([p or 0 for p in out_ptrs]), _sp(out_strides), cell_len, stripes,
                                      ctypes.c_void_p(stream)))
 
+    def crc32c_device(self, ptrs, strides, cell_len, stripes, bytes_per_checksum, out_ptr, stream: int = 0):
+        _check(lib.hec_crc32c_device(self._h, _pp(ptrs), _sp(strides), len(ptrs), cell_len, stripes,
+                                     bytes_per_checksum, ctypes.c_void_p(out_ptr), ctypes.c_void_p(stream)))
+
+    def encode_crc_device(self, data_ptrs, data_strides, parity_ptrs, parity_strides, cell_len, stripes,
+                          bytes_per_checksum, sums_ptr, stream: int = 0):
+        _check(lib.hec_encode_crc_device(self._h, _pp(data_ptrs), _sp(data_strides), _pp(parity_ptrs),
+                                         _sp(parity_strides), cell_len, stripes, bytes_per_checksum,
+                                         ctypes.c_void_p(sums_ptr), ctypes.c_void_p(stream)))
+
     def decode_mixed_workspace_size(self, stripes: int) -> int:
         return lib.hec_decode_mixed_workspace_size(self._h, stripes)
 
@@ -305,6 +318,19 @@ def encode_batch(coder: Coder, data, parity, stream=None) -> None:
     dp, ds = stripe_layout_ptrs(data, coder.data_units)
     pp, ps = stripe_layout_ptrs(parity, coder.parity_units)
     coder.encode_device(dp, ds, pp, ps, data.shape[2], data.shape[0], s.cuda_stream)
+
+
+def crc32c_batch(coder: Coder, cells, bytes_per_checksum: int = 512, stream=None):
+    """cells: uint8 cuda tensor [S, n, cell] -> uint8 tensor [S, n, nchunks, 4]
+    of big-endian CRC32C per chunk (WritePacket::calculate_checksum)."""
+    import torch
+    S, n, cell = cells.shape
+    s = stream if stream is not None else torch.cuda.current_stream(cells.device)
+    nchunks = (cell + bytes_per_checksum - 1) // bytes_per_checksum
+    out = torch.empty((S, n, nchunks, 4), dtype=torch.uint8, device=cells.device)
+    ptrs, strides = stripe_layout_ptrs(cells, n)
+    coder.crc32c_device(ptrs, strides, cell, S, bytes_per_checksum, out.data_ptr(), s.cuda_stream)
+    return out
 
 
 def decode_batch_mixed(coder: Coder, data, parity, present_masks: Sequence[int], out, stream=None,

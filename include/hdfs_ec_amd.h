@@ -163,6 +163,26 @@ int hec_gf_matmul_device(hec_coder_t *coder, const uint8_t *matrix, size_t rows,
                          const uint8_t *const *d_in, const size_t *in_strides, uint8_t *const *d_out,
                          const size_t *out_strides, size_t cell_len, size_t stripes, void *hip_stream);
 
+/* ---- CRC32C per checksum chunk ---------------------- *
+ * WritePacket::calculate_checksum (rust/src/hdfs/connection.rs:568-584) on
+ * the device: for each of `n_shards` cells of `stripes` stripes (shard i of
+ * stripe s at d_bases[i] + s*strides[i], cell_len bytes), one CRC32C
+ * (Castagnoli / crc CRC_32_ISCSI, connection.rs:37-38) per
+ * bytes_per_checksum chunk, the last one possibly short, written big-endian
+ * (put_u32) to d_out + 4*((s*n_shards + i)*nchunks + c), nchunks =
+ * ceil(cell_len / bytes_per_checksum).  Runs on the coder's device; the
+ * fast path is bytes_per_checksum == 512 with 16-B aligned cells. */
+int hec_crc32c_device(hec_coder_t *coder, const uint8_t *const *d_bases, const size_t *strides, size_t n_shards,
+                      size_t cell_len, size_t stripes, size_t bytes_per_checksum, uint8_t *d_out,
+                      void *hip_stream);
+
+/* hec_encode_device followed by hec_crc32c_device over the k data and m
+ * parity cells (shard order 0..k+m-1): everything a striped writer needs to
+ * emit its k+m packet streams. */
+int hec_encode_crc_device(hec_coder_t *coder, const uint8_t *const *d_data, const size_t *data_strides,
+                          uint8_t *const *d_parity, const size_t *parity_strides, size_t cell_len, size_t stripes,
+                          size_t bytes_per_checksum, uint8_t *d_sums, void *hip_stream);
+
 /* ---- Pinned-host pipelined batch (PCIe-inclusive path) ----------------- *
  * Encodes a [stripe][k][cell] host batch into a [stripe][m][cell] host batch,
  * streaming chunks of `chunk_stripes` stripes H2D -> encode -> D2H with

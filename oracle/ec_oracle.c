@@ -265,3 +265,33 @@ int orc_encode_batch(size_t k, size_t m, const uint8_t *data, size_t n, size_t s
     free(mat);
     return ORC_OK;
 }
+
+/* ---- CRC32C per checksum chunk --------------------- *
+ * rust/src/hdfs/connection.rs:37-38 declares CRC32C = crc 3.4's
+ * CRC_32_ISCSI (Castagnoli, reflected poly 0x82F63B78, init and xorout
+ * 0xFFFFFFFF); WritePacket::calculate_checksum (:568-584) puts one CRC per
+ * bytes_per_checksum chunk (the last may be short) as a big-endian u32;
+ * ReadPacket::get_data (:477-504) verifies the same way.  Bitwise
+ * restatement of the published algorithm. */
+uint32_t orc_crc32c(const uint8_t *p, size_t n) {
+    uint32_t crc = 0xFFFFFFFFu;
+    for (size_t i = 0; i < n; i++) {
+        crc ^= p[i];
+        for (int b = 0; b < 8; b++) crc = (crc >> 1) ^ (0x82F63B78u & (0u - (crc & 1u)));
+    }
+    return crc ^ 0xFFFFFFFFu;
+}
+
+/* calculate_checksum over one buffer: out receives ceil(n/bpc) big-endian
+ * u32s (4 bytes each). */
+void orc_chunk_crc32c(const uint8_t *p, size_t n, size_t bpc, uint8_t *out) {
+    size_t k = 0;
+    for (size_t start = 0; start < n; start += bpc, k++) {
+        size_t len = n - start < bpc ? n - start : bpc;
+        uint32_t c = orc_crc32c(p + start, len);
+        out[4 * k] = (uint8_t)(c >> 24);
+        out[4 * k + 1] = (uint8_t)(c >> 16);
+        out[4 * k + 2] = (uint8_t)(c >> 8);
+        out[4 * k + 3] = (uint8_t)c;
+    }
+}

@@ -250,6 +250,38 @@ def ec_decode(k: int, m: int, cell_size: int, codec: str,
     return cells
 
 
+# ---- CRC32C per checksum chunk (connection.rs:37-38, :568-584) ------------
+
+def _crc32c_table():
+    t = []
+    for i in range(256):
+        c = i
+        for _ in range(8):
+            c = (c >> 1) ^ (0x82F63B78 if c & 1 else 0)
+        t.append(c)
+    return t
+
+
+CRC32C_TABLE = _crc32c_table()
+
+
+def crc32c(data: bytes) -> int:
+    """CRC-32C (iSCSI): reflected 0x82F63B78, init/xorout 0xFFFFFFFF."""
+    crc = 0xFFFFFFFF
+    for b in bytes(data):
+        crc = CRC32C_TABLE[(crc ^ b) & 0xFF] ^ (crc >> 8)
+    return crc ^ 0xFFFFFFFF
+
+
+def chunk_crc32c(data: bytes, bytes_per_checksum: int) -> bytes:
+    """WritePacket::calculate_checksum: one big-endian u32 per chunk."""
+    out = bytearray()
+    data = bytes(data)
+    for start in range(0, len(data), bytes_per_checksum):
+        out += crc32c(data[start:start + bytes_per_checksum]).to_bytes(4, "big")
+    return bytes(out)
+
+
 # ---- ctypes access to the C oracle ----------------------------------------
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -271,6 +303,9 @@ def load_c_oracle() -> ctypes.CDLL:
     lib.orc_encode_batch.argtypes = [S, S, P, S, S, P]
     lib.orc_matmul_shards.argtypes = [P, S, S, P, S, P]
     lib.orc_decode_matrix.argtypes = [S, S, P, P, P, P]
+    lib.orc_crc32c.argtypes = [P, S]
+    lib.orc_crc32c.restype = ctypes.c_uint32
+    lib.orc_chunk_crc32c.argtypes = [P, S, S, P]
     return lib
 
 

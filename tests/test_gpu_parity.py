@@ -498,3 +498,50 @@ def test_device_vertical_in_file_order_out(dev, c_oracle, k, m):
     o = out.cpu().numpy().reshape(rows, k, cell)
     for i in range(m):
         assert np.array_equal(o[:, i], data[:, i])
+
+
+# ---- CRC32C per checksum chunk ------------------------
+
+def _oracle_sums(cells: np.ndarray, bpc: int) -> np.ndarray:
+    S, n, cell = cells.shape
+    nch = (cell + bpc - 1) // bpc
+    out = np.zeros((S, n, nch, 4), dtype=np.uint8)
+    for s in range(S):
+        for i in range(n):
+            out[s, i] = np.frombuffer(O.chunk_crc32c(cells[s, i].tobytes(), bpc), dtype=np.uint8).reshape(nch, 4)
+    return out
+
+
+@pytest.mark.parametrize("cell,bpc,n", [(512 * 64, 512, 3), (512 * 70 + 256, 512, 2), (1 << 16, 512, 9),
+                                        (4096, 4096, 2), (1000, 512, 3), (3 * 512 + 16, 512, 1), (2048, 100, 2)])
+def test_crc32c_device_vs_oracle(dev, cell, bpc, n):
+    S = 3
+    cells = batch_data(S, n, cell, first=cell + bpc)
+    got = H.crc32c_batch(coder(6, 3), torch.from_numpy(cells).to(dev), bpc)
+    torch.cuda.synchronize()
+    assert np.array_equal(got.cpu().numpy(), _oracle_sums(cells, bpc))
+
+
+def test_crc32c_device_published_vector(dev):
+    cells = np.frombuffer(b"123456789" + bytes(7), dtype=np.uint8).reshape(1, 1, 16).copy()
+    got = H.crc32c_batch(coder(6, 3), torch.from_numpy(cells[:, :, :9].copy()).to(dev), 512)
+    torch.cuda.synchronize()
+    assert got.cpu().numpy().ravel().tobytes() == (0xE3069283).to_bytes(4, "big")
+
+
+def test_encode_crc_device(dev, c_oracle):
+    k, m, S, cell, bpc = 6, 3, 4, 1 << 16, 512
+    data = batch_data(S, k, cell, first=31)
+    par = oracle_batch_encode(c_oracle, k, m, data)
+    d = torch.from_numpy(data).to(dev)
+    p = torch.zeros((S, m, cell), dtype=torch.uint8, device=dev)
+    nch = cell // bpc
+    sums = torch.zeros((S, k + m, nch, 4), dtype=torch.uint8, device=dev)
+    dp, ds = H.stripe_layout_ptrs(d, k)
+    pp, ps = H.stripe_layout_ptrs(p, m)
+    coder(k, m).encode_crc_device(dp, ds, pp, ps, cell, S, bpc, sums.data_ptr(),
+                                  torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(p.cpu().numpy(), par)
+    want = _oracle_sums(np.concatenate([data, par], axis=1), bpc)
+    assert np.array_equal(sums.cpu().numpy(), want)
