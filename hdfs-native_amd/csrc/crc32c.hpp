@@ -24,4 +24,10 @@ struct CrcArgs {
 // 0 ok, -1 invalid sizes, >0 hipError_t.
 int launch_crc32c(const CrcArgs& a, int device, hipStream_t stream);
 
+struct MatmulArgs;
+// Fused encode + CRC32C of all k inputs and r outputs per 512-B chunk (sums
+// [stripe][k+r][nchunks] big-endian).  Needs k in {2,3,6,10}, r <= 4,
+// 16-B aligned layout and cell_len % 16 == 0; returns -1 otherwise.
+int launch_encode_crc(const MatmulArgs& a, uint8_t* sums, int device, hipStream_t stream);
+
 }  // namespace hec

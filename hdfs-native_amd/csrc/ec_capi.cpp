@@ -786,7 +786,39 @@ int hec_crc32c_device(hec_coder_t* c, const uint8_t* const* d_bases, const size_
 int hec_encode_crc_device(hec_coder_t* c, const uint8_t* const* d_data, const size_t* data_strides,
                           uint8_t* const* d_parity, const size_t* parity_strides, size_t cell_len, size_t stripes,
                           size_t bytes_per_checksum, uint8_t* d_sums, void* hip_stream) {
-    if (!c || !d_data || !data_strides || !d_parity || !parity_strides || !d_sums) return HEC_ERR_INVALID_ARG;
+    if (!c || !d_data || !data_strides || !d_parity || !parity_strides || !d_sums || cell_len == 0 ||
+        bytes_per_checksum == 0)
+        return HEC_ERR_INVALID_ARG;
+    if (stripes == 0) return HEC_OK;
+    // Fused single pass when the shape allows it (k in {2,3,6,10}, m <= 4,
+    // 512-B chunks, 16-B aligned cells); otherwise encode, then checksum.
+    if (bytes_per_checksum == 512 && c->m <= size_t(hec::kMaxR) && !hec::g_tune_crc_unfused) {
+        const int rc = guarded([&] {
+            DeviceGuard g(c->device);
+            if (!g.ok) return fail(HEC_ERR_DEVICE, "hipSetDevice", hipErrorInvalidDevice);
+            hec::MatmulArgs a;
+            std::memset(&a, 0, sizeof(a));
+            for (size_t i = 0; i < c->k; i++) {
+                if (!d_data[i]) return int(HEC_ERR_INVALID_ARG);
+                a.in[i] = d_data[i];
+                a.in_stride[i] = data_strides[i];
+            }
+            for (size_t j = 0; j < c->m; j++) {
+                if (!d_parity[j]) return int(HEC_ERR_INVALID_ARG);
+                a.out[j] = d_parity[j];
+                a.out_stride[j] = parity_strides[j];
+                for (size_t i = 0; i < c->k; i++) a.coef[j * hec::kMaxK + i] = c->enc[(c->k + j) * c->k + i];
+            }
+            a.k = int32_t(c->k);
+            a.r = int32_t(c->m);
+            a.cell_len = cell_len;
+            a.stripes = stripes;
+            const int lrc = hec::launch_encode_crc(a, d_sums, c->device, static_cast<hipStream_t>(hip_stream));
+            if (lrc == -1) return 1;  // shape not covered: fall through
+            return lrc == 0 ? int(HEC_OK) : to_status(lrc);
+        });
+        if (rc != 1) return rc;
+    }
     int rc = hec_encode_device(c, d_data, data_strides, d_parity, parity_strides, cell_len, stripes, hip_stream);
     if (rc != HEC_OK) return rc;
     const uint8_t* bases[HEC_MAX_DATA_UNITS + HEC_MAX_PARITY_UNITS];
@@ -808,7 +840,9 @@ int hec_encode_crc_device(hec_coder_t* c, const uint8_t* const* d_data, const si
 // (0|1), 3 = resident blocks per CU, 4 = threads per block (256|512),
 // 5 = pipeline (1 = register kernel, 2 = LDS-DMA prefetch kernel),
 // 6 = chunk mapping (1 = block slabs, 2 = wave-contiguous runs), 7 = grid size,
-// 8 = tile-order group (stripes interleaved column-major; 1 = stripe-major).
+// 8 = tile-order group (stripes interleaved column-major; 1 = stripe-major),
+// 9 = 1: hec_encode_crc_device as two passes (encode, then CRC) instead of fused,
+// 10 = slabs per wave of the fused encode+CRC kernel (0 default, 4 or 8).
 int hec_tune_set(int key, int value) {
     switch (key) {
         case 1:
@@ -839,6 +873,13 @@ int hec_tune_set(int key, int value) {
         case 8:
             if (value < 0 || value > 65536) return HEC_ERR_INVALID_ARG;
             hec::g_tune_group = value;
+            return HEC_OK;
+        case 9:
+            hec::g_tune_crc_unfused = value ? 1 : 0;
+            return HEC_OK;
+        case 10:
+            if (value != 0 && value != 4 && value != 8) return HEC_ERR_INVALID_ARG;
+            hec::g_tune_fused_slabs = value;
             return HEC_OK;
         default: return HEC_ERR_INVALID_ARG;
     }

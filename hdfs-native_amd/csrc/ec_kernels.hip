@@ -25,6 +25,8 @@
 
 #include <cstdint>
 
+#include "crc32c.hpp"
+#include "crc32c_tables.hpp"
 #include "ec_kernels.hpp"
 #include "gf256.hpp"
 
@@ -565,6 +567,199 @@ __global__ __launch_bounds__(BS) void gf_decode_mixed(MixedArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Fused encode + CRC32C per 512-B chunk of every input and output cell
+// (the write path checksums all k+m cells right after the
+// encode; fusing saves a second HBM pass over them).  Register GF math as in
+// gf_matmul_v16 (MAP 0, U chunks), then each wave drops its (K+R) x U
+// 1-KiB pieces -- each exactly two chunk-aligned 512-B chunks -- into a
+// wave-private LDS image of 144-B quarter rows and runs the quarter-chunk
+// CRC of crc32c.hip over it in rounds of 64 quarters.
+// ---------------------------------------------------------------------------
+namespace {
+__constant__ crc::Tables kFusedCrcTables = crc::Tables();
+
+__device__ __forceinline__ uint32_t crc8(const uint32_t (*t)[256], uint32_t crc, uint32_t lo, uint32_t hi) {
+    lo ^= crc;
+    return t[7][lo & 0xFF] ^ t[6][(lo >> 8) & 0xFF] ^ t[5][(lo >> 16) & 0xFF] ^ t[4][lo >> 24] ^
+           t[3][hi & 0xFF] ^ t[2][(hi >> 8) & 0xFF] ^ t[1][(hi >> 16) & 0xFF] ^ t[0][hi >> 24];
+}
+}  // namespace
+
+// Layout: a wave owns SLABS KiB (SLABS slabs of 1 KiB, one 16-B load per
+// lane per slab) of every cell of its stripe; one CRC round is 64 quarters
+// = 8 pieces = 8/SLABS shards' share, over a 9-KiB image (as in crc32c.hip).
+// Inputs stream shard by shard (the next one prefetched into registers when
+// the budget allows) while being accumulated into the r parity registers
+// and staged for the round; then each parity shard is stored and staged.
+// SLABS = 8 (one shard per round) when the r x 8 accumulators fit 2 waves
+// per SIMD, else 4 (two shards per round; an odd k + r leaves one
+// half-empty round).  9 KiB of image per wave -> 8 waves per CU.
+template <int K, int R, int SLABS>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void gf_encode_crc(MatmulArgs a,
+                                                                                              uint8_t* sums) {
+    constexpr int BS = 256, PITCH = 144, STAGE = 64 * PITCH, SPR = 8 / SLABS;
+    constexpr uint32_t WAVE_BYTES = SLABS * 1024u, TILE_BYTES = 4 * WAVE_BYTES;
+    constexpr bool PF = R * SLABS <= 24;  // register prefetch of the next shard
+    __shared__ PermTable s_tab[R][kMaxK];
+    __shared__ uint8_t s_exp[512];
+    __shared__ uint8_t s_log[256];
+    __shared__ uint8_t s_coef[R * kMaxK];
+    __shared__ uint32_t s_ctab[8][256];
+    __shared__ uint32_t s_shift[3][4][256];
+    __shared__ __attribute__((aligned(16))) uint8_t s_stage[4 * STAGE];
+    prologue<R, BS>(a, K, s_tab, s_exp, s_log, s_coef);
+    for (int t = threadIdx.x; t < 8 * 256; t += BS) (&s_ctab[0][0])[t] = (&kFusedCrcTables.slice[0][0])[t];
+    for (int t = threadIdx.x; t < 3 * 4 * 256; t += BS) (&s_shift[0][0][0])[t] = (&kFusedCrcTables.shift[0][0][0])[t];
+    __syncthreads();
+    const uint32_t kfinal = kFusedCrcTables.final512;
+
+    const uint64_t cell_len = a.cell_len;
+    const uint64_t nck = (cell_len + 511) / 512;  // CRC chunks per cell
+    const uint32_t total = a.total_tiles;
+    const int wave = threadIdx.x / 64, lane = threadIdx.x & 63;
+    // this lane's quarter in a round: row `lane` = piece lane/8 = (shard
+    // slot sir, slab), chunk half (lane/4)&1 of that slab, quarter qi
+    const int qi = lane & 3, piece = lane >> 3, sir = piece / SLABS, pslab = piece % SLABS, half = (lane >> 2) & 1;
+    uint8_t* stage = s_stage + wave * STAGE;
+    uint32_t* out_sums = reinterpret_cast<uint32_t*>(sums);
+
+    for (uint32_t tile = blockIdx.x; tile < total; tile += gridDim.x) {
+        uint32_t stripe, tcol;
+        tile_coords(tile, a, stripe, tcol);
+        const uint64_t wbyte = uint64_t(tcol) * TILE_BYTES + uint64_t(wave) * WAVE_BYTES;  // wave's first byte
+        if (wbyte >= cell_len) continue;  // wave-uniform
+        // 32-bit lane offsets from a wave-uniform per-shard base (saddr +
+        // voffset addressing); dead slabs of a short last tile read slab 0
+        const uint64_t left = cell_len - wbyte;
+        uint32_t voff[SLABS];
+        bool live[SLABS];
+#pragma unroll
+        for (int u = 0; u < SLABS; u++) {
+            const uint32_t o = uint32_t(u) * 1024u + uint32_t(lane) * 16u;
+            live[u] = o < left;
+            voff[u] = live[u] ? o : 0u;
+        }
+        const uint64_t cbyte = wbyte + uint64_t(pslab) * 1024u + uint64_t(half) * 512u;
+        const bool in_cell = cbyte < cell_len;
+        const bool full = in_cell && cell_len - cbyte >= 512u;  // same for a chunk's 4 lanes
+
+        auto crc_round = [&](int first, int count) {
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("" ::: "memory");
+            const bool live_c = in_cell && sir < count;
+            uint32_t val = 0;
+            if (full && sir < count) {
+                uint32_t r = 0;
+                const uint8_t* row = stage + lane * PITCH;
+#pragma unroll
+                for (int t = 0; t < 8; t++) {
+                    const u32x4 w = *reinterpret_cast<const u32x4*>(row + t * 16);
+                    r = crc8(s_ctab, r, w.x, w.y);
+                    r = crc8(s_ctab, r, w.z, w.w);
+                }
+                if (qi < 3)
+                    r = s_shift[qi][0][r & 0xFF] ^ s_shift[qi][1][(r >> 8) & 0xFF] ^
+                        s_shift[qi][2][(r >> 16) & 0xFF] ^ s_shift[qi][3][r >> 24];
+                val = r;
+            } else if (live_c && qi == 0) {
+                const uint32_t len = uint32_t(cell_len - cbyte);
+                uint32_t r = 0xFFFFFFFFu;
+                for (uint32_t b = 0; b < len; b += 16) {
+                    const u32x4 w = *reinterpret_cast<const u32x4*>(stage + (lane + b / 128) * PITCH + (b % 128));
+                    r = crc8(s_ctab, r, w.x, w.y);
+                    r = crc8(s_ctab, r, w.z, w.w);
+                }
+                val = ~r;
+            }
+            val ^= __shfl_xor(val, 1);
+            val ^= __shfl_xor(val, 2);
+            if (live_c && qi == 0)
+                out_sums[(uint64_t(stripe) * (K + R) + first + sir) * nck + cbyte / 512] =
+                    __builtin_bswap32(full ? (val ^ kfinal) : val);
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("" ::: "memory");
+        };
+        // slab u of the shard in round slot `slot`: lane l's 16 B -> row
+        // 8*(slot*SLABS + u) + l/8, byte 16*(l%8)
+        auto stage_piece = [&](int slot, int u, const u32x4& v) {
+            *reinterpret_cast<u32x4*>(stage + (8 * (slot * SLABS + u) + lane / 8) * PITCH + 16 * (lane % 8)) = v;
+        };
+        auto after_stage = [&](int shard) {
+            if (shard % SPR == SPR - 1 || shard == K + R - 1) crc_round(shard - shard % SPR, shard % SPR + 1);
+        };
+
+        u32x4 acc[SLABS][R];
+#pragma unroll
+        for (int u = 0; u < SLABS; u++)
+#pragma unroll
+            for (int j = 0; j < R; j++) acc[u][j] = u32x4{0, 0, 0, 0};
+        u32x4 x[SLABS], xn[SLABS];
+#pragma unroll
+        for (int u = 0; u < SLABS; u++) x[u] = load16<true>(a.in[0] + (uint64_t(stripe) * a.in_stride[0] + wbyte) + voff[u]);
+#pragma unroll
+        for (int i = 0; i < K; i++) {
+            if (PF && i + 1 < K) {
+#pragma unroll
+                for (int u = 0; u < SLABS; u++)
+                    xn[u] = load16<true>(a.in[i + 1] + (uint64_t(stripe) * a.in_stride[i + 1] + wbyte) + voff[u]);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < SLABS; u++) stage_piece(i % SPR, u, x[u]);
+            // opaque per-input table offset threaded through the
+            // accumulators: keeps the table reads (and the GF math) of input
+            // i from being hoisted next to those of the other inputs
+            uint32_t toff = uint32_t(i) * uint32_t(sizeof(PermTable));
+            asm volatile("" : "+v"(toff));
+#pragma unroll
+            for (int u = 0; u < SLABS; u++) {
+                asm volatile("" : "+v"(x[u]));
+#pragma unroll
+                for (int j = 0; j < R; j++) asm volatile("" : "+v"(acc[u][j]) : "v"(toff));
+            }
+            uint32_t tb[R][5];
+#pragma unroll
+            for (int j = 0; j < R; j++) {
+                const PermTable& t =
+                    *reinterpret_cast<const PermTable*>(reinterpret_cast<const char*>(&s_tab[j][0]) + toff);
+                tb[j][0] = t.t0lo;
+                tb[j][1] = t.t0hi;
+                tb[j][2] = t.t1lo;
+                tb[j][3] = t.t1hi;
+                tb[j][4] = t.t2;
+            }
+#pragma unroll
+            for (int u = 0; u < SLABS; u++)
+#pragma unroll
+                for (int d = 0; d < 4; d++) {
+                    const Sel sl = make_sel(x[u][d]);
+#pragma unroll
+                    for (int j = 0; j < R; j++)
+                        acc[u][j][d] ^= gf_mul4(tb[j][0], tb[j][1], tb[j][2], tb[j][3], tb[j][4], sl.s0, sl.s1, sl.s2);
+                }
+            __builtin_amdgcn_sched_barrier(0);
+            after_stage(i);
+            __builtin_amdgcn_sched_barrier(0);
+            if (i + 1 < K) {
+#pragma unroll
+                for (int u = 0; u < SLABS; u++)
+                    x[u] = PF ? xn[u]
+                              : load16<true>(a.in[i + 1] + (uint64_t(stripe) * a.in_stride[i + 1] + wbyte) + voff[u]);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < R; j++) {
+#pragma unroll
+            for (int u = 0; u < SLABS; u++) {
+                if (live[u]) store16<true>(a.out[j] + (uint64_t(stripe) * a.out_stride[j] + wbyte) + voff[u], acc[u][j]);
+                stage_piece((K + j) % SPR, u, acc[u][j]);
+            }
+            after_stage(K + j);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Byte kernel: tails and unaligned layouts.  One thread per (stripe, byte) in
 // [a.byte_begin, a.cell_len); LDS log/antilog lookups.
 // ---------------------------------------------------------------------------
@@ -707,6 +902,8 @@ int g_tune_pipeline = 0;       // 0 = per-shape default, 1 = register kernel, 2 
 int g_tune_map = 0;            // 0 = default, 1 = MAP 0, 2 = MAP 1
 int g_tune_grid = 0;           // 0 = blocks_per_cu * CUs, else absolute block count
 int g_tune_group = 0;          // 0 = default (1), else stripes per tile-order group
+int g_tune_crc_unfused = 0;    // 1 = hec_encode_crc_device as two passes
+int g_tune_fused_slabs = 0;    // 0 = default, 4 / 8 = slabs per wave of the fused encode+CRC
 
 namespace {
 
@@ -849,6 +1046,61 @@ int launch_decode_mixed(const MixedArgs& in, int rows, int device, hipStream_t s
     if (grid > total) grid = total;
     void* args[] = {&a};
     const hipError_t e = hipLaunchKernel(fn, dim3(uint32_t(grid)), dim3(BS), args, res ? a.blob_bytes : 0, stream);
+    return e == hipSuccess ? 0 : int(e);
+}
+
+namespace {
+// 8 slabs per wave while the r x 8 accumulators fit (k <= 6, r <= 3), else 4
+constexpr int fused_slabs(int k, int r) { return (r <= 3 && k <= 6) ? 8 : 4; }
+
+template <int K, int R>
+const void* fused_fn(int slabs) {
+    if (slabs == 4) return reinterpret_cast<const void*>(&gf_encode_crc<K, R, 4>);
+    return reinterpret_cast<const void*>(&gf_encode_crc<K, R, 8>);
+}
+
+template <int K>
+const void* fused_pick_r(int r, int slabs) {
+    switch (r) {
+        case 1: return fused_fn<K, 1>(slabs);
+        case 2: return fused_fn<K, 2>(slabs);
+        case 3: return fused_fn<K, 3>(slabs);
+        default: return fused_fn<K, 4>(slabs);
+    }
+}
+}  // namespace
+
+int launch_encode_crc(const MatmulArgs& in, uint8_t* sums, int device, hipStream_t stream) {
+    MatmulArgs a = in;
+    bool aligned = a.cell_len % 16 == 0 && (reinterpret_cast<uintptr_t>(sums) & 3u) == 0 && a.r <= kMaxR;
+    for (int i = 0; i < a.k; i++)
+        aligned &= ((reinterpret_cast<uintptr_t>(a.in[i]) | a.in_stride[i]) & 15u) == 0;
+    for (int j = 0; j < a.r; j++)
+        aligned &= ((reinterpret_cast<uintptr_t>(a.out[j]) | a.out_stride[j]) & 15u) == 0;
+    const int slabs = (g_tune_fused_slabs == 4 || g_tune_fused_slabs == 8) ? g_tune_fused_slabs : fused_slabs(a.k, a.r);
+    const void* fn = nullptr;
+    switch (a.k) {
+        case 2: fn = fused_pick_r<2>(a.r, slabs); break;
+        case 3: fn = fused_pick_r<3>(a.r, slabs); break;
+        case 6: fn = fused_pick_r<6>(a.r, slabs); break;
+        case 10: fn = fused_pick_r<10>(a.r, slabs); break;
+        default: return -1;
+    }
+    if (!aligned) return -1;
+    const uint64_t chunks = a.cell_len / 16;
+    const uint64_t tile_bytes = 4096u * uint64_t(slabs);  // 4 waves x slabs x 1 KiB
+    const uint64_t tps = (a.cell_len + tile_bytes - 1) / tile_bytes;
+    const uint64_t total = tps * a.stripes;
+    if (chunks > 0xFFFFFFFFull || total > 0xFFFFFFFFull) return -1;
+    if (total == 0) return 0;
+    a.chunks = uint32_t(chunks);
+    a.tiles_per_stripe = uint32_t(tps);
+    a.total_tiles = uint32_t(total);
+    a.group = g_tune_group > 0 ? uint32_t(g_tune_group) : 4u;
+    uint64_t grid = uint64_t(num_cus(device)) * 2;  // ~60 KiB LDS per block: two per CU
+    if (grid > total) grid = total;
+    void* args[] = {&a, &sums};
+    const hipError_t e = hipLaunchKernel(fn, dim3(uint32_t(grid)), dim3(256), args, 0, stream);
     return e == hipSuccess ? 0 : int(e);
 }
 

@@ -82,5 +82,7 @@ extern int g_tune_pipeline;       // 0 = default, 1 = register kernel, 2 = LDS-D
 extern int g_tune_map;            // 0 = default, 1|2 = chunk mapping 0|1
 extern int g_tune_grid;           // 0 = default, else absolute grid size
 extern int g_tune_group;          // 0 = default, else stripes per tile-order group
+extern int g_tune_crc_unfused;    // 1 = encode + separate CRC pass
+extern int g_tune_fused_slabs;    // 0 = default, else 4 / 8 slabs per wave (fused encode+CRC)
 
 }  // namespace hec

@@ -176,9 +176,12 @@ int hec_crc32c_device(hec_coder_t *coder, const uint8_t *const *d_bases, const s
                       size_t cell_len, size_t stripes, size_t bytes_per_checksum, uint8_t *d_out,
                       void *hip_stream);
 
-/* hec_encode_device followed by hec_crc32c_device over the k data and m
- * parity cells (shard order 0..k+m-1): everything a striped writer needs to
- * emit its k+m packet streams. */
+/* Encode plus CRC32C of the k data and m parity cells (shard order
+ * 0..k+m-1, same output layout as hec_crc32c_device): everything a striped
+ * writer needs to emit its k+m packet streams.  One fused pass (the
+ * checksums are taken from the registers/LDS the encode already holds) for
+ * k in {2,3,6,10}, m <= 4, 512-B chunks and 16-B aligned cells; otherwise an
+ * encode followed by hec_crc32c_device. */
 int hec_encode_crc_device(hec_coder_t *coder, const uint8_t *const *d_data, const size_t *data_strides,
                           uint8_t *const *d_parity, const size_t *parity_strides, size_t cell_len, size_t stripes,
                           size_t bytes_per_checksum, uint8_t *d_sums, void *hip_stream);
@@ -212,6 +215,8 @@ int hec_decode_host_batch(hec_coder_t *coder, const uint8_t *const *h_vertical, 
  * key 6: chunk mapping (1 = block slabs, 2 = wave-contiguous runs; 0 = default)
  * key 7: absolute grid size in blocks (0 = default)
  * key 8: tile order, stripes interleaved per group (1 = stripe-major; 0 = default)
+ * key 9: 1 = hec_encode_crc_device as encode + separate CRC pass (0 = fused)
+ * key 10: fused encode+CRC slabs per wave: 0 = default, 4 or 8
  * Process-wide; affects launches made after the call. */
 int hec_tune_set(int key, int value);
 

@@ -529,19 +529,58 @@ def test_crc32c_device_published_vector(dev):
     assert got.cpu().numpy().ravel().tobytes() == (0xE3069283).to_bytes(4, "big")
 
 
-def test_encode_crc_device(dev, c_oracle):
-    k, m, S, cell, bpc = 6, 3, 4, 1 << 16, 512
-    data = batch_data(S, k, cell, first=31)
-    par = oracle_batch_encode(c_oracle, k, m, data)
+@pytest.mark.parametrize("codec,k,m,cell,S", [
+    ("rs", 6, 3, 1 << 16, 4), ("rs", 6, 3, 3 * 512 + 16, 5), ("rs", 6, 3, (1 << 16) + 48, 3),
+    ("rs", 10, 4, 1 << 15, 3), ("rs", 10, 4, 70 * 512 + 256, 2), ("rs", 3, 2, 1 << 17, 3),
+    ("rs", 2, 1, 8192 + 512, 4), ("rs", 12, 4, 1 << 14, 2), ("rs", 6, 3, 1000, 2), ("xor", 2, 1, 1 << 14, 3)])
+@pytest.mark.parametrize("fused", [0, 4, 8, None])
+def test_encode_crc_device(dev, c_oracle, codec, k, m, cell, S, fused):
+    """Fused encode+CRC (k in {2,3,6,10}) and the two-pass fallback (other k,
+    unaligned cell_len, or tune key 9) against oracle parity + oracle CRCs."""
+    bpc = 512
+    data = batch_data(S, k, cell, first=31 + cell)
+    if codec == "xor":
+        par = np.bitwise_xor.reduce(data, axis=1, keepdims=True)
+        cod = H.Coder(k, m, 0, "xor")
+    else:
+        par = oracle_batch_encode(c_oracle, k, m, data)
+        cod = coder(k, m)
     d = torch.from_numpy(data).to(dev)
     p = torch.zeros((S, m, cell), dtype=torch.uint8, device=dev)
-    nch = cell // bpc
+    nch = (cell + bpc - 1) // bpc
     sums = torch.zeros((S, k + m, nch, 4), dtype=torch.uint8, device=dev)
     dp, ds = H.stripe_layout_ptrs(d, k)
     pp, ps = H.stripe_layout_ptrs(p, m)
-    coder(k, m).encode_crc_device(dp, ds, pp, ps, cell, S, bpc, sums.data_ptr(),
-                                  torch.cuda.current_stream().cuda_stream)
-    torch.cuda.synchronize()
+    # fused: 0 = default slabs/wave, 4 / 8 forced; None = two-pass fallback
+    H.tune_set(9, 1 if fused is None else 0)
+    H.tune_set(10, fused or 0)
+    try:
+        cod.encode_crc_device(dp, ds, pp, ps, cell, S, bpc, sums.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+    finally:
+        H.tune_set(9, 0)
+        H.tune_set(10, 0)
     assert np.array_equal(p.cpu().numpy(), par)
     want = _oracle_sums(np.concatenate([data, par], axis=1), bpc)
     assert np.array_equal(sums.cpu().numpy(), want)
+
+
+def test_encode_crc_full_size_properties(dev):
+    """RS(6,3) 1 MiB x 64 fused: parity equals a plain encode and sums equal
+    a standalone CRC pass over the same k+m cells (size-independent)."""
+    k, m, cell, S = 6, 3, 1 << 20, 64
+    c = coder(k, m)
+    d = torch.empty((S, k, cell), dtype=torch.uint8, device=dev)
+    g = torch.Generator(device=dev).manual_seed(7)
+    d.random_(0, 256, generator=g)
+    p1 = torch.empty((S, m, cell), dtype=torch.uint8, device=dev)
+    p2 = torch.empty_like(p1)
+    H.encode_batch(c, d, p1)
+    sums = torch.empty((S, k + m, cell // 512, 4), dtype=torch.uint8, device=dev)
+    dp, ds = H.stripe_layout_ptrs(d, k)
+    pp, ps = H.stripe_layout_ptrs(p2, m)
+    c.encode_crc_device(dp, ds, pp, ps, cell, S, 512, sums.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    ref = H.crc32c_batch(c, torch.cat([d, p1], dim=1), 512)
+    torch.cuda.synchronize()
+    assert torch.equal(p1, p2)
+    assert torch.equal(sums, ref)
