@@ -8,27 +8,33 @@
 // emitted big-endian (put_u32).  Shards are written as whole cells, so the
 // chunks of a cell are exactly the chunks of its block stream.
 //
-// Kernel (512-B chunks): a wave owns 16 consecutive chunks (8 KiB) of one
-// cell and each lane a QUARTER chunk (128 B):
-//  1. 8 coalesced 16-B-per-lane loads (1 KiB per wave-instruction) are
-//     written to a wave-private LDS image [quarter][128 + 16 B pad]; the pad
-//     makes both the ds_write_b128 fill and the per-lane ds_read_b128 walk
-//     bank-conflict free.
-//  2. Each lane runs slicing-by-8 over its 128 B from register state 0 (the
-//     linear part of the CRC), moves it to its place in the chunk with a
-//     "append 384/256/128 zero bytes" byte table (CRC is linear over GF(2)),
-//     and two XOR shuffles combine the 4 quarters; the init/xorout constant
-//     of a 512-B chunk is folded in at the end.
-// 9 KiB of image per wave (vs 33 KiB for a chunk per lane) lets 8 waves share
-// a CU, so table walks of some waves hide the loads of others.  No
-// cross-wave traffic and no block barrier after the table prologue.  The
-// bound is the LDS table-lookup rate (1 random ds_read_b32 per byte).
+// Fast kernel (512-B chunks): a wave owns 16 consecutive chunks (8 KiB) of
+// one cell ("task") and each lane a QUARTER chunk (128 B):
+//  1. the task's 8 coalesced 16-B-per-lane loads were issued PF tasks ago
+//     into registers; they are written to a wave-private LDS image
+//     [quarter][128 + 16 B pad] (the pad makes both the ds_write_b128 fill
+//     and the per-lane ds_read_b128 walk bank-conflict free) and the
+//     registers are refilled with the loads of task + PF;
+//  2. each lane computes the linear CRC of its 128 B from state 0 with one
+//     of two lookup SCHEMEs (below), moves it to its place in the chunk with
+//     an "append 384/256/128 zero bytes" byte table (CRC is linear over
+//     GF(2)), two XOR shuffles combine the 4 quarters and the init/xorout
+//     constant of a 512-B chunk is folded in.
+// SCHEME 1: slicing-by-8 from 8 KiB of tables, 256-thread blocks, 2 per CU.
+//   Random table indices hit the 32 banks of a ds_read_b32 half-wave ~3-4
+//   ways deep: LDS-array bound (PMC: 85 % busy, 60 % of it conflicts).
+// SCHEME 4 / 8: slicing-by-1 from a table REPLICATED across the 32 banks
+//   (lane l reads column l%32: conflict free), the quarter as 4 / 8
+//   independent segment chains (latency) combined with "append 16*j zero
+//   bytes" tables; 72 KiB of tables, 512-thread blocks, 1 per CU.
+// No cross-wave traffic and no block barrier after the table prologue.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
 
 #include "crc32c.hpp"
 #include "crc32c_tables.hpp"
+#include "ec_kernels.hpp"
 
 namespace hec {
 
@@ -37,7 +43,6 @@ namespace {
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kCrcBlock = 256;
-constexpr int kWaves = kCrcBlock / 64;
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
@@ -47,46 +52,125 @@ __device__ __forceinline__ uint32_t crc_step8(const uint32_t (*t)[256], uint32_t
            t[3][hi & 0xFF] ^ t[2][(hi >> 8) & 0xFF] ^ t[1][(hi >> 16) & 0xFF] ^ t[0][hi >> 24];
 }
 
+__device__ __forceinline__ uint32_t apply_shift(const uint32_t (*t)[256], uint32_t r) {
+    return t[0][r & 0xFF] ^ t[1][(r >> 8) & 0xFF] ^ t[2][(r >> 16) & 0xFF] ^ t[3][r >> 24];
+}
+
 __constant__ crc::Tables kCrcTables = crc::Tables();
 
-// Fast path: 512-B chunks, 16-B aligned cells (cell_len % 16 == 0).
-__global__ __launch_bounds__(kCrcBlock) void crc32c_chunks512(CrcArgs a) {
-    constexpr int CH = 512, Q = CH / 4, PITCH = Q + 16, STAGE = 64 * PITCH;
-    constexpr int CHUNKS_PER_TASK = 16;
-    __shared__ uint32_t s_tab[8][256];
-    __shared__ uint32_t s_shift[3][4][256];
-    __shared__ __attribute__((aligned(16))) uint8_t s_stage[kWaves * STAGE];
-    for (int t = threadIdx.x; t < 8 * 256; t += kCrcBlock) (&s_tab[0][0])[t] = (&kCrcTables.slice[0][0])[t];
-    for (int t = threadIdx.x; t < 3 * 4 * 256; t += kCrcBlock)
-        (&s_shift[0][0][0])[t] = (&kCrcTables.shift[0][0][0])[t];
+// One wave's task: 16 chunks (8 KiB) of one cell, 8 coalesced 1-KiB loads.
+// `task` is wave-uniform (scalar base/stride loads); the loads are
+// unconditional with dead lanes clamped to the cell start -- a conditional
+// load with a zero default makes hipcc copy the result out of the load's
+// registers behind an s_waitcnt vmcnt(0), which serialises the prefetch.
+// Dead lanes' bytes are never checksummed.
+__device__ __forceinline__ void load_task(const CrcArgs& a, uint64_t groups, uint64_t task, int lane, u32x4 (&v)[8]) {
+    const uint64_t cell_idx = task / groups;
+    const uint64_t g = task - cell_idx * groups;
+    const uint64_t stripe = cell_idx / a.n_shards;
+    const uint32_t shard = uint32_t(cell_idx - stripe * a.n_shards);
+    const uint8_t* base = a.base[shard] + stripe * a.stride[shard] + g * 16u * 512u;
+    const uint64_t left = a.cell_len - g * 16u * 512u;
+#pragma unroll
+    for (int t = 0; t < 8; t++) {
+        const uint32_t off = uint32_t(t) * 1024u + uint32_t(lane) * 16u;
+        v[t] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(base + (off < left ? off : 0u)));
+    }
+}
+
+// SCHEME 4 / 8: a 128-B quarter as NCHAIN independent segments of
+// 128/NCHAIN bytes (slicing-by-1, bank-replicated table), combined by the
+// "append 16*(7-i) zero bytes" tables seg[i].
+template <int NCHAIN>
+__device__ __forceinline__ uint32_t quarter_crc_rep(const uint32_t (*rep)[32], const uint32_t (*seg)[4][256],
+                                                    const uint8_t* row, int bank) {
+    static_assert(NCHAIN == 4 || NCHAIN == 8, "4 or 8 chains");
+    constexpr int SEGW = 32 / NCHAIN;  // dwords per segment
+    u32x4 w[8];
+#pragma unroll
+    for (int t = 0; t < 8; t++) w[t] = *reinterpret_cast<const u32x4*>(row + t * 16);
+    uint32_t c[NCHAIN];
+#pragma unroll
+    for (int s = 0; s < NCHAIN; s++) c[s] = 0;
+#pragma unroll
+    for (int d = 0; d < SEGW; d++) {  // dword d of each segment
+#pragma unroll
+        for (int s = 0; s < NCHAIN; s++) {
+            const int dw = s * SEGW + d;
+            c[s] ^= w[dw / 4][dw % 4];
+        }
+#pragma unroll
+        for (int b = 0; b < 4; b++)
+#pragma unroll
+            for (int s = 0; s < NCHAIN; s++) c[s] = rep[c[s] & 0xFF][bank] ^ (c[s] >> 8);
+    }
+    uint32_t q = c[NCHAIN - 1];
+#pragma unroll
+    for (int s = 0; s < NCHAIN - 1; s++) q ^= apply_shift(seg[7 - (NCHAIN - 1 - s) * (8 / NCHAIN)], c[s]);
+    return q;
+}
+
+// SCHEME 1: the quarter with slicing-by-8.
+__device__ __forceinline__ uint32_t quarter_crc_s8(const uint32_t (*tab)[256], const uint8_t* row) {
+    uint32_t r = 0;
+#pragma unroll
+    for (int t = 0; t < 8; t++) {
+        const u32x4 w = *reinterpret_cast<const u32x4*>(row + t * 16);
+        r = crc_step8(tab, r, w.x, w.y);
+        r = crc_step8(tab, r, w.z, w.w);
+    }
+    return r;
+}
+
+template <int SCHEME>
+struct CrcShape {
+    static constexpr int kBlock = SCHEME <= 1 ? 256 : 512;
+    static constexpr int kWaves = kBlock / 64;
+    // table words: slice[8][256] | rep[256][32] ; shift[3][4][256] ; seg[7][4][256]
+    static constexpr int kMainWords = SCHEME <= 1 ? 8 * 256 : 256 * 32;
+    static constexpr int kSegWords = SCHEME <= 1 ? 0 : 7 * 4 * 256;
+    static constexpr int kTableWords = kMainWords + 3 * 4 * 256 + kSegWords;
+};
+
+template <int SCHEME, int PF>
+__global__ __launch_bounds__(CrcShape<SCHEME>::kBlock) void crc32c_chunks512(CrcArgs a) {
+    using Sh = CrcShape<SCHEME>;
+    constexpr int CH = 512, Q = CH / 4, PITCH = Q + 16, STAGE = 64 * PITCH, BS = Sh::kBlock;
+    __shared__ uint32_t s_tables[Sh::kTableWords];
+    __shared__ __attribute__((aligned(16))) uint8_t s_stage[Sh::kWaves * STAGE];
+    uint32_t* s_main = s_tables;
+    const uint32_t(*s_shift)[4][256] = reinterpret_cast<const uint32_t(*)[4][256]>(s_tables + Sh::kMainWords);
+    const uint32_t(*s_seg)[4][256] =
+        reinterpret_cast<const uint32_t(*)[4][256]>(s_tables + Sh::kMainWords + 3 * 4 * 256);
+    if constexpr (SCHEME <= 1) {
+        for (int t = threadIdx.x; t < 8 * 256; t += BS) s_main[t] = (&kCrcTables.slice[0][0])[t];
+    } else {
+        for (int t = threadIdx.x; t < 256 * 32; t += BS) s_main[t] = kCrcTables.slice[0][t / 32];
+        for (int t = threadIdx.x; t < 7 * 4 * 256; t += BS)
+            s_tables[Sh::kMainWords + 3 * 4 * 256 + t] = (&kCrcTables.seg[0][0][0])[t];
+    }
+    for (int t = threadIdx.x; t < 3 * 4 * 256; t += BS) s_tables[Sh::kMainWords + t] = (&kCrcTables.shift[0][0][0])[t];
     __syncthreads();
     const uint32_t kfinal = kCrcTables.final512;
 
-    const int wave = threadIdx.x / 64, lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / 64), lane = threadIdx.x & 63;
     const int qi = lane & 3, c = lane >> 2;  // quarter, chunk within the task
     uint8_t* stage = s_stage + wave * STAGE;
     const uint64_t groups = a.groups_per_cell;
     const uint64_t tasks = groups * a.n_shards * a.stripes;
-    for (uint64_t task = uint64_t(blockIdx.x) * kWaves + wave; task < tasks; task += uint64_t(gridDim.x) * kWaves) {
+    const uint64_t step = uint64_t(gridDim.x) * Sh::kWaves;
+
+    // stage v (task's data), refill v with task `next`'s loads, checksum
+    auto run_task = [&](uint64_t task, u32x4 (&v)[8], uint64_t next) {
         const uint64_t cell_idx = task / groups;
         const uint64_t g = task - cell_idx * groups;
-        const uint64_t stripe = cell_idx / a.n_shards;
-        const uint32_t shard = uint32_t(cell_idx - stripe * a.n_shards);
-        const uint8_t* base = a.base[shard] + stripe * a.stride[shard];
-        const uint64_t start = g * CHUNKS_PER_TASK * CH;
-        u32x4 v[8];
-#pragma unroll
-        for (int t = 0; t < 8; t++) {
-            const uint32_t off = uint32_t(t) * 1024u + uint32_t(lane) * 16u;
-            v[t] = u32x4{0, 0, 0, 0};
-            if (start + off < a.cell_len)
-                v[t] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(base + start + off));
-        }
+        const uint64_t start = g * 16u * CH;
 #pragma unroll
         for (int t = 0; t < 8; t++) {
             const uint32_t off = uint32_t(t) * 1024u + uint32_t(lane) * 16u;
             *reinterpret_cast<u32x4*>(stage + (off / Q) * PITCH + (off % Q)) = v[t];
         }
+        if (next < tasks) load_task(a, groups, next, lane, v);
         // lanes read what other lanes of the SAME wave wrote: a wave's LDS ops
         // complete in order; only the compiler must not hoist the reads
         __builtin_amdgcn_wave_barrier();
@@ -96,27 +180,25 @@ __global__ __launch_bounds__(kCrcBlock) void crc32c_chunks512(CrcArgs a) {
         const bool live = cstart < a.cell_len;
         const bool full = live && a.cell_len - cstart >= uint64_t(CH);  // same for the chunk's 4 lanes
         uint32_t val = 0;
-        if (full) {
-            uint32_t r = 0;
-            const uint8_t* row = stage + lane * PITCH;
-#pragma unroll
-            for (int t = 0; t < Q / 16; t++) {
-                const u32x4 w = *reinterpret_cast<const u32x4*>(row + t * 16);
-                r = crc_step8(s_tab, r, w.x, w.y);
-                r = crc_step8(s_tab, r, w.z, w.w);
-            }
-            if (qi < 3)
-                r = s_shift[qi][0][r & 0xFF] ^ s_shift[qi][1][(r >> 8) & 0xFF] ^ s_shift[qi][2][(r >> 16) & 0xFF] ^
-                    s_shift[qi][3][r >> 24];
+        if constexpr (SCHEME == 0) {
+            // measurement only: the task's loads + staging, no CRC math
+            val = *reinterpret_cast<const uint32_t*>(stage + lane * PITCH);
+        } else if (full) {
+            uint32_t r;
+            if constexpr (SCHEME == 1)
+                r = quarter_crc_s8(reinterpret_cast<const uint32_t(*)[256]>(s_main), stage + lane * PITCH);
+            else
+                r = quarter_crc_rep<SCHEME>(reinterpret_cast<const uint32_t(*)[32]>(s_main), s_seg,
+                                            stage + lane * PITCH, lane & 31);
+            if (qi < 3) r = apply_shift(s_shift[qi], r);
             val = r;
         } else if (live && qi == 0) {
-            // short last chunk of the cell: this lane walks it whole
+            // short last chunk of the cell: this lane walks it whole, bytewise
             const uint32_t len = uint32_t(a.cell_len - cstart);
             uint32_t r = 0xFFFFFFFFu;
-            for (uint32_t p = 0; p < len; p += 16) {
-                const u32x4 w = *reinterpret_cast<const u32x4*>(stage + (4 * c + p / Q) * PITCH + (p % Q));
-                r = crc_step8(s_tab, r, w.x, w.y);
-                r = crc_step8(s_tab, r, w.z, w.w);
+            for (uint32_t p = 0; p < len; p++) {
+                const uint32_t idx = (r ^ stage[(4 * c + p / Q) * PITCH + (p % Q)]) & 0xFF;
+                r = (SCHEME <= 1 ? s_main[idx] : s_main[idx * 32]) ^ (r >> 8);
             }
             val = ~r;
         }
@@ -124,10 +206,26 @@ __global__ __launch_bounds__(kCrcBlock) void crc32c_chunks512(CrcArgs a) {
         val ^= __shfl_xor(val, 2);
         if (live && qi == 0) {
             const uint32_t crc = full ? (val ^ kfinal) : val;
-            reinterpret_cast<uint32_t*>(a.out)[cell_idx * a.chunks_per_cell + g * CHUNKS_PER_TASK + c] = bswap32(crc);
+            reinterpret_cast<uint32_t*>(a.out)[cell_idx * a.chunks_per_cell + g * 16u + c] = bswap32(crc);
         }
         __builtin_amdgcn_wave_barrier();
         asm volatile("" ::: "memory");
+    };
+
+    // PF register sets in flight: task t's loads are issued while task t-PF
+    // is checksummed
+    uint64_t task = uint64_t(blockIdx.x) * Sh::kWaves + wave;
+    u32x4 va[8], vb[8];
+    if (task < tasks) load_task(a, groups, task, lane, va);
+    if (PF == 2 && task + step < tasks) load_task(a, groups, task + step, lane, vb);
+    while (task < tasks) {
+        run_task(task, va, task + PF * step);
+        task += step;
+        if constexpr (PF == 2) {
+            if (task >= tasks) break;
+            run_task(task, vb, task + 2 * step);
+            task += step;
+        }
     }
 }
 
@@ -159,6 +257,12 @@ int num_cus_for(int dev) {
     return v;
 }
 
+template <int SCHEME>
+const void* crc_fn(int pf) {
+    return pf == 2 ? reinterpret_cast<const void*>(&crc32c_chunks512<SCHEME, 2>)
+                   : reinterpret_cast<const void*>(&crc32c_chunks512<SCHEME, 1>);
+}
+
 }  // namespace
 
 int launch_crc32c(const CrcArgs& in, int device, hipStream_t stream) {
@@ -175,10 +279,17 @@ int launch_crc32c(const CrcArgs& in, int device, hipStream_t stream) {
     if (aligned && a.bytes_per_checksum == 512) {
         a.groups_per_cell = (a.chunks_per_cell + 15) / 16;
         const uint64_t tasks = a.groups_per_cell * a.n_shards * a.stripes;
-        uint64_t grid = (tasks + kWaves - 1) / kWaves;
-        if (grid > uint64_t(cus) * 2) grid = uint64_t(cus) * 2;  // 56 KiB LDS per block: two per CU
-        e = hipLaunchKernel(reinterpret_cast<const void*>(&crc32c_chunks512), dim3(uint32_t(grid)), dim3(kCrcBlock),
-                            args, 0, stream);
+        const int scheme = g_tune_crc_variant == 2 ? 4 : g_tune_crc_variant == 3 ? 8 : g_tune_crc_variant == 9 ? 0 : 1;
+        const int pf = g_tune_crc_prefetch == 1 ? 1 : 2;
+        const int waves = scheme <= 1 ? CrcShape<1>::kWaves : CrcShape<4>::kWaves;
+        const int per_cu = scheme <= 1 ? 2 : 1;  // LDS: 56 KiB / ~144 KiB per block
+        uint64_t grid = (tasks + waves - 1) / waves;
+        if (grid > uint64_t(cus) * per_cu) grid = uint64_t(cus) * per_cu;
+        const void* fn = scheme == 1   ? crc_fn<1>(pf)
+                         : scheme == 4 ? crc_fn<4>(pf)
+                         : scheme == 8 ? crc_fn<8>(pf)
+                                       : crc_fn<0>(pf);
+        e = hipLaunchKernel(fn, dim3(uint32_t(grid)), dim3(uint32_t(waves * 64)), args, 0, stream);
     } else {
         const uint64_t total = a.chunks_per_cell * a.n_shards * a.stripes;
         uint64_t grid = (total + kCrcBlock - 1) / kCrcBlock;

@@ -842,7 +842,11 @@ int hec_encode_crc_device(hec_coder_t* c, const uint8_t* const* d_data, const si
 // 6 = chunk mapping (1 = block slabs, 2 = wave-contiguous runs), 7 = grid size,
 // 8 = tile-order group (stripes interleaved column-major; 1 = stripe-major),
 // 9 = 1: hec_encode_crc_device as two passes (encode, then CRC) instead of fused,
-// 10 = slabs per wave of the fused encode+CRC kernel (0 default, 4 or 8).
+// 10 = slabs per wave of the fused encode+CRC kernel (0 default, 4 or 8),
+// 11 = CRC lookup scheme (0 default, 1 slice-by-8 tables, 2 / 3 bank-replicated
+//      slice-by-1 with 4 / 8 chains per lane; 9 = loads + staging only, WRONG
+//      sums: measures the kernel's memory side),
+// 12 = CRC kernel register prefetch depth in tasks (0 default = 2, 1 or 2).
 int hec_tune_set(int key, int value) {
     switch (key) {
         case 1:
@@ -880,6 +884,14 @@ int hec_tune_set(int key, int value) {
         case 10:
             if (value != 0 && value != 4 && value != 8) return HEC_ERR_INVALID_ARG;
             hec::g_tune_fused_slabs = value;
+            return HEC_OK;
+        case 11:
+            if ((value < 0 || value > 3) && value != 9) return HEC_ERR_INVALID_ARG;
+            hec::g_tune_crc_variant = value;
+            return HEC_OK;
+        case 12:
+            if (value < 0 || value > 2) return HEC_ERR_INVALID_ARG;
+            hec::g_tune_crc_prefetch = value;
             return HEC_OK;
         default: return HEC_ERR_INVALID_ARG;
     }

@@ -83,6 +83,8 @@ extern int g_tune_map;            // 0 = default, 1|2 = chunk mapping 0|1
 extern int g_tune_grid;           // 0 = default, else absolute grid size
 extern int g_tune_group;          // 0 = default, else stripes per tile-order group
 extern int g_tune_crc_unfused;    // 1 = encode + separate CRC pass
+extern int g_tune_crc_variant;    // 0 = default, 1 = slice-by-8, 2/3 = bank-replicated slice-by-1, 4/8 chains
+extern int g_tune_crc_prefetch;   // 0 = default, 1 / 2 tasks of register prefetch (CRC kernel)
 extern int g_tune_fused_slabs;    // 0 = default, else 4 / 8 slabs per wave (fused encode+CRC)
 
 }  // namespace hec

@@ -514,11 +514,20 @@ def _oracle_sums(cells: np.ndarray, bpc: int) -> np.ndarray:
 
 @pytest.mark.parametrize("cell,bpc,n", [(512 * 64, 512, 3), (512 * 70 + 256, 512, 2), (1 << 16, 512, 9),
                                         (4096, 4096, 2), (1000, 512, 3), (3 * 512 + 16, 512, 1), (2048, 100, 2)])
-def test_crc32c_device_vs_oracle(dev, cell, bpc, n):
+@pytest.mark.parametrize("variant,pf", [(0, 0), (1, 1), (2, 2), (3, 1), (3, 2)])
+def test_crc32c_device_vs_oracle(dev, cell, bpc, n, variant, pf):
+    """All CRC lookup schemes (tune key 11) and prefetch depths (key 12)
+    against the oracle."""
     S = 3
     cells = batch_data(S, n, cell, first=cell + bpc)
-    got = H.crc32c_batch(coder(6, 3), torch.from_numpy(cells).to(dev), bpc)
-    torch.cuda.synchronize()
+    H.tune_set(11, variant)
+    H.tune_set(12, pf)
+    try:
+        got = H.crc32c_batch(coder(6, 3), torch.from_numpy(cells).to(dev), bpc)
+        torch.cuda.synchronize()
+    finally:
+        H.tune_set(11, 0)
+        H.tune_set(12, 0)
     assert np.array_equal(got.cpu().numpy(), _oracle_sums(cells, bpc))
 
 
