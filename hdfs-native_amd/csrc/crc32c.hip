@@ -20,19 +20,24 @@
 //     an "append 384/256/128 zero bytes" byte table (CRC is linear over
 //     GF(2)), two XOR shuffles combine the 4 quarters and the init/xorout
 //     constant of a 512-B chunk is folded in.
-// SCHEME 1: slicing-by-8 from 8 KiB of tables, 256-thread blocks, 2 per CU.
-//   Random table indices hit the 32 banks of a ds_read_b32 half-wave ~3-4
-//   ways deep: LDS-array bound (PMC: 85 % busy, 60 % of it conflicts).
+// SCHEME 1 (default): slicing-by-8 from 8 KiB of tables, 256-thread blocks,
+//   2 per CU.  Random table indices hit the 32 banks of a ds_read_b32
+//   half-wave ~3-4 ways deep (PMC: LDS array 85 % busy, 60 % of it conflict
+//   cycles).
 // SCHEME 4 / 8: slicing-by-1 from a table REPLICATED across the 32 banks
 //   (lane l reads column l%32: conflict free), the quarter as 4 / 8
 //   independent segment chains (latency) combined with "append 16*j zero
-//   bytes" tables; 72 KiB of tables, 512-thread blocks, 1 per CU.
+//   bytes" tables; 72 KiB of tables, 512-thread blocks, 1 per CU.  Halves
+//   the LDS-array cycles but not the time: with 2 waves per SIMD the byte
+//   chain's latency, not LDS throughput, sets the pace (all schemes measure
+//   4.6-4.9 TB/s against 6.4 for the kernel's loads alone).
 // No cross-wave traffic and no block barrier after the table prologue.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
 
 #include "crc32c.hpp"
+#include "crc32c_device.hpp"
 #include "crc32c_tables.hpp"
 #include "ec_kernels.hpp"
 
@@ -45,16 +50,6 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 constexpr int kCrcBlock = 256;
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
-
-__device__ __forceinline__ uint32_t crc_step8(const uint32_t (*t)[256], uint32_t crc, uint32_t lo, uint32_t hi) {
-    lo ^= crc;
-    return t[7][lo & 0xFF] ^ t[6][(lo >> 8) & 0xFF] ^ t[5][(lo >> 16) & 0xFF] ^ t[4][lo >> 24] ^
-           t[3][hi & 0xFF] ^ t[2][(hi >> 8) & 0xFF] ^ t[1][(hi >> 16) & 0xFF] ^ t[0][hi >> 24];
-}
-
-__device__ __forceinline__ uint32_t apply_shift(const uint32_t (*t)[256], uint32_t r) {
-    return t[0][r & 0xFF] ^ t[1][(r >> 8) & 0xFF] ^ t[2][(r >> 16) & 0xFF] ^ t[3][r >> 24];
-}
 
 __constant__ crc::Tables kCrcTables = crc::Tables();
 
@@ -78,78 +73,29 @@ __device__ __forceinline__ void load_task(const CrcArgs& a, uint64_t groups, uin
     }
 }
 
-// SCHEME 4 / 8: a 128-B quarter as NCHAIN independent segments of
-// 128/NCHAIN bytes (slicing-by-1, bank-replicated table), combined by the
-// "append 16*(7-i) zero bytes" tables seg[i].
-template <int NCHAIN>
-__device__ __forceinline__ uint32_t quarter_crc_rep(const uint32_t (*rep)[32], const uint32_t (*seg)[4][256],
-                                                    const uint8_t* row, int bank) {
-    static_assert(NCHAIN == 4 || NCHAIN == 8, "4 or 8 chains");
-    constexpr int SEGW = 32 / NCHAIN;  // dwords per segment
-    u32x4 w[8];
-#pragma unroll
-    for (int t = 0; t < 8; t++) w[t] = *reinterpret_cast<const u32x4*>(row + t * 16);
-    uint32_t c[NCHAIN];
-#pragma unroll
-    for (int s = 0; s < NCHAIN; s++) c[s] = 0;
-#pragma unroll
-    for (int d = 0; d < SEGW; d++) {  // dword d of each segment
-#pragma unroll
-        for (int s = 0; s < NCHAIN; s++) {
-            const int dw = s * SEGW + d;
-            c[s] ^= w[dw / 4][dw % 4];
-        }
-#pragma unroll
-        for (int b = 0; b < 4; b++)
-#pragma unroll
-            for (int s = 0; s < NCHAIN; s++) c[s] = rep[c[s] & 0xFF][bank] ^ (c[s] >> 8);
-    }
-    uint32_t q = c[NCHAIN - 1];
-#pragma unroll
-    for (int s = 0; s < NCHAIN - 1; s++) q ^= apply_shift(seg[7 - (NCHAIN - 1 - s) * (8 / NCHAIN)], c[s]);
-    return q;
-}
-
-// SCHEME 1: the quarter with slicing-by-8.
-__device__ __forceinline__ uint32_t quarter_crc_s8(const uint32_t (*tab)[256], const uint8_t* row) {
-    uint32_t r = 0;
-#pragma unroll
-    for (int t = 0; t < 8; t++) {
-        const u32x4 w = *reinterpret_cast<const u32x4*>(row + t * 16);
-        r = crc_step8(tab, r, w.x, w.y);
-        r = crc_step8(tab, r, w.z, w.w);
-    }
-    return r;
-}
-
 template <int SCHEME>
-struct CrcShape {
+struct CrcShape : crcdev::TableLayout<SCHEME> {
     static constexpr int kBlock = SCHEME <= 1 ? 256 : 512;
     static constexpr int kWaves = kBlock / 64;
-    // table words: slice[8][256] | rep[256][32] ; shift[3][4][256] ; seg[7][4][256]
-    static constexpr int kMainWords = SCHEME <= 1 ? 8 * 256 : 256 * 32;
-    static constexpr int kSegWords = SCHEME <= 1 ? 0 : 7 * 4 * 256;
-    static constexpr int kTableWords = kMainWords + 3 * 4 * 256 + kSegWords;
 };
 
 template <int SCHEME, int PF>
 __global__ __launch_bounds__(CrcShape<SCHEME>::kBlock) void crc32c_chunks512(CrcArgs a) {
     using Sh = CrcShape<SCHEME>;
     constexpr int CH = 512, Q = CH / 4, PITCH = Q + 16, STAGE = 64 * PITCH, BS = Sh::kBlock;
-    __shared__ uint32_t s_tables[Sh::kTableWords];
+    __shared__ uint32_t s_tables[Sh::kWords];
     __shared__ __attribute__((aligned(16))) uint8_t s_stage[Sh::kWaves * STAGE];
     uint32_t* s_main = s_tables;
-    const uint32_t(*s_shift)[4][256] = reinterpret_cast<const uint32_t(*)[4][256]>(s_tables + Sh::kMainWords);
-    const uint32_t(*s_seg)[4][256] =
-        reinterpret_cast<const uint32_t(*)[4][256]>(s_tables + Sh::kMainWords + 3 * 4 * 256);
+    const uint32_t(*s_shift)[4][256] = reinterpret_cast<const uint32_t(*)[4][256]>(s_tables + Sh::kShiftOff);
+    const uint32_t(*s_seg)[4][256] = reinterpret_cast<const uint32_t(*)[4][256]>(s_tables + Sh::kSegOff);
     if constexpr (SCHEME <= 1) {
         for (int t = threadIdx.x; t < 8 * 256; t += BS) s_main[t] = (&kCrcTables.slice[0][0])[t];
     } else {
         for (int t = threadIdx.x; t < 256 * 32; t += BS) s_main[t] = kCrcTables.slice[0][t / 32];
         for (int t = threadIdx.x; t < 7 * 4 * 256; t += BS)
-            s_tables[Sh::kMainWords + 3 * 4 * 256 + t] = (&kCrcTables.seg[0][0][0])[t];
+            s_tables[Sh::kSegOff + t] = (&kCrcTables.seg[0][0][0])[t];
     }
-    for (int t = threadIdx.x; t < 3 * 4 * 256; t += BS) s_tables[Sh::kMainWords + t] = (&kCrcTables.shift[0][0][0])[t];
+    for (int t = threadIdx.x; t < 3 * 4 * 256; t += BS) s_tables[Sh::kShiftOff + t] = (&kCrcTables.shift[0][0][0])[t];
     __syncthreads();
     const uint32_t kfinal = kCrcTables.final512;
 
@@ -186,11 +132,11 @@ __global__ __launch_bounds__(CrcShape<SCHEME>::kBlock) void crc32c_chunks512(Crc
         } else if (full) {
             uint32_t r;
             if constexpr (SCHEME == 1)
-                r = quarter_crc_s8(reinterpret_cast<const uint32_t(*)[256]>(s_main), stage + lane * PITCH);
+                r = crcdev::quarter_s8(reinterpret_cast<const uint32_t(*)[256]>(s_main), stage + lane * PITCH);
             else
-                r = quarter_crc_rep<SCHEME>(reinterpret_cast<const uint32_t(*)[32]>(s_main), s_seg,
-                                            stage + lane * PITCH, lane & 31);
-            if (qi < 3) r = apply_shift(s_shift[qi], r);
+                r = crcdev::quarter_rep<SCHEME>(reinterpret_cast<const uint32_t(*)[32]>(s_main), s_seg,
+                                                stage + lane * PITCH, lane & 31);
+            if (qi < 3) r = crcdev::apply_shift(s_shift[qi], r);
             val = r;
         } else if (live && qi == 0) {
             // short last chunk of the cell: this lane walks it whole, bytewise
@@ -279,6 +225,9 @@ int launch_crc32c(const CrcArgs& in, int device, hipStream_t stream) {
     if (aligned && a.bytes_per_checksum == 512) {
         a.groups_per_cell = (a.chunks_per_cell + 15) / 16;
         const uint64_t tasks = a.groups_per_cell * a.n_shards * a.stripes;
+        // default: slicing-by-8, 2 tasks of prefetch.  Interleaved A/B
+        // (profiles/r01_probe_crc.log): 4.91 TB/s vs 4.80 (replicated, 4
+        // chains) and 4.64 (8 chains); the memory side alone reaches 6.4.
         const int scheme = g_tune_crc_variant == 2 ? 4 : g_tune_crc_variant == 3 ? 8 : g_tune_crc_variant == 9 ? 0 : 1;
         const int pf = g_tune_crc_prefetch == 1 ? 1 : 2;
         const int waves = scheme <= 1 ? CrcShape<1>::kWaves : CrcShape<4>::kWaves;

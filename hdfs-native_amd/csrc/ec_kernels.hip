@@ -26,6 +26,7 @@
 #include <cstdint>
 
 #include "crc32c.hpp"
+#include "crc32c_device.hpp"
 #include "crc32c_tables.hpp"
 #include "ec_kernels.hpp"
 #include "gf256.hpp"
@@ -577,12 +578,6 @@ __global__ __launch_bounds__(BS) void gf_decode_mixed(MixedArgs a) {
 // ---------------------------------------------------------------------------
 namespace {
 __constant__ crc::Tables kFusedCrcTables = crc::Tables();
-
-__device__ __forceinline__ uint32_t crc8(const uint32_t (*t)[256], uint32_t crc, uint32_t lo, uint32_t hi) {
-    lo ^= crc;
-    return t[7][lo & 0xFF] ^ t[6][(lo >> 8) & 0xFF] ^ t[5][(lo >> 16) & 0xFF] ^ t[4][lo >> 24] ^
-           t[3][hi & 0xFF] ^ t[2][(hi >> 8) & 0xFF] ^ t[1][(hi >> 16) & 0xFF] ^ t[0][hi >> 24];
-}
 }  // namespace
 
 // Layout: a wave owns SLABS KiB (SLABS slabs of 1 KiB, one 16-B load per
@@ -594,24 +589,32 @@ __device__ __forceinline__ uint32_t crc8(const uint32_t (*t)[256], uint32_t crc,
 // SLABS = 8 (one shard per round) when the r x 8 accumulators fit 2 waves
 // per SIMD, else 4 (two shards per round; an odd k + r leaves one
 // half-empty round).  9 KiB of image per wave -> 8 waves per CU.
-template <int K, int R, int SLABS>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void gf_encode_crc(MatmulArgs a,
-                                                                                              uint8_t* sums) {
-    constexpr int BS = 256, PITCH = 144, STAGE = 64 * PITCH, SPR = 8 / SLABS;
-    constexpr uint32_t WAVE_BYTES = SLABS * 1024u, TILE_BYTES = 4 * WAVE_BYTES;
+template <int K, int R, int SLABS, int SCHEME>
+__global__ __launch_bounds__(SCHEME == 1 ? 256 : 512) __attribute__((amdgpu_waves_per_eu(2, 2))) void gf_encode_crc(
+    MatmulArgs a, uint8_t* sums) {
+    using TL = crcdev::TableLayout<SCHEME>;
+    constexpr int BS = SCHEME == 1 ? 256 : 512, WAVES = BS / 64;
+    constexpr int PITCH = 144, STAGE = 64 * PITCH, SPR = 8 / SLABS;
+    constexpr uint32_t WAVE_BYTES = SLABS * 1024u, TILE_BYTES = WAVES * WAVE_BYTES;
     constexpr bool PF = R * SLABS <= 24;  // register prefetch of the next shard
     __shared__ PermTable s_tab[R][kMaxK];
     __shared__ uint8_t s_exp[512];
     __shared__ uint8_t s_log[256];
     __shared__ uint8_t s_coef[R * kMaxK];
-    __shared__ uint32_t s_ctab[8][256];
-    __shared__ uint32_t s_shift[3][4][256];
-    __shared__ __attribute__((aligned(16))) uint8_t s_stage[4 * STAGE];
+    __shared__ uint32_t s_ctabs[TL::kWords];
+    __shared__ __attribute__((aligned(16))) uint8_t s_stage[WAVES * STAGE];
     prologue<R, BS>(a, K, s_tab, s_exp, s_log, s_coef);
-    for (int t = threadIdx.x; t < 8 * 256; t += BS) (&s_ctab[0][0])[t] = (&kFusedCrcTables.slice[0][0])[t];
-    for (int t = threadIdx.x; t < 3 * 4 * 256; t += BS) (&s_shift[0][0][0])[t] = (&kFusedCrcTables.shift[0][0][0])[t];
+    if constexpr (SCHEME == 1) {
+        for (int t = threadIdx.x; t < 8 * 256; t += BS) s_ctabs[t] = (&kFusedCrcTables.slice[0][0])[t];
+    } else {
+        for (int t = threadIdx.x; t < 256 * 32; t += BS) s_ctabs[t] = kFusedCrcTables.slice[0][t / 32];
+        for (int t = threadIdx.x; t < 7 * 4 * 256; t += BS) s_ctabs[TL::kSegOff + t] = (&kFusedCrcTables.seg[0][0][0])[t];
+    }
+    for (int t = threadIdx.x; t < 3 * 4 * 256; t += BS) s_ctabs[TL::kShiftOff + t] = (&kFusedCrcTables.shift[0][0][0])[t];
     __syncthreads();
     const uint32_t kfinal = kFusedCrcTables.final512;
+    const uint32_t(*s_shift)[4][256] = reinterpret_cast<const uint32_t(*)[4][256]>(s_ctabs + TL::kShiftOff);
+    const uint32_t(*s_seg)[4][256] = reinterpret_cast<const uint32_t(*)[4][256]>(s_ctabs + TL::kSegOff);
 
     const uint64_t cell_len = a.cell_len;
     const uint64_t nck = (cell_len + 511) / 512;  // CRC chunks per cell
@@ -649,25 +652,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             const bool live_c = in_cell && sir < count;
             uint32_t val = 0;
             if (full && sir < count) {
-                uint32_t r = 0;
-                const uint8_t* row = stage + lane * PITCH;
-#pragma unroll
-                for (int t = 0; t < 8; t++) {
-                    const u32x4 w = *reinterpret_cast<const u32x4*>(row + t * 16);
-                    r = crc8(s_ctab, r, w.x, w.y);
-                    r = crc8(s_ctab, r, w.z, w.w);
-                }
-                if (qi < 3)
-                    r = s_shift[qi][0][r & 0xFF] ^ s_shift[qi][1][(r >> 8) & 0xFF] ^
-                        s_shift[qi][2][(r >> 16) & 0xFF] ^ s_shift[qi][3][r >> 24];
+                uint32_t r;
+                if constexpr (SCHEME == 1)
+                    r = crcdev::quarter_s8(reinterpret_cast<const uint32_t(*)[256]>(s_ctabs), stage + lane * PITCH);
+                else
+                    r = crcdev::quarter_rep<SCHEME>(reinterpret_cast<const uint32_t(*)[32]>(s_ctabs), s_seg,
+                                                    stage + lane * PITCH, lane & 31);
+                if (qi < 3) r = crcdev::apply_shift(s_shift[qi], r);
                 val = r;
             } else if (live_c && qi == 0) {
+                // short last chunk of the cell: this lane walks it whole, bytewise
                 const uint32_t len = uint32_t(cell_len - cbyte);
                 uint32_t r = 0xFFFFFFFFu;
-                for (uint32_t b = 0; b < len; b += 16) {
-                    const u32x4 w = *reinterpret_cast<const u32x4*>(stage + (lane + b / 128) * PITCH + (b % 128));
-                    r = crc8(s_ctab, r, w.x, w.y);
-                    r = crc8(s_ctab, r, w.z, w.w);
+                for (uint32_t b = 0; b < len; b++) {
+                    const uint32_t idx = (r ^ stage[(lane + b / 128) * PITCH + (b % 128)]) & 0xFF;
+                    r = (SCHEME == 1 ? s_ctabs[idx] : s_ctabs[idx * 32]) ^ (r >> 8);
                 }
                 val = ~r;
             }
@@ -1056,18 +1055,21 @@ namespace {
 constexpr int fused_slabs(int k, int r) { return (r <= 3 && k <= 6) ? 8 : 4; }
 
 template <int K, int R>
-const void* fused_fn(int slabs) {
-    if (slabs == 4) return reinterpret_cast<const void*>(&gf_encode_crc<K, R, 4>);
-    return reinterpret_cast<const void*>(&gf_encode_crc<K, R, 8>);
+const void* fused_fn(int slabs, int scheme) {
+    if (scheme == 1)
+        return slabs == 4 ? reinterpret_cast<const void*>(&gf_encode_crc<K, R, 4, 1>)
+                          : reinterpret_cast<const void*>(&gf_encode_crc<K, R, 8, 1>);
+    return slabs == 4 ? reinterpret_cast<const void*>(&gf_encode_crc<K, R, 4, 4>)
+                      : reinterpret_cast<const void*>(&gf_encode_crc<K, R, 8, 4>);
 }
 
 template <int K>
-const void* fused_pick_r(int r, int slabs) {
+const void* fused_pick_r(int r, int slabs, int scheme) {
     switch (r) {
-        case 1: return fused_fn<K, 1>(slabs);
-        case 2: return fused_fn<K, 2>(slabs);
-        case 3: return fused_fn<K, 3>(slabs);
-        default: return fused_fn<K, 4>(slabs);
+        case 1: return fused_fn<K, 1>(slabs, scheme);
+        case 2: return fused_fn<K, 2>(slabs, scheme);
+        case 3: return fused_fn<K, 3>(slabs, scheme);
+        default: return fused_fn<K, 4>(slabs, scheme);
     }
 }
 }  // namespace
@@ -1080,17 +1082,19 @@ int launch_encode_crc(const MatmulArgs& in, uint8_t* sums, int device, hipStream
     for (int j = 0; j < a.r; j++)
         aligned &= ((reinterpret_cast<uintptr_t>(a.out[j]) | a.out_stride[j]) & 15u) == 0;
     const int slabs = (g_tune_fused_slabs == 4 || g_tune_fused_slabs == 8) ? g_tune_fused_slabs : fused_slabs(a.k, a.r);
+    const int scheme = g_tune_crc_variant == 1 ? 1 : 4;  // CRC lookups (crc32c_device.hpp)
+    const int waves = scheme == 1 ? 4 : 8;
     const void* fn = nullptr;
     switch (a.k) {
-        case 2: fn = fused_pick_r<2>(a.r, slabs); break;
-        case 3: fn = fused_pick_r<3>(a.r, slabs); break;
-        case 6: fn = fused_pick_r<6>(a.r, slabs); break;
-        case 10: fn = fused_pick_r<10>(a.r, slabs); break;
+        case 2: fn = fused_pick_r<2>(a.r, slabs, scheme); break;
+        case 3: fn = fused_pick_r<3>(a.r, slabs, scheme); break;
+        case 6: fn = fused_pick_r<6>(a.r, slabs, scheme); break;
+        case 10: fn = fused_pick_r<10>(a.r, slabs, scheme); break;
         default: return -1;
     }
     if (!aligned) return -1;
     const uint64_t chunks = a.cell_len / 16;
-    const uint64_t tile_bytes = 4096u * uint64_t(slabs);  // 4 waves x slabs x 1 KiB
+    const uint64_t tile_bytes = 1024u * uint64_t(slabs) * uint64_t(waves);  // 4 waves x slabs x 1 KiB
     const uint64_t tps = (a.cell_len + tile_bytes - 1) / tile_bytes;
     const uint64_t total = tps * a.stripes;
     if (chunks > 0xFFFFFFFFull || total > 0xFFFFFFFFull) return -1;
@@ -1099,10 +1103,11 @@ int launch_encode_crc(const MatmulArgs& in, uint8_t* sums, int device, hipStream
     a.tiles_per_stripe = uint32_t(tps);
     a.total_tiles = uint32_t(total);
     a.group = g_tune_group > 0 ? uint32_t(g_tune_group) : 4u;
-    uint64_t grid = uint64_t(num_cus(device)) * 2;  // ~60 KiB LDS per block: two per CU
+    // LDS: ~61 KiB per 256-thread block (two per CU) / ~131 KiB per 512-thread block (one)
+    uint64_t grid = uint64_t(num_cus(device)) * (scheme == 1 ? 2 : 1);
     if (grid > total) grid = total;
     void* args[] = {&a, &sums};
-    const hipError_t e = hipLaunchKernel(fn, dim3(uint32_t(grid)), dim3(256), args, 0, stream);
+    const hipError_t e = hipLaunchKernel(fn, dim3(uint32_t(grid)), dim3(uint32_t(waves * 64)), args, 0, stream);
     return e == hipSuccess ? 0 : int(e);
 }
 

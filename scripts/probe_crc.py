@@ -1,7 +1,9 @@
-"""Measurement tool (GPU box): CRC32C-per-chunk kernel variants on 9 x 1 MiB
-cells x S stripes.  Prints ms and TB/s per variant (tune key 11), and is the
-target of scripts/pmc_crc.sh (PMC counters per kernel name)."""
+"""Measurement tool (GPU box): CRC32C-per-chunk kernel variants (tune key 11
+scheme x key 12 prefetch) on 9 x 1 MiB cells x S stripes, interleaved over
+ROUNDS rounds so clock/thermal drift hits every variant alike; prints the
+median per variant.  Also the target of scripts/pmc_crc.sh."""
 import os
+import statistics
 import sys
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "hdfs-native_amd"))
@@ -11,27 +13,32 @@ import hdfs_native_ec as H  # noqa: E402
 
 S = int(os.environ.get("PROBE_STRIPES", "256"))
 REPS = int(os.environ.get("PROBE_REPS", "10"))
+ROUNDS = int(os.environ.get("PROBE_ROUNDS", "5"))
 n, cell = 9, 1 << 20
 dev = torch.device("cuda:0")
 cells = torch.empty((S, n, cell), dtype=torch.uint8, device=dev)
 cells.random_(0, 256, generator=torch.Generator(device=dev).manual_seed(1))
 coder = H.Coder(6, 3, 0)
-ref = None
-for variant, pf in [(v, p) for v in (1, 2, 3, 9) for p in (1, 2)]:
-    H.tune_set(11, variant)
-    H.tune_set(12, pf)
-    out = H.crc32c_batch(coder, cells)
-    torch.cuda.synchronize()
-    if ref is None:
-        ref = out
-    assert variant == 9 or torch.equal(out, ref), f"variant {variant} mismatch"
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-    ev[0].record()
-    for _ in range(REPS):
-        H.crc32c_batch(coder, cells)
-    ev[1].record()
-    torch.cuda.synchronize()
-    ms = ev[0].elapsed_time(ev[1]) / REPS
-    print(f"variant {variant} prefetch {pf}: {ms:.3f} ms  {n * cell * S / ms / 1e9:.2f} TB/s")
+variants = [(v, p) for v in (1, 2, 3, 9) for p in (1, 2)]
+ref = H.crc32c_batch(coder, cells)
+times = {v: [] for v in variants}
+for _ in range(ROUNDS):
+    for variant, pf in variants:
+        H.tune_set(11, variant)
+        H.tune_set(12, pf)
+        out = H.crc32c_batch(coder, cells)
+        torch.cuda.synchronize()
+        assert variant == 9 or torch.equal(out, ref), f"variant {variant} mismatch"
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        ev[0].record()
+        for _ in range(REPS):
+            H.crc32c_batch(coder, cells)
+        ev[1].record()
+        torch.cuda.synchronize()
+        times[(variant, pf)].append(ev[0].elapsed_time(ev[1]) / REPS)
 H.tune_set(11, 0)
 H.tune_set(12, 0)
+for (variant, pf), t in times.items():
+    ms = statistics.median(t)
+    print(f"variant {variant} prefetch {pf}: median {ms:.3f} ms  {n * cell * S / ms / 1e9:.2f} TB/s  "
+          f"(min {min(t):.3f} max {max(t):.3f})")
