@@ -48,7 +48,9 @@ def parse():
     ap.add_argument("--global-stripes", type=int, default=0,
                     help="split this many stripes across the ranks instead (strong scaling)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="also time the oracle stripe-parallel on T threads")
+    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0),
+                    help="also time the oracle stripe-parallel on T threads (default $OMP_NUM_THREADS: the "
+                         "box's CPU share; 0/1 = single-threaded only)")
     ap.add_argument("--host-path", action="store_true", help="also measure the pinned H2D+encode+D2H pipeline")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--tune", default="", help="key=value,... passed to hec_tune_set (measurement)")
@@ -63,10 +65,30 @@ def parse():
     return ap.parse_args()
 
 
+def host_info():
+    """CPU model and core counts of the host the baseline ran on (§8d)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count()
+    return {"cpu_model": model, "nproc": os.cpu_count(), "usable_cpus": usable}
+
+
 def cpu_baseline(k, m, cell, seconds, threads=1):
     """Times the C restatement of the reference loop (oracle, matrix.rs:204-231
     order) on the host: encode + decode({0..m-1} missing) of 1-stripe calls,
-    the same work as one Coder::encode + Coder::decode per stripe."""
+    the same work as one Coder::encode + Coder::decode per stripe.  With
+    threads > 1 every thread codes its own stripe buffers (stripe-parallel,
+    ctypes releases the GIL around each call)."""
     import ctypes
 
     import numpy as np
@@ -74,18 +96,22 @@ def cpu_baseline(k, m, cell, seconds, threads=1):
     import ec_oracle
     from hdfs_native_ec.synth import batch_data
     lib = ec_oracle.load_c_oracle()
-    data = batch_data(1, k, cell)[0]
-    par = np.empty((m, cell), dtype=np.uint8)
-    rec = np.empty((k, cell), dtype=np.uint8)
-    ins = (ctypes.c_void_p * k)(*[data[i].ctypes.data for i in range(k)])
-    outs = (ctypes.c_void_p * m)(*[par[j].ctypes.data for j in range(m)])
-    shards = (ctypes.c_void_p * (k + m))(*([0] * m + [data[i].ctypes.data for i in range(m, k)] +
-                                            [par[j].ctypes.data for j in range(m)]))
-    recs = (ctypes.c_void_p * (k + m))(*([rec[i].ctypes.data for i in range(k)] + [0] * m))
+    bufs = []
+    for t in range(threads):
+        data = batch_data(1, k, cell, first=t)[0]
+        par = np.empty((m, cell), dtype=np.uint8)
+        rec = np.empty((k, cell), dtype=np.uint8)
+        ins = (ctypes.c_void_p * k)(*[data[i].ctypes.data for i in range(k)])
+        outs = (ctypes.c_void_p * m)(*[par[j].ctypes.data for j in range(m)])
+        shards = (ctypes.c_void_p * (k + m))(*([0] * m + [data[i].ctypes.data for i in range(m, k)] +
+                                                [par[j].ctypes.data for j in range(m)]))
+        recs = (ctypes.c_void_p * (k + m))(*([rec[i].ctypes.data for i in range(k)] + [0] * m))
+        bufs.append((data, par, rec, ins, outs, shards, recs))
     counts = [0] * threads
     stop = time.perf_counter() + seconds
 
     def work(t):
+        _, _, _, ins, outs, shards, recs = bufs[t]
         while time.perf_counter() < stop:
             lib.orc_encode(k, m, ins, cell, outs)
             lib.orc_decode(k, m, shards, cell, recs)
@@ -98,11 +124,14 @@ def cpu_baseline(k, m, cell, seconds, threads=1):
     for th in ths:
         th.join()
     el = time.perf_counter() - t0
-    assert np.array_equal(rec[:m], data[:m]), "cpu baseline decode mismatch"
+    for data, _, rec, *_ in bufs:
+        assert np.array_equal(rec[:m], data[:m]), "cpu baseline decode mismatch"
     n = sum(counts)
     return {"value": round(2 * n * k * cell / GIB / el, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
-            "sample": f"{n} x (encode + decode 0..{m - 1} missing) of one RS({k},{m}) stripe, {cell} B cells, "
-                      f"{el:.1f} s, C restatement oracle/ec_oracle.c (reference Rust path unbuildable here)"}
+            "sample": f"{n} x (encode + decode 0..{m - 1} missing) of one RS({k},{m}) stripe per thread, "
+                      f"{cell} B cells, {el:.1f} s on {threads} thread(s), C restatement oracle/ec_oracle.c "
+                      f"(reference Rust path unbuildable here)",
+            "host": host_info()}
 
 
 def main():
