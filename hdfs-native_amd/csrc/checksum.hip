@@ -1,12 +1,15 @@
-// crc32c.hip -- CRC32C per checksum chunk on gfx950.
+// checksum.hip -- per-chunk checksums on gfx950.
 //
-// Reference: every DataTransferProtocol packet carries one CRC32C per
-// bytes_per_checksum chunk of its data (WritePacket::calculate_checksum,
-// rust/src/hdfs/connection.rs:568-584; verified on read in
-// ReadPacket::get_data, :477-504).  CRC32C = crc 3.4 CRC_32_ISCSI
-// (connection.rs:37-38): reflected poly 0x82F63B78, init/xorout 0xFFFFFFFF,
-// emitted big-endian (put_u32).  Shards are written as whole cells, so the
-// chunks of a cell are exactly the chunks of its block stream.
+// Reference: every DataTransferProtocol packet carries one checksum per
+// bytes_per_checksum chunk of its data: CRC32C on write
+// (WritePacket::calculate_checksum, rust/src/hdfs/connection.rs:568-584),
+// CRC32C or CRC32 verified on read (ReadPacket::get_data, :477-504; a
+// mismatch is HdfsError::ChecksumError).  CRC32C = crc 3.4 CRC_32_ISCSI,
+// CRC32 = CRC_32_CKSUM (connection.rs:37-38; parameters in
+// checksum_tables.hpp); sums are big-endian (put_u32 / get_u32).  Shards
+// are written as whole cells, so the chunks of a cell are exactly the
+// chunks of its block stream.  Compute mode writes the sums; verify mode
+// compares them with the expected sums and flags the cell.
 //
 // Fast kernel (512-B chunks): a wave owns 16 consecutive chunks (8 KiB) of
 // one cell ("task") and each lane a QUARTER chunk (128 B):
@@ -36,9 +39,9 @@
 
 #include <cstdint>
 
-#include "crc32c.hpp"
-#include "crc32c_device.hpp"
-#include "crc32c_tables.hpp"
+#include "checksum.hpp"
+#include "checksum_device.hpp"
+#include "checksum_tables.hpp"
 #include "ec_kernels.hpp"
 
 namespace hec {
@@ -51,7 +54,29 @@ constexpr int kCrcBlock = 256;
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
-__constant__ crc::Tables kCrcTables = crc::Tables();
+__constant__ crc::Tables<crc::kCrc32c> kTablesCrc32c = crc::Tables<crc::kCrc32c>();
+__constant__ crc::Tables<crc::kCksum> kTablesCksum = crc::Tables<crc::kCksum>();
+
+template <int KIND>
+__device__ __forceinline__ const crc::Tables<KIND>& tables() {
+    if constexpr (KIND == crc::kCrc32c)
+        return kTablesCrc32c;
+    else
+        return kTablesCksum;
+}
+
+// Compute mode: store the big-endian sum.  Verify mode: flag the cell on a
+// mismatch (every flagging lane stores the same byte).
+__device__ __forceinline__ void emit_sum(const CrcArgs& a, uint64_t cell_idx, uint64_t chunk, uint32_t crc) {
+    const uint64_t stripe = cell_idx / a.n_shards;
+    const uint64_t cell = stripe * a.n_total + a.sid[cell_idx - stripe * a.n_shards];
+    const uint64_t at = cell * a.chunks_per_cell + chunk;
+    if (a.expected) {
+        if (reinterpret_cast<const uint32_t*>(a.expected)[at] != bswap32(crc)) a.bad[cell] = 1;
+    } else {
+        reinterpret_cast<uint32_t*>(a.out)[at] = bswap32(crc);
+    }
+}
 
 // One wave's task: 16 chunks (8 KiB) of one cell, 8 coalesced 1-KiB loads.
 // `task` is wave-uniform (scalar base/stride loads); the loads are
@@ -79,25 +104,19 @@ struct CrcShape : crcdev::TableLayout<SCHEME> {
     static constexpr int kWaves = kBlock / 64;
 };
 
-template <int SCHEME, int PF>
-__global__ __launch_bounds__(CrcShape<SCHEME>::kBlock) void crc32c_chunks512(CrcArgs a) {
+template <int KIND, int SCHEME, int PF>
+__global__ __launch_bounds__(CrcShape<SCHEME>::kBlock) void checksum_chunks512(CrcArgs a) {
     using Sh = CrcShape<SCHEME>;
+    using Spec = crc::Spec<KIND>;
+    constexpr bool REFL = Spec::kReflected;
     constexpr int CH = 512, Q = CH / 4, PITCH = Q + 16, STAGE = 64 * PITCH, BS = Sh::kBlock;
     __shared__ uint32_t s_tables[Sh::kWords];
     __shared__ __attribute__((aligned(16))) uint8_t s_stage[Sh::kWaves * STAGE];
     uint32_t* s_main = s_tables;
     const uint32_t(*s_shift)[4][256] = reinterpret_cast<const uint32_t(*)[4][256]>(s_tables + Sh::kShiftOff);
-    const uint32_t(*s_seg)[4][256] = reinterpret_cast<const uint32_t(*)[4][256]>(s_tables + Sh::kSegOff);
-    if constexpr (SCHEME <= 1) {
-        for (int t = threadIdx.x; t < 8 * 256; t += BS) s_main[t] = (&kCrcTables.slice[0][0])[t];
-    } else {
-        for (int t = threadIdx.x; t < 256 * 32; t += BS) s_main[t] = kCrcTables.slice[0][t / 32];
-        for (int t = threadIdx.x; t < 7 * 4 * 256; t += BS)
-            s_tables[Sh::kSegOff + t] = (&kCrcTables.seg[0][0][0])[t];
-    }
-    for (int t = threadIdx.x; t < 3 * 4 * 256; t += BS) s_tables[Sh::kShiftOff + t] = (&kCrcTables.shift[0][0][0])[t];
+    crcdev::stage_tables<SCHEME, BS>(s_tables, tables<KIND>());
     __syncthreads();
-    const uint32_t kfinal = kCrcTables.final512;
+    const uint32_t kfinal = tables<KIND>().final512;
 
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / 64), lane = threadIdx.x & 63;
     const int qi = lane & 3, c = lane >> 2;  // quarter, chunk within the task
@@ -130,30 +149,20 @@ __global__ __launch_bounds__(CrcShape<SCHEME>::kBlock) void crc32c_chunks512(Crc
             // measurement only: the task's loads + staging, no CRC math
             val = *reinterpret_cast<const uint32_t*>(stage + lane * PITCH);
         } else if (full) {
-            uint32_t r;
-            if constexpr (SCHEME == 1)
-                r = crcdev::quarter_s8(reinterpret_cast<const uint32_t(*)[256]>(s_main), stage + lane * PITCH);
-            else
-                r = crcdev::quarter_rep<SCHEME>(reinterpret_cast<const uint32_t(*)[32]>(s_main), s_seg,
-                                                stage + lane * PITCH, lane & 31);
+            uint32_t r = crcdev::quarter<SCHEME, REFL>(s_main, stage + lane * PITCH, lane);
             if (qi < 3) r = crcdev::apply_shift(s_shift[qi], r);
             val = r;
         } else if (live && qi == 0) {
             // short last chunk of the cell: this lane walks it whole, bytewise
             const uint32_t len = uint32_t(a.cell_len - cstart);
-            uint32_t r = 0xFFFFFFFFu;
-            for (uint32_t p = 0; p < len; p++) {
-                const uint32_t idx = (r ^ stage[(4 * c + p / Q) * PITCH + (p % Q)]) & 0xFF;
-                r = (SCHEME <= 1 ? s_main[idx] : s_main[idx * 32]) ^ (r >> 8);
-            }
-            val = ~r;
+            uint32_t r = Spec::kInit;
+            for (uint32_t p = 0; p < len; p++)
+                r = crcdev::byte_step<REFL, (SCHEME <= 1 ? 1 : 32)>(s_main, r, stage[(4 * c + p / Q) * PITCH + (p % Q)]);
+            val = r ^ Spec::kXorout;
         }
         val ^= __shfl_xor(val, 1);
         val ^= __shfl_xor(val, 2);
-        if (live && qi == 0) {
-            const uint32_t crc = full ? (val ^ kfinal) : val;
-            reinterpret_cast<uint32_t*>(a.out)[cell_idx * a.chunks_per_cell + g * 16u + c] = bswap32(crc);
-        }
+        if (live && qi == 0) emit_sum(a, cell_idx, g * 16u + c, full ? (val ^ kfinal) : val);
         __builtin_amdgcn_wave_barrier();
         asm volatile("" ::: "memory");
     };
@@ -177,9 +186,11 @@ __global__ __launch_bounds__(CrcShape<SCHEME>::kBlock) void crc32c_chunks512(Crc
 
 // Generic path: any chunk size / alignment.  One lane per chunk, bytes from
 // global memory, slice-by-1.
-__global__ __launch_bounds__(kCrcBlock) void crc32c_chunks_bytes(CrcArgs a) {
-    __shared__ uint32_t s_tab[8][256];
-    for (int t = threadIdx.x; t < 8 * 256; t += kCrcBlock) (&s_tab[0][0])[t] = (&kCrcTables.slice[0][0])[t];
+template <int KIND>
+__global__ __launch_bounds__(kCrcBlock) void checksum_chunks_bytes(CrcArgs a) {
+    using Spec = crc::Spec<KIND>;
+    __shared__ uint32_t s_tab[256];
+    for (int t = threadIdx.x; t < 256; t += kCrcBlock) s_tab[t] = tables<KIND>().slice[0][t];
     __syncthreads();
     const uint64_t total = a.chunks_per_cell * a.n_shards * a.stripes;
     for (uint64_t gidx = uint64_t(blockIdx.x) * kCrcBlock + threadIdx.x; gidx < total;
@@ -191,9 +202,9 @@ __global__ __launch_bounds__(kCrcBlock) void crc32c_chunks_bytes(CrcArgs a) {
         const uint8_t* p = a.base[shard] + stripe * a.stride[shard] + chunk * a.bytes_per_checksum;
         const uint64_t cs = chunk * a.bytes_per_checksum;
         const uint64_t len = a.cell_len - cs < a.bytes_per_checksum ? a.cell_len - cs : a.bytes_per_checksum;
-        uint32_t crc = 0xFFFFFFFFu;
-        for (uint64_t i = 0; i < len; i++) crc = s_tab[0][(crc ^ p[i]) & 0xFF] ^ (crc >> 8);
-        reinterpret_cast<uint32_t*>(a.out)[gidx] = bswap32(~crc);
+        uint32_t crc = Spec::kInit;
+        for (uint64_t i = 0; i < len; i++) crc = crcdev::byte_step<Spec::kReflected, 1>(s_tab, crc, p[i]);
+        emit_sum(a, cell_idx, chunk, crc ^ Spec::kXorout);
     }
 }
 
@@ -203,17 +214,30 @@ int num_cus_for(int dev) {
     return v;
 }
 
-template <int SCHEME>
+template <int KIND, int SCHEME>
 const void* crc_fn(int pf) {
-    return pf == 2 ? reinterpret_cast<const void*>(&crc32c_chunks512<SCHEME, 2>)
-                   : reinterpret_cast<const void*>(&crc32c_chunks512<SCHEME, 1>);
+    return pf == 2 ? reinterpret_cast<const void*>(&checksum_chunks512<KIND, SCHEME, 2>)
+                   : reinterpret_cast<const void*>(&checksum_chunks512<KIND, SCHEME, 1>);
+}
+
+template <int KIND>
+const void* crc_pick(int scheme, int pf) {
+    return scheme == 1   ? crc_fn<KIND, 1>(pf)
+           : scheme == 4 ? crc_fn<KIND, 4>(pf)
+           : scheme == 8 ? crc_fn<KIND, 8>(pf)
+                         : crc_fn<KIND, 0>(pf);
 }
 
 }  // namespace
 
-int launch_crc32c(const CrcArgs& in, int device, hipStream_t stream) {
+int launch_checksum(const CrcArgs& in, int device, hipStream_t stream) {
     CrcArgs a = in;
     if (a.bytes_per_checksum == 0 || a.cell_len == 0 || a.n_shards == 0) return -1;
+    if (a.kind != crc::kCrc32c && a.kind != crc::kCksum) return -1;
+    if (a.expected && !a.bad) return -1;
+    if (a.n_shards > uint32_t(kCrcMaxShards) || a.n_total < a.n_shards) return -1;
+    for (uint32_t i = 0; i < a.n_shards; i++)
+        if (a.sid[i] >= a.n_total) return -1;
     a.chunks_per_cell = (a.cell_len + a.bytes_per_checksum - 1) / a.bytes_per_checksum;
     if (a.stripes == 0) return 0;
     bool aligned = a.cell_len % 16 == 0 && (reinterpret_cast<uintptr_t>(a.out) & 3u) == 0;
@@ -234,17 +258,15 @@ int launch_crc32c(const CrcArgs& in, int device, hipStream_t stream) {
         const int per_cu = scheme <= 1 ? 2 : 1;  // LDS: 56 KiB / ~144 KiB per block
         uint64_t grid = (tasks + waves - 1) / waves;
         if (grid > uint64_t(cus) * per_cu) grid = uint64_t(cus) * per_cu;
-        const void* fn = scheme == 1   ? crc_fn<1>(pf)
-                         : scheme == 4 ? crc_fn<4>(pf)
-                         : scheme == 8 ? crc_fn<8>(pf)
-                                       : crc_fn<0>(pf);
+        const void* fn = a.kind == crc::kCrc32c ? crc_pick<crc::kCrc32c>(scheme, pf) : crc_pick<crc::kCksum>(scheme, pf);
         e = hipLaunchKernel(fn, dim3(uint32_t(grid)), dim3(uint32_t(waves * 64)), args, 0, stream);
     } else {
         const uint64_t total = a.chunks_per_cell * a.n_shards * a.stripes;
         uint64_t grid = (total + kCrcBlock - 1) / kCrcBlock;
         if (grid > uint64_t(cus) * 4) grid = uint64_t(cus) * 4;
-        e = hipLaunchKernel(reinterpret_cast<const void*>(&crc32c_chunks_bytes), dim3(uint32_t(grid)),
-                            dim3(kCrcBlock), args, 0, stream);
+        const void* fn = a.kind == crc::kCrc32c ? reinterpret_cast<const void*>(&checksum_chunks_bytes<crc::kCrc32c>)
+                                                : reinterpret_cast<const void*>(&checksum_chunks_bytes<crc::kCksum>);
+        e = hipLaunchKernel(fn, dim3(uint32_t(grid)), dim3(kCrcBlock), args, 0, stream);
     }
     return e == hipSuccess ? 0 : int(e);
 }

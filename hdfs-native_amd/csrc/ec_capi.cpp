@@ -22,7 +22,8 @@
 #include <vector>
 
 #include "../../include/hdfs_ec_amd.h"
-#include "crc32c.hpp"
+#include "checksum.hpp"
+#include "checksum_tables.hpp"
 #include "ec_kernels.hpp"
 #include "gf256.hpp"
 
@@ -200,6 +201,7 @@ const char* hec_strerror(int status) {
         case HEC_ERR_DEVICE: return "HIP device error";
         case HEC_ERR_NO_MEMORY: return "out of memory";
         case HEC_ERR_SINGULAR: return "Matrix is singular";
+        case HEC_ERR_CHECKSUM: return "checksum error";
         default: return "unknown status";
     }
 }
@@ -754,12 +756,51 @@ int hec_decode_host_batch(hec_coder_t* c, const uint8_t* const* h_vertical, size
     });
 }
 
-// ---- CRC32C per checksum chunk -------------------------
+// ---- Chunk checksums ------------------------------------
 
-int hec_crc32c_device(hec_coder_t* c, const uint8_t* const* d_bases, const size_t* strides, size_t n_shards,
-                      size_t cell_len, size_t stripes, size_t bytes_per_checksum, uint8_t* d_out, void* hip_stream) {
-    if (!c || !d_bases || !strides || !d_out || n_shards == 0 || n_shards > size_t(hec::kCrcMaxShards) ||
-        cell_len == 0 || bytes_per_checksum == 0)
+namespace {
+
+// HEC_CHECKSUM_* (ChecksumTypeProto) -> crc::Kind; -1 for NULL / invalid
+int crc_kind(int checksum_type) {
+    switch (checksum_type) {
+        case HEC_CHECKSUM_CRC32C: return hec::crc::kCrc32c;
+        case HEC_CHECKSUM_CRC32: return hec::crc::kCksum;
+        default: return -1;
+    }
+}
+
+// One checksum launch over n_shards cells per stripe; cell (s, i) sits at
+// s * n_total + sid[i] in the sums/flags layouts (sid == nullptr: identity).
+int checksum_launch(hec_coder* c, int kind, const uint8_t* const* bases, const size_t* strides, const uint8_t* sid,
+                    size_t n_shards, size_t n_total, size_t cell_len, size_t stripes, size_t bpc, uint8_t* out,
+                    const uint8_t* expected, uint8_t* bad, hipStream_t stream) {
+    hec::CrcArgs a;
+    std::memset(&a, 0, sizeof(a));
+    for (size_t i = 0; i < n_shards; i++) {
+        if (!bases[i]) return HEC_ERR_INVALID_ARG;
+        a.base[i] = bases[i];
+        a.stride[i] = strides[i];
+        a.sid[i] = uint8_t(sid ? sid[i] : i);
+    }
+    a.n_total = uint32_t(n_total);
+    a.out = out;
+    a.expected = expected;
+    a.bad = bad;
+    a.kind = kind;
+    a.n_shards = uint32_t(n_shards);
+    a.cell_len = cell_len;
+    a.stripes = stripes;
+    a.bytes_per_checksum = bpc;
+    const int rc = hec::launch_checksum(a, c->device, stream);
+    return rc == 0 ? HEC_OK : to_status(rc);
+}
+
+int checksum_entry(hec_coder* c, int checksum_type, const uint8_t* const* d_bases, const size_t* strides,
+                   size_t n_shards, size_t cell_len, size_t stripes, size_t bpc, uint8_t* d_out,
+                   const uint8_t* d_expected, uint8_t* d_bad, void* hip_stream) {
+    const int kind = crc_kind(checksum_type);
+    if (!c || !d_bases || !strides || kind < 0 || n_shards == 0 || n_shards > size_t(hec::kCrcMaxShards) ||
+        cell_len == 0 || bpc == 0 || (!d_out && !d_expected) || (d_expected && !d_bad))
         return HEC_ERR_INVALID_ARG;
     for (size_t i = 0; i < n_shards; i++)
         if (!d_bases[i]) return HEC_ERR_INVALID_ARG;
@@ -767,20 +808,36 @@ int hec_crc32c_device(hec_coder_t* c, const uint8_t* const* d_bases, const size_
     return guarded([&] {
         DeviceGuard g(c->device);
         if (!g.ok) return fail(HEC_ERR_DEVICE, "hipSetDevice", hipErrorInvalidDevice);
-        hec::CrcArgs a;
-        std::memset(&a, 0, sizeof(a));
-        for (size_t i = 0; i < n_shards; i++) {
-            a.base[i] = d_bases[i];
-            a.stride[i] = strides[i];
-        }
-        a.out = d_out;
-        a.n_shards = uint32_t(n_shards);
-        a.cell_len = cell_len;
-        a.stripes = stripes;
-        a.bytes_per_checksum = bytes_per_checksum;
-        const int rc = hec::launch_crc32c(a, c->device, static_cast<hipStream_t>(hip_stream));
-        return rc == 0 ? HEC_OK : to_status(rc);
+        return checksum_launch(c, kind, d_bases, strides, nullptr, n_shards, n_shards, cell_len, stripes, bpc, d_out,
+                               d_expected, d_bad, static_cast<hipStream_t>(hip_stream));
     });
+}
+
+}  // namespace
+
+int hec_crc32c_device(hec_coder_t* c, const uint8_t* const* d_bases, const size_t* strides, size_t n_shards,
+                      size_t cell_len, size_t stripes, size_t bytes_per_checksum, uint8_t* d_out, void* hip_stream) {
+    if (!d_out) return HEC_ERR_INVALID_ARG;
+    return checksum_entry(c, HEC_CHECKSUM_CRC32C, d_bases, strides, n_shards, cell_len, stripes, bytes_per_checksum,
+                          d_out, nullptr, nullptr, hip_stream);
+}
+
+int hec_checksum_device(hec_coder_t* c, int checksum_type, const uint8_t* const* d_bases, const size_t* strides,
+                        size_t n_shards, size_t cell_len, size_t stripes, size_t bytes_per_checksum, uint8_t* d_out,
+                        void* hip_stream) {
+    if (!d_out) return HEC_ERR_INVALID_ARG;
+    return checksum_entry(c, checksum_type, d_bases, strides, n_shards, cell_len, stripes, bytes_per_checksum, d_out,
+                          nullptr, nullptr, hip_stream);
+}
+
+int hec_checksum_verify_device(hec_coder_t* c, int checksum_type, const uint8_t* const* d_bases,
+                               const size_t* strides, size_t n_shards, size_t cell_len, size_t stripes,
+                               size_t bytes_per_checksum, const uint8_t* d_expected, uint8_t* d_bad,
+                               void* hip_stream) {
+    if (checksum_type == HEC_CHECKSUM_NULL) return c ? HEC_OK : HEC_ERR_INVALID_ARG;
+    if (!d_expected || !d_bad) return HEC_ERR_INVALID_ARG;
+    return checksum_entry(c, checksum_type, d_bases, strides, n_shards, cell_len, stripes, bytes_per_checksum,
+                          nullptr, d_expected, d_bad, hip_stream);
 }
 
 int hec_encode_crc_device(hec_coder_t* c, const uint8_t* const* d_data, const size_t* data_strides,
@@ -813,7 +870,13 @@ int hec_encode_crc_device(hec_coder_t* c, const uint8_t* const* d_data, const si
             a.r = int32_t(c->m);
             a.cell_len = cell_len;
             a.stripes = stripes;
-            const int lrc = hec::launch_encode_crc(a, d_sums, c->device, static_cast<hipStream_t>(hip_stream));
+            hec::FusedCrcArgs cs;
+            std::memset(&cs, 0, sizeof(cs));
+            cs.sums = d_sums;
+            cs.n_total = uint32_t(c->k + c->m);
+            cs.kind = hec::crc::kCrc32c;
+            for (size_t i = 0; i < c->k + c->m; i++) cs.shard_id[i] = uint8_t(i);
+            const int lrc = hec::launch_encode_crc(a, cs, c->device, static_cast<hipStream_t>(hip_stream));
             if (lrc == -1) return 1;  // shape not covered: fall through
             return lrc == 0 ? int(HEC_OK) : to_status(lrc);
         });
@@ -832,6 +895,164 @@ int hec_encode_crc_device(hec_coder_t* c, const uint8_t* const* d_data, const si
         st[c->k + j] = parity_strides[j];
     }
     return hec_crc32c_device(c, bases, st, c->k + c->m, cell_len, stripes, bytes_per_checksum, d_sums, hip_stream);
+}
+
+// The verified striped read (block_reader.rs:480-525 -> ec_decode): phase 1
+// verifies the batch plan's survivors of every stripe and rebuilds its
+// missing data in one pass; phase 2 re-plans, one stripe at a time, the
+// stripes where a survivor failed: drop it, take the next available shard
+// (verifying it first, as read_slice starts the next parity reader), and
+// rebuild every missing or failed data cell of that stripe.
+int hec_decode_verify_device(hec_coder_t* c, int checksum_type, const uint8_t* const* d_shards,
+                             const size_t* shard_strides, uint8_t* const* d_out, const size_t* out_strides,
+                             size_t cell_len, size_t stripes, size_t bytes_per_checksum, const uint8_t* d_sums,
+                             uint8_t* d_bad, void* hip_stream) {
+    if (!c || !d_shards || !shard_strides || !d_out || !out_strides || cell_len == 0) return HEC_ERR_INVALID_ARG;
+    if (checksum_type == HEC_CHECKSUM_NULL)
+        return hec_decode_device(c, d_shards, shard_strides, d_out, out_strides, cell_len, stripes, hip_stream);
+    const int kind = crc_kind(checksum_type);
+    if (kind < 0 || bytes_per_checksum == 0 || !d_sums || !d_bad) return HEC_ERR_INVALID_ARG;
+    for (size_t i = 0; i < c->k; i++)
+        if (!d_out[i]) return HEC_ERR_INVALID_ARG;
+    if (stripes == 0) return HEC_OK;
+    return guarded([&]() -> int {
+        const size_t k = c->k, n = c->k + c->m;
+        const hipStream_t stream = static_cast<hipStream_t>(hip_stream);
+        uint8_t present[HEC_MAX_DATA_UNITS + HEC_MAX_PARITY_UNITS];
+        for (size_t i = 0; i < n; i++) present[i] = d_shards[i] != nullptr;
+        const DecodePlan& p = cached_plan(c, present);
+        if (p.status != HEC_OK) return p.status;  // fewer than k available: nothing is read
+        std::vector<size_t> surv = p.survivors;
+        if (p.missing.empty())
+            for (size_t i = 0; i < k; i++) surv.push_back(i);  // nothing to rebuild: the data cells are read
+        DeviceGuard g(c->device);
+        if (!g.ok) return fail(HEC_ERR_DEVICE, "hipSetDevice", hipErrorInvalidDevice);
+        HEC_HIP(hipMemsetAsync(d_bad, 0, stripes * n, stream), HEC_ERR_DEVICE);
+
+        // ---- phase 1: the whole batch under the batch plan
+        const uint8_t* in[HEC_MAX_DATA_UNITS];
+        size_t ist[HEC_MAX_DATA_UNITS];
+        uint8_t sid[HEC_MAX_DATA_UNITS];
+        for (size_t r = 0; r < k; r++) {
+            in[r] = d_shards[surv[r]];
+            ist[r] = shard_strides[surv[r]];
+            sid[r] = uint8_t(surv[r]);
+        }
+        bool fused = false;
+        if (!p.missing.empty() && p.missing.size() <= size_t(hec::kMaxR) && bytes_per_checksum == 512) {
+            hec::MatmulArgs a;
+            std::memset(&a, 0, sizeof(a));
+            for (size_t r = 0; r < k; r++) {
+                a.in[r] = in[r];
+                a.in_stride[r] = ist[r];
+            }
+            for (size_t j = 0; j < p.missing.size(); j++) {
+                a.out[j] = d_out[p.missing[j]];
+                a.out_stride[j] = out_strides[p.missing[j]];
+                for (size_t i = 0; i < k; i++) a.coef[j * hec::kMaxK + i] = p.matrix[j * k + i];
+            }
+            a.k = int32_t(k);
+            a.r = int32_t(p.missing.size());
+            a.cell_len = cell_len;
+            a.stripes = stripes;
+            hec::FusedCrcArgs cs;
+            std::memset(&cs, 0, sizeof(cs));
+            cs.expected = d_sums;
+            cs.bad = d_bad;
+            cs.n_total = uint32_t(n);
+            cs.kind = kind;
+            for (size_t r = 0; r < k; r++) cs.shard_id[r] = sid[r];
+            const int lrc = hec::launch_decode_verify(a, cs, c->device, stream);
+            if (lrc > 0) return to_status(lrc);
+            fused = lrc == 0;
+        }
+        if (!fused) {
+            int rc = checksum_launch(c, kind, in, ist, sid, k, n, cell_len, stripes, bytes_per_checksum, nullptr,
+                                     d_sums, d_bad, stream);
+            if (rc != HEC_OK) return rc;
+            if (!p.missing.empty()) {
+                uint8_t* out[HEC_MAX_DATA_UNITS];
+                size_t ost[HEC_MAX_DATA_UNITS];
+                for (size_t j = 0; j < p.missing.size(); j++) {
+                    out[j] = d_out[p.missing[j]];
+                    ost[j] = out_strides[p.missing[j]];
+                }
+                rc = matmul_batch(c->device, p.matrix.data(), p.missing.size(), k, in, ist, out, ost, cell_len, stripes,
+                                  stream);
+                if (rc != HEC_OK) return rc;
+            }
+        }
+        std::vector<uint8_t> bad(stripes * n);
+        HEC_HIP(hipMemcpyAsync(bad.data(), d_bad, bad.size(), hipMemcpyDeviceToHost, stream), HEC_ERR_DEVICE);
+        HEC_HIP(hipStreamSynchronize(stream), HEC_ERR_DEVICE);
+
+        // ---- phase 2: stripes with a failed survivor, one at a time
+        int status = HEC_OK;
+        for (size_t s = 0; s < stripes; s++) {
+            uint8_t* row = &bad[s * n];
+            bool any = false;
+            for (size_t r = 0; r < k; r++) any |= row[surv[r]] != 0;
+            if (!any) continue;
+            uint8_t ok[HEC_MAX_DATA_UNITS + HEC_MAX_PARITY_UNITS] = {};  // verified good
+            for (size_t r = 0; r < k; r++) ok[surv[r]] = row[surv[r]] == 0;
+            uint8_t avail[HEC_MAX_DATA_UNITS + HEC_MAX_PARITY_UNITS];
+            bool enough = true;
+            for (;;) {
+                // the first k available shards that have not failed
+                std::vector<size_t> pick, todo;
+                for (size_t i = 0; i < n; i++) {
+                    avail[i] = present[i] && !row[i];
+                    if (avail[i] && pick.size() < k) pick.push_back(i);
+                }
+                if (pick.size() < k) {
+                    enough = false;
+                    break;
+                }
+                for (size_t i : pick)
+                    if (!ok[i]) todo.push_back(i);
+                if (todo.empty()) break;
+                const uint8_t* tb[HEC_MAX_DATA_UNITS + HEC_MAX_PARITY_UNITS];
+                size_t ts[HEC_MAX_DATA_UNITS + HEC_MAX_PARITY_UNITS];
+                uint8_t tid[HEC_MAX_DATA_UNITS + HEC_MAX_PARITY_UNITS];
+                for (size_t t = 0; t < todo.size(); t++) {
+                    tb[t] = d_shards[todo[t]] + s * shard_strides[todo[t]];
+                    ts[t] = 0;
+                    tid[t] = uint8_t(todo[t]);
+                }
+                const size_t nck = (cell_len + bytes_per_checksum - 1) / bytes_per_checksum;
+                const int rc = checksum_launch(c, kind, tb, ts, tid, todo.size(), n, cell_len, 1, bytes_per_checksum,
+                                               nullptr, d_sums + s * n * nck * 4, d_bad + s * n, stream);
+                if (rc != HEC_OK) return rc;
+                HEC_HIP(hipMemcpyAsync(row, d_bad + s * n, n, hipMemcpyDeviceToHost, stream), HEC_ERR_DEVICE);
+                HEC_HIP(hipStreamSynchronize(stream), HEC_ERR_DEVICE);
+                for (size_t i : todo) ok[i] = row[i] == 0;
+            }
+            if (!enough) {
+                status = HEC_ERR_NOT_ENOUGH_SHARDS;
+                continue;
+            }
+            const DecodePlan& q = cached_plan(c, avail);
+            if (q.status != HEC_OK) return q.status;
+            if (q.missing.empty()) continue;
+            const uint8_t* qin[HEC_MAX_DATA_UNITS];
+            size_t qst[HEC_MAX_DATA_UNITS];
+            uint8_t* qout[HEC_MAX_DATA_UNITS];
+            size_t qost[HEC_MAX_DATA_UNITS];
+            for (size_t r = 0; r < k; r++) {
+                qin[r] = d_shards[q.survivors[r]] + s * shard_strides[q.survivors[r]];
+                qst[r] = 0;
+            }
+            for (size_t j = 0; j < q.missing.size(); j++) {
+                qout[j] = d_out[q.missing[j]] + s * out_strides[q.missing[j]];
+                qost[j] = 0;
+            }
+            const int rc = matmul_batch(c->device, q.matrix.data(), q.missing.size(), k, qin, qst, qout, qost, cell_len,
+                                        1, stream);
+            if (rc != HEC_OK) return rc;
+        }
+        HEC_HIP(hipStreamSynchronize(stream), HEC_ERR_DEVICE);
+        return status;
+    });
 }
 
 // Tuning knobs for the measurement harness (not part of the reference API).

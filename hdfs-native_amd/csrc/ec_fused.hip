@@ -1,0 +1,328 @@
+// ec_fused.hip -- the GF(2^8) stripe multiply fused with the per-chunk
+// checksums of the cells it streams, so that a striped
+// write or read touches HBM once:
+//   * encode: parity of the k data cells plus the CRC32C of all k+m cells
+//     (CellBuffer::encode, block_writer.rs:817-851, feeding k+m packet
+//     streams whose WritePacket::calculate_checksum, connection.rs:568-584,
+//     puts one CRC32C per 512-B chunk);
+//   * decode + verify: the read side (block_reader.rs:480-525 -> ec_decode):
+//     the k survivors' chunk checksums (CRC32C or CRC32 = CRC_32_CKSUM,
+//     ReadPacket::get_data, connection.rs:477-504) are checked against the
+//     sums that came with their packets while the missing data cells are
+//     rebuilt from the same registers; a mismatch flags the cell
+//     (HdfsError::ChecksumError), and the host re-plans that stripe.
+// Register GF math as in gf_matmul_v16 (ec_kernels.hip); each wave drops its
+// 1-KiB pieces -- each exactly two chunk-aligned 512-B chunks -- into a
+// wave-private LDS image of 144-B quarter rows and runs the quarter-chunk
+// checksum of checksum.hip over it in rounds of 64 quarters.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "checksum.hpp"
+#include "checksum_device.hpp"
+#include "checksum_tables.hpp"
+#include "ec_kernels.hpp"
+#include "gf_device.hpp"
+
+namespace hec {
+
+namespace {
+__constant__ crc::Tables<crc::kCrc32c> kFusedCrc32c = crc::Tables<crc::kCrc32c>();
+__constant__ crc::Tables<crc::kCksum> kFusedCksum = crc::Tables<crc::kCksum>();
+
+template <int KIND>
+__device__ __forceinline__ const crc::Tables<KIND>& fused_tables() {
+    if constexpr (KIND == crc::kCrc32c)
+        return kFusedCrc32c;
+    else
+        return kFusedCksum;
+}
+}  // namespace
+
+// Layout: a wave owns SLABS KiB (SLABS slabs of 1 KiB, one 16-B load per
+// lane per slab) of every cell of its stripe; one checksum round is 64
+// quarters = 8 pieces = 8/SLABS shards' share, over a 9-KiB image (as in
+// checksum.hip).  Inputs stream shard by shard (the next one prefetched
+// into registers when the budget allows) while being accumulated into the
+// r output registers and staged for the round; then (encode) each parity
+// shard is stored and staged, or (VERIFY) each rebuilt cell is only stored.
+// SLABS = 8 (one shard per round) when the r x 8 accumulators fit 2 waves
+// per SIMD, else 4 (two shards per round; an odd shard count leaves one
+// half-empty round).  9 KiB of image per wave -> 8 waves per CU.
+//   encode (VERIFY = false): checksummed shards 0..K+R-1 = inputs then
+//     outputs; sums[(stripe * n_total + shard_id[s]) * nck + chunk].
+//   VERIFY: checksummed shards 0..K-1 = the survivors; their expected sums
+//     sit at the same index (shard_id = survivor shard numbers), a mismatch
+//     sets bad[stripe * n_total + shard_id[s]].
+template <int K, int R, int SLABS, int SCHEME, int KIND, bool VERIFY>
+__global__ __launch_bounds__(SCHEME == 1 ? 256 : 512) __attribute__((amdgpu_waves_per_eu(2, 2))) void gf_fused_crc(
+    MatmulArgs a, FusedCrcArgs cs) {
+    using TL = crcdev::TableLayout<SCHEME>;
+    using Spec = crc::Spec<KIND>;
+    constexpr bool REFL = Spec::kReflected;
+    constexpr int BS = SCHEME == 1 ? 256 : 512, WAVES = BS / 64;
+    constexpr int PITCH = 144, STAGE = 64 * PITCH, SPR = 8 / SLABS;
+    constexpr int NSUM = VERIFY ? K : K + R;  // checksummed shards
+    constexpr uint32_t WAVE_BYTES = SLABS * 1024u, TILE_BYTES = WAVES * WAVE_BYTES;
+    constexpr bool PF = R * SLABS <= 24;  // register prefetch of the next shard
+    __shared__ PermTable s_tab[R][kMaxK];
+    __shared__ uint8_t s_exp[512];
+    __shared__ uint8_t s_log[256];
+    __shared__ uint8_t s_coef[R * kMaxK];
+    __shared__ uint32_t s_ctabs[TL::kWords];
+    __shared__ __attribute__((aligned(16))) uint8_t s_stage[WAVES * STAGE];
+    prologue<R, BS>(a, K, s_tab, s_exp, s_log, s_coef);
+    crcdev::stage_tables<SCHEME, BS>(s_ctabs, fused_tables<KIND>());
+    __syncthreads();
+    const uint32_t kfinal = fused_tables<KIND>().final512;
+    const uint32_t(*s_shift)[4][256] = reinterpret_cast<const uint32_t(*)[4][256]>(s_ctabs + TL::kShiftOff);
+
+    const uint64_t cell_len = a.cell_len;
+    const uint64_t nck = (cell_len + 511) / 512;  // checksum chunks per cell
+    const uint32_t total = a.total_tiles;
+    const int wave = threadIdx.x / 64, lane = threadIdx.x & 63;
+    // this lane's quarter in a round: row `lane` = piece lane/8 = (shard
+    // slot sir, slab), chunk half (lane/4)&1 of that slab, quarter qi
+    const int qi = lane & 3, piece = lane >> 3, sir = piece / SLABS, pslab = piece % SLABS, half = (lane >> 2) & 1;
+    uint8_t* stage = s_stage + wave * STAGE;
+    uint32_t* out_sums = reinterpret_cast<uint32_t*>(cs.sums);
+    const uint32_t* exp_sums = reinterpret_cast<const uint32_t*>(cs.expected);
+
+    for (uint32_t tile = blockIdx.x; tile < total; tile += gridDim.x) {
+        uint32_t stripe, tcol;
+        tile_coords(tile, a, stripe, tcol);
+        const uint64_t wbyte = uint64_t(tcol) * TILE_BYTES + uint64_t(wave) * WAVE_BYTES;  // wave's first byte
+        if (wbyte >= cell_len) continue;  // wave-uniform
+        // 32-bit lane offsets from a wave-uniform per-shard base (saddr +
+        // voffset addressing); dead slabs of a short last tile read slab 0
+        const uint64_t left = cell_len - wbyte;
+        uint32_t voff[SLABS];
+        bool live[SLABS];
+#pragma unroll
+        for (int u = 0; u < SLABS; u++) {
+            const uint32_t o = uint32_t(u) * 1024u + uint32_t(lane) * 16u;
+            live[u] = o < left;
+            voff[u] = live[u] ? o : 0u;
+        }
+        const uint64_t cbyte = wbyte + uint64_t(pslab) * 1024u + uint64_t(half) * 512u;
+        const bool in_cell = cbyte < cell_len;
+        const bool full = in_cell && cell_len - cbyte >= 512u;  // same for a chunk's 4 lanes
+
+        // `first` is a compile-time constant at every (unrolled) call site,
+        // so the shard ids are scalar kernarg reads
+        auto sum_cell = [&](int first) {
+            const uint32_t sid = (SPR > 1 && sir > 0 && first + 1 < NSUM) ? cs.shard_id[first + 1] : cs.shard_id[first];
+            return uint64_t(stripe) * cs.n_total + sid;
+        };
+        auto crc_round = [&](int first, int count) {
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("" ::: "memory");
+            const bool live_c = in_cell && sir < count;
+            uint32_t want = 0;
+            if (VERIFY && live_c && qi == 0) want = exp_sums[sum_cell(first) * nck + cbyte / 512];  // issued before the lookups
+            uint32_t val = 0;
+            if (full && sir < count) {
+                uint32_t r = crcdev::quarter<SCHEME, REFL>(s_ctabs, stage + lane * PITCH, lane);
+                if (qi < 3) r = crcdev::apply_shift(s_shift[qi], r);
+                val = r;
+            } else if (live_c && qi == 0) {
+                // short last chunk of the cell: this lane walks it whole, bytewise
+                const uint32_t len = uint32_t(cell_len - cbyte);
+                uint32_t r = Spec::kInit;
+                for (uint32_t b = 0; b < len; b++)
+                    r = crcdev::byte_step<REFL, (SCHEME == 1 ? 1 : 32)>(s_ctabs, r,
+                                                                       stage[(lane + b / 128) * PITCH + (b % 128)]);
+                val = r ^ Spec::kXorout;
+            }
+            val ^= __shfl_xor(val, 1);
+            val ^= __shfl_xor(val, 2);
+            if (live_c && qi == 0) {
+                const uint32_t be = __builtin_bswap32(full ? (val ^ kfinal) : val);
+                if constexpr (VERIFY) {
+                    if (be != want) cs.bad[sum_cell(first)] = 1;
+                } else {
+                    out_sums[sum_cell(first) * nck + cbyte / 512] = be;
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("" ::: "memory");
+        };
+        // slab u of the shard in round slot `slot`: lane l's 16 B -> row
+        // 8*(slot*SLABS + u) + l/8, byte 16*(l%8)
+        auto stage_piece = [&](int slot, int u, const u32x4& v) {
+            *reinterpret_cast<u32x4*>(stage + (8 * (slot * SLABS + u) + lane / 8) * PITCH + 16 * (lane % 8)) = v;
+        };
+        auto after_stage = [&](int shard) {
+            if (shard % SPR == SPR - 1 || shard == NSUM - 1) crc_round(shard - shard % SPR, shard % SPR + 1);
+        };
+
+        u32x4 acc[SLABS][R];
+#pragma unroll
+        for (int u = 0; u < SLABS; u++)
+#pragma unroll
+            for (int j = 0; j < R; j++) acc[u][j] = u32x4{0, 0, 0, 0};
+        u32x4 x[SLABS], xn[SLABS];
+#pragma unroll
+        for (int u = 0; u < SLABS; u++) x[u] = load16<true>(a.in[0] + (uint64_t(stripe) * a.in_stride[0] + wbyte) + voff[u]);
+#pragma unroll
+        for (int i = 0; i < K; i++) {
+            if (PF && i + 1 < K) {
+#pragma unroll
+                for (int u = 0; u < SLABS; u++)
+                    xn[u] = load16<true>(a.in[i + 1] + (uint64_t(stripe) * a.in_stride[i + 1] + wbyte) + voff[u]);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < SLABS; u++) stage_piece(i % SPR, u, x[u]);
+            // opaque per-input table offset threaded through the
+            // accumulators: keeps the table reads (and the GF math) of input
+            // i from being hoisted next to those of the other inputs
+            uint32_t toff = uint32_t(i) * uint32_t(sizeof(PermTable));
+            asm volatile("" : "+v"(toff));
+#pragma unroll
+            for (int u = 0; u < SLABS; u++) {
+                asm volatile("" : "+v"(x[u]));
+#pragma unroll
+                for (int j = 0; j < R; j++) asm volatile("" : "+v"(acc[u][j]) : "v"(toff));
+            }
+            uint32_t tb[R][5];
+#pragma unroll
+            for (int j = 0; j < R; j++) {
+                const PermTable& t =
+                    *reinterpret_cast<const PermTable*>(reinterpret_cast<const char*>(&s_tab[j][0]) + toff);
+                tb[j][0] = t.t0lo;
+                tb[j][1] = t.t0hi;
+                tb[j][2] = t.t1lo;
+                tb[j][3] = t.t1hi;
+                tb[j][4] = t.t2;
+            }
+#pragma unroll
+            for (int u = 0; u < SLABS; u++)
+#pragma unroll
+                for (int d = 0; d < 4; d++) {
+                    const Sel sl = make_sel(x[u][d]);
+#pragma unroll
+                    for (int j = 0; j < R; j++)
+                        acc[u][j][d] ^= gf_mul4(tb[j][0], tb[j][1], tb[j][2], tb[j][3], tb[j][4], sl.s0, sl.s1, sl.s2);
+                }
+            __builtin_amdgcn_sched_barrier(0);
+            after_stage(i);
+            __builtin_amdgcn_sched_barrier(0);
+            if (i + 1 < K) {
+#pragma unroll
+                for (int u = 0; u < SLABS; u++)
+                    x[u] = PF ? xn[u]
+                              : load16<true>(a.in[i + 1] + (uint64_t(stripe) * a.in_stride[i + 1] + wbyte) + voff[u]);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < R; j++) {
+#pragma unroll
+            for (int u = 0; u < SLABS; u++) {
+                if (live[u]) store16<true>(a.out[j] + (uint64_t(stripe) * a.out_stride[j] + wbyte) + voff[u], acc[u][j]);
+                if constexpr (!VERIFY) stage_piece((K + j) % SPR, u, acc[u][j]);
+            }
+            if constexpr (!VERIFY) after_stage(K + j);
+        }
+    }
+}
+
+namespace {
+
+int g_cus[64] = {0};
+
+int cus_of(int dev) {
+    if (dev < 0 || dev >= 64) return 256;
+    if (!g_cus[dev]) {
+        int v = 0;
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+        g_cus[dev] = v;
+    }
+    return g_cus[dev];
+}
+
+// 8 slabs per wave while the r x 8 accumulators fit (k <= 6, r <= 3), else 4
+constexpr int fused_slabs(int k, int r) { return (r <= 3 && k <= 6) ? 8 : 4; }
+
+template <int K, int R>
+const void* encode_fn(int slabs, int scheme) {
+    if (scheme == 1)
+        return slabs == 4 ? reinterpret_cast<const void*>(&gf_fused_crc<K, R, 4, 1, crc::kCrc32c, false>)
+                          : reinterpret_cast<const void*>(&gf_fused_crc<K, R, 8, 1, crc::kCrc32c, false>);
+    return slabs == 4 ? reinterpret_cast<const void*>(&gf_fused_crc<K, R, 4, 4, crc::kCrc32c, false>)
+                      : reinterpret_cast<const void*>(&gf_fused_crc<K, R, 8, 4, crc::kCrc32c, false>);
+}
+
+// verify: default slabs and lookup scheme only, both checksum kinds
+template <int K, int R>
+const void* verify_fn(int kind) {
+    constexpr int SL = fused_slabs(K, R);
+    return kind == crc::kCrc32c ? reinterpret_cast<const void*>(&gf_fused_crc<K, R, SL, 4, crc::kCrc32c, true>)
+                                : reinterpret_cast<const void*>(&gf_fused_crc<K, R, SL, 4, crc::kCksum, true>);
+}
+
+template <int K>
+const void* pick_r(bool verify, int r, int slabs, int scheme, int kind) {
+    switch (r) {
+        case 1: return verify ? verify_fn<K, 1>(kind) : encode_fn<K, 1>(slabs, scheme);
+        case 2: return verify ? verify_fn<K, 2>(kind) : encode_fn<K, 2>(slabs, scheme);
+        case 3: return verify ? verify_fn<K, 3>(kind) : encode_fn<K, 3>(slabs, scheme);
+        default: return verify ? verify_fn<K, 4>(kind) : encode_fn<K, 4>(slabs, scheme);
+    }
+}
+
+int launch_fused(const MatmulArgs& in, const FusedCrcArgs& cs, bool verify, int device, hipStream_t stream) {
+    MatmulArgs a = in;
+    const void* sums = verify ? static_cast<const void*>(cs.expected) : static_cast<const void*>(cs.sums);
+    bool aligned = a.cell_len % 16 == 0 && sums && (reinterpret_cast<uintptr_t>(sums) & 3u) == 0 && a.r >= 1 &&
+                   a.r <= kMaxR && (!verify || cs.bad);
+    for (int i = 0; i < a.k; i++)
+        aligned &= ((reinterpret_cast<uintptr_t>(a.in[i]) | a.in_stride[i]) & 15u) == 0;
+    for (int j = 0; j < a.r; j++)
+        aligned &= ((reinterpret_cast<uintptr_t>(a.out[j]) | a.out_stride[j]) & 15u) == 0;
+    if (cs.kind != crc::kCrc32c && (cs.kind != crc::kCksum || !verify)) return -1;
+    const int slabs = verify                                               ? fused_slabs(a.k, a.r)
+                      : (g_tune_fused_slabs == 4 || g_tune_fused_slabs == 8) ? g_tune_fused_slabs
+                                                                             : fused_slabs(a.k, a.r);
+    const int scheme = (!verify && g_tune_crc_variant == 1) ? 1 : 4;  // checksum lookups (checksum_device.hpp)
+    const int waves = scheme == 1 ? 4 : 8;
+    const void* fn = nullptr;
+    switch (a.k) {
+        case 2: fn = pick_r<2>(verify, a.r, slabs, scheme, cs.kind); break;
+        case 3: fn = pick_r<3>(verify, a.r, slabs, scheme, cs.kind); break;
+        case 6: fn = pick_r<6>(verify, a.r, slabs, scheme, cs.kind); break;
+        case 10: fn = pick_r<10>(verify, a.r, slabs, scheme, cs.kind); break;
+        default: return -1;
+    }
+    if (!aligned) return -1;
+    const uint64_t chunks = a.cell_len / 16;
+    const uint64_t tile_bytes = 1024u * uint64_t(slabs) * uint64_t(waves);  // waves x slabs x 1 KiB
+    const uint64_t tps = (a.cell_len + tile_bytes - 1) / tile_bytes;
+    const uint64_t total = tps * a.stripes;
+    if (chunks > 0xFFFFFFFFull || total > 0xFFFFFFFFull) return -1;
+    if (total == 0) return 0;
+    a.chunks = uint32_t(chunks);
+    a.tiles_per_stripe = uint32_t(tps);
+    a.total_tiles = uint32_t(total);
+    a.group = g_tune_group > 0 ? uint32_t(g_tune_group) : 4u;
+    // LDS: ~61 KiB per 256-thread block (two per CU) / ~131 KiB per 512-thread block (one)
+    uint64_t grid = uint64_t(cus_of(device)) * (scheme == 1 ? 2 : 1);
+    if (grid > total) grid = total;
+    FusedCrcArgs c = cs;
+    void* args[] = {&a, &c};
+    const hipError_t e = hipLaunchKernel(fn, dim3(uint32_t(grid)), dim3(uint32_t(waves * 64)), args, 0, stream);
+    return e == hipSuccess ? 0 : int(e);
+}
+
+}  // namespace
+
+int launch_encode_crc(const MatmulArgs& a, const FusedCrcArgs& c, int device, hipStream_t stream) {
+    return launch_fused(a, c, false, device, stream);
+}
+
+int launch_decode_verify(const MatmulArgs& a, const FusedCrcArgs& c, int device, hipStream_t stream) {
+    return launch_fused(a, c, true, device, stream);
+}
+
+}  // namespace hec

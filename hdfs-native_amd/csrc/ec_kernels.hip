@@ -25,129 +25,10 @@
 
 #include <cstdint>
 
-#include "crc32c.hpp"
-#include "crc32c_device.hpp"
-#include "crc32c_tables.hpp"
 #include "ec_kernels.hpp"
-#include "gf256.hpp"
+#include "gf_device.hpp"
 
 namespace hec {
-
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-
-__constant__ GfTables kDevGf = GfTables();
-
-// PermTable (ec_kernels.hpp): 8 dwords (32 B) per coefficient so that a
-// ds_read_b128 + ds_read_b32 pair fetches it (broadcast: all lanes read the
-// same address, so no bank conflicts).
-
-__device__ __forceinline__ uint8_t lds_gf_mul(const uint8_t* s_exp, const uint8_t* s_log, uint8_t a,
-                                              uint8_t b) {
-    return (a == 0 || b == 0) ? 0 : s_exp[s_log[a] + s_log[b]];
-}
-
-__device__ __forceinline__ uint32_t pack4(uint8_t a, uint8_t b, uint8_t c, uint8_t d) {
-    return uint32_t(a) | (uint32_t(b) << 8) | (uint32_t(c) << 16) | (uint32_t(d) << 24);
-}
-
-// Builds the v_perm_b32 product tables for coefficient c using the LDS
-// log/antilog tables.
-__device__ void build_perm_table(PermTable* t, uint8_t c, const uint8_t* s_exp, const uint8_t* s_log) {
-    uint8_t p0[8], p1[8], p2[4];
-#pragma unroll
-    for (int e = 0; e < 8; e++) {
-        p0[e] = lds_gf_mul(s_exp, s_log, c, uint8_t(e));
-        p1[e] = lds_gf_mul(s_exp, s_log, c, uint8_t(e << 3));
-    }
-#pragma unroll
-    for (int e = 0; e < 4; e++) p2[e] = lds_gf_mul(s_exp, s_log, c, uint8_t(e << 6));
-    t->t0lo = pack4(p0[0], p0[1], p0[2], p0[3]);
-    t->t0hi = pack4(p0[4], p0[5], p0[6], p0[7]);
-    t->t1lo = pack4(p1[0], p1[1], p1[2], p1[3]);
-    t->t1hi = pack4(p1[4], p1[5], p1[6], p1[7]);
-    t->t2 = pack4(p2[0], p2[1], p2[2], p2[3]);
-    t->pad0 = t->pad1 = t->pad2 = 0;
-}
-
-// c * x for the four bytes of x.  v_perm_b32(S0=hi, S1=lo, sel): selector
-// byte 0..3 picks a byte of lo, 4..7 a byte of hi.
-__device__ __forceinline__ uint32_t gf_mul4(uint32_t t0lo, uint32_t t0hi, uint32_t t1lo, uint32_t t1hi,
-                                            uint32_t t2, uint32_t s0, uint32_t s1, uint32_t s2) {
-    uint32_t a = __builtin_amdgcn_perm(t0hi, t0lo, s0);
-    uint32_t b = __builtin_amdgcn_perm(t1hi, t1lo, s1);
-    uint32_t c = __builtin_amdgcn_perm(t2, t2, s2);
-    return a ^ b ^ c;
-}
-
-struct Sel {
-    uint32_t s0, s1, s2;
-};
-
-// Tile order: stripes are taken G at a time and, inside a group, tiles go
-// column-major (tile-column c of all G stripes, then c+1), so the blocks in
-// flight together touch G stripes x (grid/G) columns.  G = 1 is plain
-// stripe-major order.
-__device__ __forceinline__ void tile_coords(uint32_t tile, const MatmulArgs& a, uint32_t& stripe, uint32_t& tcol) {
-    const uint32_t tps = a.tiles_per_stripe;
-    const uint32_t G = a.group;
-    if (G <= 1) {
-        stripe = tile / tps;
-        tcol = tile - stripe * tps;
-        return;
-    }
-    const uint32_t per_group = G * tps;
-    const uint32_t g = tile / per_group;
-    const uint32_t r = tile - g * per_group;
-    const uint32_t first = g * G;
-    const uint32_t rem = uint32_t(a.stripes) - first;
-    const uint32_t gs = rem < G ? rem : G;  // last group may be short
-    tcol = r / gs;
-    stripe = first + (r - tcol * gs);
-}
-
-__device__ __forceinline__ Sel make_sel(uint32_t x) {
-    Sel s;
-    s.s0 = x & 0x07070707u;
-    s.s1 = (x >> 3) & 0x07070707u;
-    s.s2 = (x >> 6) & 0x03030303u;
-    return s;
-}
-
-template <bool NT>
-__device__ __forceinline__ u32x4 load16(const uint8_t* p) {
-    if constexpr (NT)
-        return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
-    else
-        return *reinterpret_cast<const u32x4*>(p);
-}
-
-template <bool NT>
-__device__ __forceinline__ void store16(uint8_t* p, u32x4 v) {
-    if constexpr (NT)
-        __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
-    else
-        *reinterpret_cast<u32x4*>(p) = v;
-}
-
-// Stage log/antilog + coefficient rows in LDS, build the perm tables.
-template <int R, int BS>
-__device__ __forceinline__ void prologue(const MatmulArgs& a, int k, PermTable (*s_tab)[kMaxK], uint8_t* s_exp,
-                                         uint8_t* s_log, uint8_t* s_coef) {
-    static_assert(BS >= 256 && BS % 256 == 0, "prologue assumes >= 256 threads");
-    const int tid = threadIdx.x;
-    if (tid < 256) {
-        s_exp[tid] = kDevGf.exp[tid];
-        s_exp[tid + 256] = kDevGf.exp[tid + 256];
-        s_log[tid] = kDevGf.log[tid];
-    }
-    if (tid < R * kMaxK) s_coef[tid] = a.coef[tid];
-    __syncthreads();
-    for (int t = tid; t < R * k; t += BS) {
-        int j = t / k, i = t - j * k;
-        build_perm_table(&s_tab[j][i], s_coef[j * kMaxK + i], s_exp, s_log);
-    }
-    __syncthreads();
-}
 
 // ---------------------------------------------------------------------------
 // Vector kernel: 16 B per lane per shard, U column chunks per lane.
@@ -568,197 +449,6 @@ __global__ __launch_bounds__(BS) void gf_decode_mixed(MixedArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Fused encode + CRC32C per 512-B chunk of every input and output cell
-// (the write path checksums all k+m cells right after the
-// encode; fusing saves a second HBM pass over them).  Register GF math as in
-// gf_matmul_v16 (MAP 0, U chunks), then each wave drops its (K+R) x U
-// 1-KiB pieces -- each exactly two chunk-aligned 512-B chunks -- into a
-// wave-private LDS image of 144-B quarter rows and runs the quarter-chunk
-// CRC of crc32c.hip over it in rounds of 64 quarters.
-// ---------------------------------------------------------------------------
-namespace {
-__constant__ crc::Tables kFusedCrcTables = crc::Tables();
-}  // namespace
-
-// Layout: a wave owns SLABS KiB (SLABS slabs of 1 KiB, one 16-B load per
-// lane per slab) of every cell of its stripe; one CRC round is 64 quarters
-// = 8 pieces = 8/SLABS shards' share, over a 9-KiB image (as in crc32c.hip).
-// Inputs stream shard by shard (the next one prefetched into registers when
-// the budget allows) while being accumulated into the r parity registers
-// and staged for the round; then each parity shard is stored and staged.
-// SLABS = 8 (one shard per round) when the r x 8 accumulators fit 2 waves
-// per SIMD, else 4 (two shards per round; an odd k + r leaves one
-// half-empty round).  9 KiB of image per wave -> 8 waves per CU.
-template <int K, int R, int SLABS, int SCHEME>
-__global__ __launch_bounds__(SCHEME == 1 ? 256 : 512) __attribute__((amdgpu_waves_per_eu(2, 2))) void gf_encode_crc(
-    MatmulArgs a, uint8_t* sums) {
-    using TL = crcdev::TableLayout<SCHEME>;
-    constexpr int BS = SCHEME == 1 ? 256 : 512, WAVES = BS / 64;
-    constexpr int PITCH = 144, STAGE = 64 * PITCH, SPR = 8 / SLABS;
-    constexpr uint32_t WAVE_BYTES = SLABS * 1024u, TILE_BYTES = WAVES * WAVE_BYTES;
-    constexpr bool PF = R * SLABS <= 24;  // register prefetch of the next shard
-    __shared__ PermTable s_tab[R][kMaxK];
-    __shared__ uint8_t s_exp[512];
-    __shared__ uint8_t s_log[256];
-    __shared__ uint8_t s_coef[R * kMaxK];
-    __shared__ uint32_t s_ctabs[TL::kWords];
-    __shared__ __attribute__((aligned(16))) uint8_t s_stage[WAVES * STAGE];
-    prologue<R, BS>(a, K, s_tab, s_exp, s_log, s_coef);
-    if constexpr (SCHEME == 1) {
-        for (int t = threadIdx.x; t < 8 * 256; t += BS) s_ctabs[t] = (&kFusedCrcTables.slice[0][0])[t];
-    } else {
-        for (int t = threadIdx.x; t < 256 * 32; t += BS) s_ctabs[t] = kFusedCrcTables.slice[0][t / 32];
-        for (int t = threadIdx.x; t < 7 * 4 * 256; t += BS) s_ctabs[TL::kSegOff + t] = (&kFusedCrcTables.seg[0][0][0])[t];
-    }
-    for (int t = threadIdx.x; t < 3 * 4 * 256; t += BS) s_ctabs[TL::kShiftOff + t] = (&kFusedCrcTables.shift[0][0][0])[t];
-    __syncthreads();
-    const uint32_t kfinal = kFusedCrcTables.final512;
-    const uint32_t(*s_shift)[4][256] = reinterpret_cast<const uint32_t(*)[4][256]>(s_ctabs + TL::kShiftOff);
-    const uint32_t(*s_seg)[4][256] = reinterpret_cast<const uint32_t(*)[4][256]>(s_ctabs + TL::kSegOff);
-
-    const uint64_t cell_len = a.cell_len;
-    const uint64_t nck = (cell_len + 511) / 512;  // CRC chunks per cell
-    const uint32_t total = a.total_tiles;
-    const int wave = threadIdx.x / 64, lane = threadIdx.x & 63;
-    // this lane's quarter in a round: row `lane` = piece lane/8 = (shard
-    // slot sir, slab), chunk half (lane/4)&1 of that slab, quarter qi
-    const int qi = lane & 3, piece = lane >> 3, sir = piece / SLABS, pslab = piece % SLABS, half = (lane >> 2) & 1;
-    uint8_t* stage = s_stage + wave * STAGE;
-    uint32_t* out_sums = reinterpret_cast<uint32_t*>(sums);
-
-    for (uint32_t tile = blockIdx.x; tile < total; tile += gridDim.x) {
-        uint32_t stripe, tcol;
-        tile_coords(tile, a, stripe, tcol);
-        const uint64_t wbyte = uint64_t(tcol) * TILE_BYTES + uint64_t(wave) * WAVE_BYTES;  // wave's first byte
-        if (wbyte >= cell_len) continue;  // wave-uniform
-        // 32-bit lane offsets from a wave-uniform per-shard base (saddr +
-        // voffset addressing); dead slabs of a short last tile read slab 0
-        const uint64_t left = cell_len - wbyte;
-        uint32_t voff[SLABS];
-        bool live[SLABS];
-#pragma unroll
-        for (int u = 0; u < SLABS; u++) {
-            const uint32_t o = uint32_t(u) * 1024u + uint32_t(lane) * 16u;
-            live[u] = o < left;
-            voff[u] = live[u] ? o : 0u;
-        }
-        const uint64_t cbyte = wbyte + uint64_t(pslab) * 1024u + uint64_t(half) * 512u;
-        const bool in_cell = cbyte < cell_len;
-        const bool full = in_cell && cell_len - cbyte >= 512u;  // same for a chunk's 4 lanes
-
-        auto crc_round = [&](int first, int count) {
-            __builtin_amdgcn_wave_barrier();
-            asm volatile("" ::: "memory");
-            const bool live_c = in_cell && sir < count;
-            uint32_t val = 0;
-            if (full && sir < count) {
-                uint32_t r;
-                if constexpr (SCHEME == 1)
-                    r = crcdev::quarter_s8(reinterpret_cast<const uint32_t(*)[256]>(s_ctabs), stage + lane * PITCH);
-                else
-                    r = crcdev::quarter_rep<SCHEME>(reinterpret_cast<const uint32_t(*)[32]>(s_ctabs), s_seg,
-                                                    stage + lane * PITCH, lane & 31);
-                if (qi < 3) r = crcdev::apply_shift(s_shift[qi], r);
-                val = r;
-            } else if (live_c && qi == 0) {
-                // short last chunk of the cell: this lane walks it whole, bytewise
-                const uint32_t len = uint32_t(cell_len - cbyte);
-                uint32_t r = 0xFFFFFFFFu;
-                for (uint32_t b = 0; b < len; b++) {
-                    const uint32_t idx = (r ^ stage[(lane + b / 128) * PITCH + (b % 128)]) & 0xFF;
-                    r = (SCHEME == 1 ? s_ctabs[idx] : s_ctabs[idx * 32]) ^ (r >> 8);
-                }
-                val = ~r;
-            }
-            val ^= __shfl_xor(val, 1);
-            val ^= __shfl_xor(val, 2);
-            if (live_c && qi == 0)
-                out_sums[(uint64_t(stripe) * (K + R) + first + sir) * nck + cbyte / 512] =
-                    __builtin_bswap32(full ? (val ^ kfinal) : val);
-            __builtin_amdgcn_wave_barrier();
-            asm volatile("" ::: "memory");
-        };
-        // slab u of the shard in round slot `slot`: lane l's 16 B -> row
-        // 8*(slot*SLABS + u) + l/8, byte 16*(l%8)
-        auto stage_piece = [&](int slot, int u, const u32x4& v) {
-            *reinterpret_cast<u32x4*>(stage + (8 * (slot * SLABS + u) + lane / 8) * PITCH + 16 * (lane % 8)) = v;
-        };
-        auto after_stage = [&](int shard) {
-            if (shard % SPR == SPR - 1 || shard == K + R - 1) crc_round(shard - shard % SPR, shard % SPR + 1);
-        };
-
-        u32x4 acc[SLABS][R];
-#pragma unroll
-        for (int u = 0; u < SLABS; u++)
-#pragma unroll
-            for (int j = 0; j < R; j++) acc[u][j] = u32x4{0, 0, 0, 0};
-        u32x4 x[SLABS], xn[SLABS];
-#pragma unroll
-        for (int u = 0; u < SLABS; u++) x[u] = load16<true>(a.in[0] + (uint64_t(stripe) * a.in_stride[0] + wbyte) + voff[u]);
-#pragma unroll
-        for (int i = 0; i < K; i++) {
-            if (PF && i + 1 < K) {
-#pragma unroll
-                for (int u = 0; u < SLABS; u++)
-                    xn[u] = load16<true>(a.in[i + 1] + (uint64_t(stripe) * a.in_stride[i + 1] + wbyte) + voff[u]);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int u = 0; u < SLABS; u++) stage_piece(i % SPR, u, x[u]);
-            // opaque per-input table offset threaded through the
-            // accumulators: keeps the table reads (and the GF math) of input
-            // i from being hoisted next to those of the other inputs
-            uint32_t toff = uint32_t(i) * uint32_t(sizeof(PermTable));
-            asm volatile("" : "+v"(toff));
-#pragma unroll
-            for (int u = 0; u < SLABS; u++) {
-                asm volatile("" : "+v"(x[u]));
-#pragma unroll
-                for (int j = 0; j < R; j++) asm volatile("" : "+v"(acc[u][j]) : "v"(toff));
-            }
-            uint32_t tb[R][5];
-#pragma unroll
-            for (int j = 0; j < R; j++) {
-                const PermTable& t =
-                    *reinterpret_cast<const PermTable*>(reinterpret_cast<const char*>(&s_tab[j][0]) + toff);
-                tb[j][0] = t.t0lo;
-                tb[j][1] = t.t0hi;
-                tb[j][2] = t.t1lo;
-                tb[j][3] = t.t1hi;
-                tb[j][4] = t.t2;
-            }
-#pragma unroll
-            for (int u = 0; u < SLABS; u++)
-#pragma unroll
-                for (int d = 0; d < 4; d++) {
-                    const Sel sl = make_sel(x[u][d]);
-#pragma unroll
-                    for (int j = 0; j < R; j++)
-                        acc[u][j][d] ^= gf_mul4(tb[j][0], tb[j][1], tb[j][2], tb[j][3], tb[j][4], sl.s0, sl.s1, sl.s2);
-                }
-            __builtin_amdgcn_sched_barrier(0);
-            after_stage(i);
-            __builtin_amdgcn_sched_barrier(0);
-            if (i + 1 < K) {
-#pragma unroll
-                for (int u = 0; u < SLABS; u++)
-                    x[u] = PF ? xn[u]
-                              : load16<true>(a.in[i + 1] + (uint64_t(stripe) * a.in_stride[i + 1] + wbyte) + voff[u]);
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < R; j++) {
-#pragma unroll
-            for (int u = 0; u < SLABS; u++) {
-                if (live[u]) store16<true>(a.out[j] + (uint64_t(stripe) * a.out_stride[j] + wbyte) + voff[u], acc[u][j]);
-                stage_piece((K + j) % SPR, u, acc[u][j]);
-            }
-            after_stage(K + j);
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
 // Byte kernel: tails and unaligned layouts.  One thread per (stripe, byte) in
 // [a.byte_begin, a.cell_len); LDS log/antilog lookups.
 // ---------------------------------------------------------------------------
@@ -1047,67 +737,6 @@ int launch_decode_mixed(const MixedArgs& in, int rows, int device, hipStream_t s
     if (grid > total) grid = total;
     void* args[] = {&a};
     const hipError_t e = hipLaunchKernel(fn, dim3(uint32_t(grid)), dim3(BS), args, res ? a.blob_bytes : 0, stream);
-    return e == hipSuccess ? 0 : int(e);
-}
-
-namespace {
-// 8 slabs per wave while the r x 8 accumulators fit (k <= 6, r <= 3), else 4
-constexpr int fused_slabs(int k, int r) { return (r <= 3 && k <= 6) ? 8 : 4; }
-
-template <int K, int R>
-const void* fused_fn(int slabs, int scheme) {
-    if (scheme == 1)
-        return slabs == 4 ? reinterpret_cast<const void*>(&gf_encode_crc<K, R, 4, 1>)
-                          : reinterpret_cast<const void*>(&gf_encode_crc<K, R, 8, 1>);
-    return slabs == 4 ? reinterpret_cast<const void*>(&gf_encode_crc<K, R, 4, 4>)
-                      : reinterpret_cast<const void*>(&gf_encode_crc<K, R, 8, 4>);
-}
-
-template <int K>
-const void* fused_pick_r(int r, int slabs, int scheme) {
-    switch (r) {
-        case 1: return fused_fn<K, 1>(slabs, scheme);
-        case 2: return fused_fn<K, 2>(slabs, scheme);
-        case 3: return fused_fn<K, 3>(slabs, scheme);
-        default: return fused_fn<K, 4>(slabs, scheme);
-    }
-}
-}  // namespace
-
-int launch_encode_crc(const MatmulArgs& in, uint8_t* sums, int device, hipStream_t stream) {
-    MatmulArgs a = in;
-    bool aligned = a.cell_len % 16 == 0 && (reinterpret_cast<uintptr_t>(sums) & 3u) == 0 && a.r <= kMaxR;
-    for (int i = 0; i < a.k; i++)
-        aligned &= ((reinterpret_cast<uintptr_t>(a.in[i]) | a.in_stride[i]) & 15u) == 0;
-    for (int j = 0; j < a.r; j++)
-        aligned &= ((reinterpret_cast<uintptr_t>(a.out[j]) | a.out_stride[j]) & 15u) == 0;
-    const int slabs = (g_tune_fused_slabs == 4 || g_tune_fused_slabs == 8) ? g_tune_fused_slabs : fused_slabs(a.k, a.r);
-    const int scheme = g_tune_crc_variant == 1 ? 1 : 4;  // CRC lookups (crc32c_device.hpp)
-    const int waves = scheme == 1 ? 4 : 8;
-    const void* fn = nullptr;
-    switch (a.k) {
-        case 2: fn = fused_pick_r<2>(a.r, slabs, scheme); break;
-        case 3: fn = fused_pick_r<3>(a.r, slabs, scheme); break;
-        case 6: fn = fused_pick_r<6>(a.r, slabs, scheme); break;
-        case 10: fn = fused_pick_r<10>(a.r, slabs, scheme); break;
-        default: return -1;
-    }
-    if (!aligned) return -1;
-    const uint64_t chunks = a.cell_len / 16;
-    const uint64_t tile_bytes = 1024u * uint64_t(slabs) * uint64_t(waves);  // 4 waves x slabs x 1 KiB
-    const uint64_t tps = (a.cell_len + tile_bytes - 1) / tile_bytes;
-    const uint64_t total = tps * a.stripes;
-    if (chunks > 0xFFFFFFFFull || total > 0xFFFFFFFFull) return -1;
-    if (total == 0) return 0;
-    a.chunks = uint32_t(chunks);
-    a.tiles_per_stripe = uint32_t(tps);
-    a.total_tiles = uint32_t(total);
-    a.group = g_tune_group > 0 ? uint32_t(g_tune_group) : 4u;
-    // LDS: ~61 KiB per 256-thread block (two per CU) / ~131 KiB per 512-thread block (one)
-    uint64_t grid = uint64_t(num_cus(device)) * (scheme == 1 ? 2 : 1);
-    if (grid > total) grid = total;
-    void* args[] = {&a, &sums};
-    const hipError_t e = hipLaunchKernel(fn, dim3(uint32_t(grid)), dim3(uint32_t(waves * 64)), args, 0, stream);
     return e == hipSuccess ? 0 : int(e);
 }
 

@@ -28,6 +28,12 @@ HEC_ERR_UNSUPPORTED_CODEC = -3
 HEC_ERR_DEVICE = -4
 HEC_ERR_NO_MEMORY = -5
 HEC_ERR_SINGULAR = -6
+HEC_ERR_CHECKSUM = -7
+
+# ChecksumTypeProto values (rust/src/proto/hadoop.hdfs.rs:1363)
+CHECKSUM_NULL = 0
+CHECKSUM_CRC32 = 1   # crc CRC_32_CKSUM (connection.rs:37)
+CHECKSUM_CRC32C = 2  # crc CRC_32_ISCSI (connection.rs:38)
 
 # Every symbol include/hdfs_ec_amd.h declares (checked by tests/test_capi.py).
 EXPORTS = [
@@ -37,7 +43,8 @@ EXPORTS = [
     "hec_encode_device", "hec_decode_device", "hec_gf_matmul_device",
     "hec_encode_host_batch", "hec_tune_set", "hec_decode_mixed_workspace_size",
     "hec_decode_device_mixed", "hec_coder_create_codec", "hec_decode_host_batch",
-    "hec_crc32c_device", "hec_encode_crc_device",
+    "hec_crc32c_device", "hec_encode_crc_device", "hec_checksum_device", "hec_checksum_verify_device",
+    "hec_decode_verify_device",
 ]
 
 
@@ -51,6 +58,11 @@ class ErasureCodingError(HdfsError):
 
 class UnsupportedErasureCodingPolicy(HdfsError):
     """HdfsError::UnsupportedErasureCodingPolicy (error.rs:32-33)."""
+
+
+class ChecksumError(HdfsError):
+    """HdfsError::ChecksumError (error.rs; raised by ReadPacket::get_data,
+    connection.rs:497-499)."""
 
 
 class DeviceError(HdfsError):
@@ -105,6 +117,9 @@ def _load() -> ctypes.CDLL:
         "hec_decode_host_batch": ([P, PP, S, S, P, S], I),
         "hec_crc32c_device": ([P, PP, SP, S, S, S, S, P, P], I),
         "hec_encode_crc_device": ([P, PP, SP, PP, SP, S, S, S, P, P], I),
+        "hec_checksum_device": ([P, I, PP, SP, S, S, S, S, P, P], I),
+        "hec_checksum_verify_device": ([P, I, PP, SP, S, S, S, S, P, P, P], I),
+        "hec_decode_verify_device": ([P, I, PP, SP, PP, SP, S, S, S, P, P, P], I),
         "hec_tune_set": ([I, I], I),
         "hec_decode_mixed_workspace_size": ([P, S], S),
         "hec_decode_device_mixed": ([P, PP, SP, PP, SP, ctypes.POINTER(ctypes.c_uint64), S, S, P, S, P], I),
@@ -131,6 +146,8 @@ def _check(rc: int) -> None:
         raise ErasureCodingError("Not enough valid shards")
     if rc == HEC_ERR_UNSUPPORTED_CODEC:
         raise UnsupportedErasureCodingPolicy(msg)
+    if rc == HEC_ERR_CHECKSUM:
+        raise ChecksumError(msg)
     if rc in (HEC_ERR_INVALID_ARG, HEC_ERR_SINGULAR):
         raise ValueError(msg)
     if rc == HEC_ERR_NO_MEMORY:
@@ -265,6 +282,27 @@ class Coder:
         _check(lib.hec_crc32c_device(self._h, _pp(ptrs), _sp(strides), len(ptrs), cell_len, stripes,
                                      bytes_per_checksum, ctypes.c_void_p(out_ptr), ctypes.c_void_p(stream)))
 
+    def checksum_device(self, checksum_type: int, ptrs, strides, cell_len, stripes, bytes_per_checksum, out_ptr,
+                        stream: int = 0):
+        _check(lib.hec_checksum_device(self._h, checksum_type, _pp(ptrs), _sp(strides), len(ptrs), cell_len, stripes,
+                                       bytes_per_checksum, ctypes.c_void_p(out_ptr), ctypes.c_void_p(stream)))
+
+    def checksum_verify_device(self, checksum_type: int, ptrs, strides, cell_len, stripes, bytes_per_checksum,
+                               expected_ptr, bad_ptr, stream: int = 0):
+        _check(lib.hec_checksum_verify_device(self._h, checksum_type, _pp(ptrs), _sp(strides), len(ptrs), cell_len,
+                                              stripes, bytes_per_checksum, ctypes.c_void_p(expected_ptr),
+                                              ctypes.c_void_p(bad_ptr), ctypes.c_void_p(stream)))
+
+    def decode_verify_device(self, checksum_type: int, shard_ptrs, shard_strides, out_ptrs, out_strides, cell_len,
+                             stripes, bytes_per_checksum, sums_ptr, bad_ptr, stream: int = 0) -> None:
+        """Verified striped read (hec_decode_verify_device): raises
+        ErasureCodingError when a stripe has fewer than k cells that verify
+        (the bad flags are written either way)."""
+        _check(lib.hec_decode_verify_device(self._h, checksum_type, _pp(shard_ptrs), _sp(shard_strides),
+                                            _pp(out_ptrs), _sp(out_strides), cell_len, stripes, bytes_per_checksum,
+                                            ctypes.c_void_p(sums_ptr), ctypes.c_void_p(bad_ptr),
+                                            ctypes.c_void_p(stream)))
+
     def encode_crc_device(self, data_ptrs, data_strides, parity_ptrs, parity_strides, cell_len, stripes,
                           bytes_per_checksum, sums_ptr, stream: int = 0):
         _check(lib.hec_encode_crc_device(self._h, _pp(data_ptrs), _sp(data_strides), _pp(parity_ptrs),
@@ -331,6 +369,57 @@ def crc32c_batch(coder: Coder, cells, bytes_per_checksum: int = 512, stream=None
     ptrs, strides = stripe_layout_ptrs(cells, n)
     coder.crc32c_device(ptrs, strides, cell, S, bytes_per_checksum, out.data_ptr(), s.cuda_stream)
     return out
+
+
+def checksum_batch(coder: Coder, cells, checksum_type: int = CHECKSUM_CRC32C, bytes_per_checksum: int = 512,
+                   stream=None):
+    """cells: uint8 cuda tensor [S, n, cell] -> uint8 tensor [S, n, nchunks, 4]
+    of big-endian chunk checksums (CRC32C or CRC32 = CRC_32_CKSUM)."""
+    import torch
+    S, n, cell = cells.shape
+    s = stream if stream is not None else torch.cuda.current_stream(cells.device)
+    nchunks = (cell + bytes_per_checksum - 1) // bytes_per_checksum
+    out = torch.empty((S, n, nchunks, 4), dtype=torch.uint8, device=cells.device)
+    ptrs, strides = stripe_layout_ptrs(cells, n)
+    coder.checksum_device(checksum_type, ptrs, strides, cell, S, bytes_per_checksum, out.data_ptr(), s.cuda_stream)
+    return out
+
+
+def checksum_verify_batch(coder: Coder, cells, expected, checksum_type: int = CHECKSUM_CRC32C,
+                          bytes_per_checksum: int = 512, stream=None):
+    """ReadPacket::get_data's check: -> uint8 tensor [S, n], 1 where a cell
+    has a chunk whose checksum differs from `expected` [S, n, nchunks, 4]."""
+    import torch
+    S, n, cell = cells.shape
+    s = stream if stream is not None else torch.cuda.current_stream(cells.device)
+    bad = torch.zeros((S, n), dtype=torch.uint8, device=cells.device)
+    ptrs, strides = stripe_layout_ptrs(cells, n)
+    coder.checksum_verify_device(checksum_type, ptrs, strides, cell, S, bytes_per_checksum,
+                                 expected.data_ptr(), bad.data_ptr(), s.cuda_stream)
+    return bad
+
+
+def decode_verify_batch(coder: Coder, data, parity, missing: Sequence[int], sums, out,
+                        checksum_type: int = CHECKSUM_CRC32C, bytes_per_checksum: int = 512, stream=None,
+                        missing_parity: Sequence[int] = ()):
+    """Verified striped read over data [S,k,cell] / parity [S,m,cell] with
+    data shards `missing` (and parity shards `missing_parity`) unavailable
+    for the batch; sums [S, k+m, nchunks, 4] are the packets' checksums.
+    Rebuilt data lands in out [S,k,cell]; returns the bad-cell flags
+    [S, k+m] (uint8 cuda tensor)."""
+    import torch
+    k, m = coder.data_units, coder.parity_units
+    S = data.shape[0]
+    s = stream if stream is not None else torch.cuda.current_stream(data.device)
+    dp, ds = stripe_layout_ptrs(data, k)
+    pp, ps = stripe_layout_ptrs(parity, m)
+    op, os_ = stripe_layout_ptrs(out, k)
+    miss, pmiss = set(missing), set(missing_parity)
+    ptrs = [None if i in miss else dp[i] for i in range(k)] + [None if j in pmiss else pp[j] for j in range(m)]
+    bad = torch.empty((S, k + m), dtype=torch.uint8, device=data.device)
+    coder.decode_verify_device(checksum_type, ptrs, ds + ps, op, os_, data.shape[2], S, bytes_per_checksum,
+                               sums.data_ptr(), bad.data_ptr(), s.cuda_stream)
+    return bad
 
 
 def decode_batch_mixed(coder: Coder, data, parity, present_masks: Sequence[int], out, stream=None,

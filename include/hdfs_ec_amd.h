@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define HEC_ABI_VERSION 1
+#define HEC_ABI_VERSION 2
 
 /* Status codes */
 #define HEC_OK 0
@@ -45,6 +45,13 @@ extern "C" {
 #define HEC_ERR_DEVICE (-4)            /* HIP runtime / launch failure */
 #define HEC_ERR_NO_MEMORY (-5)         /* host or device allocation failed */
 #define HEC_ERR_SINGULAR (-6)          /* reference panics "Matrix is singular" matrix.rs:121-123 */
+#define HEC_ERR_CHECKSUM (-7)          /* HdfsError::ChecksumError connection.rs:497-499 */
+
+/* Chunk checksum types: ChecksumTypeProto values (rust/src/proto/hadoop.hdfs.rs:1363),
+ * mapped to algorithms by ReadPacket::get_data (rust/src/hdfs/connection.rs:483-487). */
+#define HEC_CHECKSUM_NULL 0   /* CHECKSUM_NULL: no verification */
+#define HEC_CHECKSUM_CRC32 1  /* crc 3.4 CRC_32_CKSUM (connection.rs:37): MSB-first 0x04C11DB7, init 0, xorout ~0 */
+#define HEC_CHECKSUM_CRC32C 2 /* crc 3.4 CRC_32_ISCSI (connection.rs:38): Castagnoli, reflected, init/xorout ~0 */
 
 /* Limits of this engine (the reference has k+m <= 256 through `r as u8`). */
 #define HEC_MAX_DATA_UNITS 32
@@ -163,7 +170,7 @@ int hec_gf_matmul_device(hec_coder_t *coder, const uint8_t *matrix, size_t rows,
                          const uint8_t *const *d_in, const size_t *in_strides, uint8_t *const *d_out,
                          const size_t *out_strides, size_t cell_len, size_t stripes, void *hip_stream);
 
-/* ---- CRC32C per checksum chunk ---------------------- *
+/* ---- Chunk checksums -------------------------------- *
  * WritePacket::calculate_checksum (rust/src/hdfs/connection.rs:568-584) on
  * the device: for each of `n_shards` cells of `stripes` stripes (shard i of
  * stripe s at d_bases[i] + s*strides[i], cell_len bytes), one CRC32C
@@ -175,6 +182,48 @@ int hec_gf_matmul_device(hec_coder_t *coder, const uint8_t *matrix, size_t rows,
 int hec_crc32c_device(hec_coder_t *coder, const uint8_t *const *d_bases, const size_t *strides, size_t n_shards,
                       size_t cell_len, size_t stripes, size_t bytes_per_checksum, uint8_t *d_out,
                       void *hip_stream);
+
+/* The same for either algorithm the read path accepts: `checksum_type` is
+ * HEC_CHECKSUM_CRC32C or HEC_CHECKSUM_CRC32 (HEC_CHECKSUM_NULL is invalid
+ * here: there is nothing to compute). */
+int hec_checksum_device(hec_coder_t *coder, int checksum_type, const uint8_t *const *d_bases, const size_t *strides,
+                        size_t n_shards, size_t cell_len, size_t stripes, size_t bytes_per_checksum,
+                        uint8_t *d_out, void *hip_stream);
+
+/* ReadPacket::get_data's check (connection.rs:477-504) over whole cells:
+ * recomputes every chunk checksum and compares it with d_expected (same
+ * layout as hec_checksum_device's output, big-endian as received).
+ * d_bad[s*n_shards + i] is set to 1 when any chunk of cell (s, i)
+ * mismatches (the reference's HdfsError::ChecksumError for that packet) and
+ * is otherwise left untouched: zero it first.  HEC_CHECKSUM_NULL verifies
+ * nothing and returns HEC_OK.  Asynchronous on hip_stream. */
+int hec_checksum_verify_device(hec_coder_t *coder, int checksum_type, const uint8_t *const *d_bases,
+                               const size_t *strides, size_t n_shards, size_t cell_len, size_t stripes,
+                               size_t bytes_per_checksum, const uint8_t *d_expected, uint8_t *d_bad,
+                               void *hip_stream);
+
+/* The striped read of one batch of rows (block_reader.rs:480-525 feeding
+ * EcSchema::ec_decode, ec/mod.rs:62-89) with every cell it consumes
+ * checksum-verified.  d_shards[k+m] as hec_decode_device (NULL = shard not
+ * available for the whole batch).  Per stripe the survivors are the first k
+ * available shards whose chunk checksums verify against d_sums
+ * ([stripe][k+m][nchunks] big-endian, the sums that arrived with the
+ * packets); a shard that fails is skipped and the next available one is
+ * read instead, as read_slice drops a failing cell reader and starts the
+ * next parity reader.  Every data shard that is missing or failed is
+ * rebuilt into d_out[i] (out_strides as hec_decode_device); present data
+ * shards that verify are not copied.  d_bad[s*(k+m) + i] = 1 marks the
+ * cells that failed (zeroed by the call; device memory).  When every stripe
+ * verifies first time this is one fused pass over the survivors (k in
+ * {2,3,6,10}, 512-B chunks, 16-B aligned); failing stripes are re-planned
+ * on the host and redone one by one.  Synchronous (it must see the
+ * verdicts).  Returns HEC_ERR_NOT_ENOUGH_SHARDS when some stripe has fewer
+ * than k shards that verify (its d_bad flags say which; the other stripes
+ * are still rebuilt).  HEC_CHECKSUM_NULL decodes without verifying. */
+int hec_decode_verify_device(hec_coder_t *coder, int checksum_type, const uint8_t *const *d_shards,
+                             const size_t *shard_strides, uint8_t *const *d_out, const size_t *out_strides,
+                             size_t cell_len, size_t stripes, size_t bytes_per_checksum, const uint8_t *d_sums,
+                             uint8_t *d_bad, void *hip_stream);
 
 /* Encode plus CRC32C of the k data and m parity cells (shard order
  * 0..k+m-1, same output layout as hec_crc32c_device): everything a striped

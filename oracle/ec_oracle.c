@@ -295,3 +295,30 @@ void orc_chunk_crc32c(const uint8_t *p, size_t n, size_t bpc, uint8_t *out) {
         out[4 * k + 3] = (uint8_t)c;
     }
 }
+
+/* ---- CRC32 = crc 3.4's CRC_32_CKSUM (connection.rs:37) ---------------- *
+ * The reference's algorithm for ChecksumTypeProto CHECKSUM_CRC32 on read
+ * (ReadPacket::get_data, connection.rs:483-487): crc-catalog 2.4.0
+ * parameters width 32, poly 0x04C11DB7, init 0, refin/refout false,
+ * xorout 0xFFFFFFFF (check 0x765E7680).  Bitwise, MSB first. */
+uint32_t orc_crc32_cksum(const uint8_t *p, size_t n) {
+    uint32_t crc = 0;
+    for (size_t i = 0; i < n; i++) {
+        crc ^= (uint32_t)p[i] << 24;
+        for (int b = 0; b < 8; b++) crc = (crc << 1) ^ (0x04C11DB7u & (0u - (crc >> 31)));
+    }
+    return crc ^ 0xFFFFFFFFu;
+}
+
+/* checksum_type: 1 = CRC32 (CRC_32_CKSUM), 2 = CRC32C (ChecksumTypeProto). */
+void orc_chunk_checksum(int checksum_type, const uint8_t *p, size_t n, size_t bpc, uint8_t *out) {
+    size_t k = 0;
+    for (size_t start = 0; start < n; start += bpc, k++) {
+        size_t len = n - start < bpc ? n - start : bpc;
+        uint32_t c = checksum_type == 1 ? orc_crc32_cksum(p + start, len) : orc_crc32c(p + start, len);
+        out[4 * k] = (uint8_t)(c >> 24);
+        out[4 * k + 1] = (uint8_t)(c >> 16);
+        out[4 * k + 2] = (uint8_t)(c >> 8);
+        out[4 * k + 3] = (uint8_t)c;
+    }
+}

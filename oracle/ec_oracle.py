@@ -14,6 +14,11 @@ Restates hdfs-native 0.14.1's EC path (read-only reference, Rust):
   rust/src/ec/mod.rs:62-89      EcSchema::ec_decode
   rust/src/ec/mod.rs:93-144     resolve_ec_policy
   rust/src/hdfs/block_writer.rs:817-851  CellBuffer::encode padding semantics
+  rust/src/hdfs/connection.rs:37-38, :477-504, :568-584  chunk checksums
+      (crc 3.4.0 / crc-catalog 2.4.0, Cargo.lock:375-387, not vendored:
+      CRC_32_ISCSI and CRC_32_CKSUM restated from their published parameters)
+  rust/src/hdfs/block_reader.rs:480-525  read_slice: a cell whose packet
+      fails its checksum drops that reader; the next parity reader is read
 
 Pinning: tests/test_oracle.py checks this module and the C oracle against the
 reference's own KATs (gf256.rs:144-202, mod.rs:152-160) and against each other.
@@ -282,6 +287,76 @@ def chunk_crc32c(data: bytes, bytes_per_checksum: int) -> bytes:
     return bytes(out)
 
 
+# CRC_32_CKSUM (crc-catalog: width 32, poly 0x04C11DB7, init 0, refin/refout
+# false, xorout 0xFFFFFFFF, check 0x765E7680): the reference's "CRC32"
+# (connection.rs:37), used for ChecksumTypeProto CHECKSUM_CRC32 on read.
+def _cksum_table():
+    t = []
+    for i in range(256):
+        c = i << 24
+        for _ in range(8):
+            c = ((c << 1) ^ 0x04C11DB7 if c & 0x80000000 else c << 1) & 0xFFFFFFFF
+        t.append(c)
+    return t
+
+
+CKSUM_TABLE = _cksum_table()
+
+
+def crc32_cksum(data: bytes) -> int:
+    """CRC-32/CKSUM: MSB-first 0x04C11DB7, init 0, xorout 0xFFFFFFFF."""
+    crc = 0
+    for b in bytes(data):
+        crc = CKSUM_TABLE[((crc >> 24) ^ b) & 0xFF] ^ ((crc << 8) & 0xFFFFFFFF)
+    return crc ^ 0xFFFFFFFF
+
+
+CHECKSUM_NULL, CHECKSUM_CRC32, CHECKSUM_CRC32C = 0, 1, 2  # ChecksumTypeProto (hadoop.hdfs.rs:1363)
+_ALGO = {CHECKSUM_CRC32: crc32_cksum, CHECKSUM_CRC32C: crc32c}
+
+
+def chunk_checksums(data: bytes, bytes_per_checksum: int, checksum_type: int = CHECKSUM_CRC32C) -> bytes:
+    """One big-endian u32 per bytes_per_checksum chunk (last may be short)."""
+    algo = _ALGO[checksum_type]
+    data = bytes(data)
+    return b"".join(algo(data[s:s + bytes_per_checksum]).to_bytes(4, "big")
+                    for s in range(0, len(data), bytes_per_checksum))
+
+
+def get_data_ok(data: bytes, sums: bytes, bytes_per_checksum: int, checksum_type: int) -> bool:
+    """ReadPacket::get_data (connection.rs:477-504): False = ChecksumError."""
+    if checksum_type == CHECKSUM_NULL:
+        return True
+    return chunk_checksums(data, bytes_per_checksum, checksum_type) == bytes(sums)
+
+
+def verified_read_row(k: int, m: int, cells: List[Optional[bytes]], sums: List[bytes], bytes_per_checksum: int,
+                      checksum_type: int):
+    """One row of the striped read with verification (block_reader.rs:480-525
+    then ec/mod.rs:62-89): cells are read in index order from the available
+    shards (None = no reader); a cell that fails get_data drops its reader
+    and the next shard is read, until k good cells are held.  Returns
+    (data cells [k] as bytes, bad flags [k+m]); raises NotEnoughShards when
+    fewer than k cells verify."""
+    bad = [0] * (k + m)
+    good: List[Optional[np.ndarray]] = [None] * (k + m)
+    held = 0
+    for i in range(k + m):
+        if held == k:
+            break
+        if cells[i] is None:
+            continue
+        if get_data_ok(cells[i], sums[i], bytes_per_checksum, checksum_type):
+            good[i] = np.frombuffer(bytes(cells[i]), dtype=np.uint8)
+            held += 1
+        else:
+            bad[i] = 1
+    if held < k:
+        raise NotEnoughShards("Not enough valid shards")
+    full = decode(k, m, good)
+    return [full[i].tobytes() for i in range(k)], bad
+
+
 # ---- ctypes access to the C oracle ----------------------------------------
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -306,6 +381,9 @@ def load_c_oracle() -> ctypes.CDLL:
     lib.orc_crc32c.argtypes = [P, S]
     lib.orc_crc32c.restype = ctypes.c_uint32
     lib.orc_chunk_crc32c.argtypes = [P, S, S, P]
+    lib.orc_crc32_cksum.argtypes = [P, S]
+    lib.orc_crc32_cksum.restype = ctypes.c_uint32
+    lib.orc_chunk_checksum.argtypes = [ctypes.c_int, P, S, S, P]
     return lib
 
 

@@ -32,8 +32,9 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version_and_strerror():
-    assert H.lib.hec_abi_version() == 1
+    assert H.lib.hec_abi_version() == 2
     assert "Not enough valid shards" in H.strerror(H.HEC_ERR_NOT_ENOUGH_SHARDS)
+    assert H.strerror(H.HEC_ERR_CHECKSUM) == "checksum error"
     assert H.strerror(12345) == "unknown status"
 
 
@@ -86,6 +87,13 @@ def test_null_coder_calls_return_status():
     assert H.lib.hec_encode(None, None, 16, None) == H.HEC_ERR_INVALID_ARG
     assert H.lib.hec_decode(None, None, 16, None) == H.HEC_ERR_INVALID_ARG
     assert H.lib.hec_coder_data_units(None) == 0
+    assert H.lib.hec_checksum_device(None, 2, None, None, 1, 16, 1, 512, None, None) == H.HEC_ERR_INVALID_ARG
+    assert H.lib.hec_checksum_verify_device(None, 2, None, None, 1, 16, 1, 512, None, None,
+                                            None) == H.HEC_ERR_INVALID_ARG
+    assert H.lib.hec_checksum_verify_device(None, 0, None, None, 1, 16, 1, 512, None, None,
+                                            None) == H.HEC_ERR_INVALID_ARG
+    assert H.lib.hec_decode_verify_device(None, 2, None, None, None, None, 16, 1, 512, None, None,
+                                          None) == H.HEC_ERR_INVALID_ARG
     H.lib.hec_coder_destroy(None)
 
 

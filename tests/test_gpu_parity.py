@@ -593,3 +593,188 @@ def test_encode_crc_full_size_properties(dev):
     torch.cuda.synchronize()
     assert torch.equal(p1, p2)
     assert torch.equal(sums, ref)
+
+
+# ---- Chunk checksums on the read path: CRC32 / CRC32C verify and the ----
+# ---- verified striped read (connection.rs:477-504) ----
+
+CKSUM_TYPES = [H.CHECKSUM_CRC32C, H.CHECKSUM_CRC32]
+
+
+def _oracle_checksums(cells: np.ndarray, bpc: int, ctype: int) -> np.ndarray:
+    S, n, cell = cells.shape
+    nch = (cell + bpc - 1) // bpc
+    out = np.zeros((S, n, nch, 4), dtype=np.uint8)
+    for s in range(S):
+        for i in range(n):
+            out[s, i] = np.frombuffer(O.chunk_checksums(cells[s, i].tobytes(), bpc, ctype),
+                                      dtype=np.uint8).reshape(nch, 4)
+    return out
+
+
+@pytest.mark.parametrize("ctype", CKSUM_TYPES)
+@pytest.mark.parametrize("cell,bpc,n", [(512 * 64, 512, 3), (512 * 70 + 256, 512, 2), (1000, 512, 3),
+                                        (4096, 4096, 2), (2048, 100, 2)])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+def test_checksum_device_vs_oracle(dev, ctype, cell, bpc, n, variant):
+    S = 3
+    cells = batch_data(S, n, cell, first=cell + bpc + ctype)
+    H.tune_set(11, variant)
+    try:
+        got = H.checksum_batch(coder(6, 3), torch.from_numpy(cells).to(dev), ctype, bpc)
+        torch.cuda.synchronize()
+    finally:
+        H.tune_set(11, 0)
+    assert np.array_equal(got.cpu().numpy(), _oracle_checksums(cells, bpc, ctype))
+
+
+def test_checksum_device_catalog_checks(dev):
+    cells = torch.from_numpy(np.frombuffer(b"123456789", dtype=np.uint8).reshape(1, 1, 9).copy()).to(dev)
+    for ctype, want in ((H.CHECKSUM_CRC32C, 0xE3069283), (H.CHECKSUM_CRC32, 0x765E7680)):
+        got = H.checksum_batch(coder(6, 3), cells, ctype, 512)
+        torch.cuda.synchronize()
+        assert got.cpu().numpy().ravel().tobytes() == want.to_bytes(4, "big")
+
+
+@pytest.mark.parametrize("ctype", CKSUM_TYPES)
+@pytest.mark.parametrize("cell,bpc", [(1 << 15, 512), (512 * 9 + 48, 512), (3000, 100)])
+def test_checksum_verify_flags_exactly_the_corrupt_cells(dev, ctype, cell, bpc):
+    S, n = 4, 5
+    cells = batch_data(S, n, cell, first=77 + cell)
+    sums = torch.from_numpy(_oracle_checksums(cells, bpc, ctype)).to(dev)
+    bent = cells.copy()
+    hits = {(0, 1): 0, (2, 4): cell - 1, (3, 0): cell // 2}  # first, last (short chunk), middle byte
+    for (s, i), b in hits.items():
+        bent[s, i, b] ^= 0x10
+    bad = H.checksum_verify_batch(coder(6, 3), torch.from_numpy(bent).to(dev), sums, ctype, bpc)
+    torch.cuda.synchronize()
+    want = np.zeros((S, n), dtype=np.uint8)
+    for s, i in hits:
+        want[s, i] = 1
+    assert np.array_equal(bad.cpu().numpy(), want)
+    # CHECKSUM_NULL verifies nothing
+    none = H.checksum_verify_batch(coder(6, 3), torch.from_numpy(bent).to(dev), sums, H.CHECKSUM_NULL, bpc)
+    assert not none.any()
+
+
+def _verified_read_expect(k, m, data, parity, missing, missing_parity, sums_np, bpc, ctype):
+    """Per stripe: oracle verified_read_row -> (data [S,k,cell], bad [S,k+m],
+    ok [S])."""
+    S, _, cell = data.shape
+    outs, bads, oks = np.zeros_like(data), np.zeros((S, k + m), dtype=np.uint8), []
+    for s in range(S):
+        cells = [None if i in missing else data[s, i].tobytes() for i in range(k)]
+        cells += [None if j in missing_parity else parity[s, j].tobytes() for j in range(m)]
+        sums = [sums_np[s, i].tobytes() for i in range(k + m)]
+        try:
+            got, bad = O.verified_read_row(k, m, cells, sums, bpc, ctype)
+            outs[s] = np.stack([np.frombuffer(g, dtype=np.uint8) for g in got])
+            oks.append(True)
+        except O.NotEnoughShards:
+            # flags the oracle saw before giving up: every available cell failed-or-read
+            bad = [0] * (k + m)
+            for i in range(k + m):
+                if cells[i] is not None and not O.get_data_ok(cells[i], sums[i], bpc, ctype):
+                    bad[i] = 1
+            oks.append(False)
+        bads[s] = bad
+    return outs, bads, oks
+
+
+@pytest.mark.parametrize("ctype", CKSUM_TYPES)
+@pytest.mark.parametrize("k,m,cell,bpc,missing,missing_parity", [
+    (6, 3, 1 << 15, 512, [0, 1, 2], []), (6, 3, 512 * 9 + 48, 512, [4], [1]), (6, 3, 1 << 14, 512, [], []),
+    (10, 4, 1 << 14, 512, [0, 1, 2, 3], []), (10, 4, 1 << 13, 512, [7], [0]), (3, 2, 1 << 14, 512, [1], []),
+    (2, 1, 8192, 512, [0], []), (12, 4, 1 << 13, 512, [2, 5], []), (6, 3, 3000, 100, [0, 5], []),
+    (6, 3, 4096 + 16, 4096, [3], [])])
+def test_decode_verify_vs_oracle(dev, c_oracle, ctype, k, m, cell, bpc, missing, missing_parity):
+    """Fused (k in {2,3,6,10}, 512-B chunks) and two-pass decode+verify: clean
+    stripes, corrupt survivors (data and parity), a stripe that runs out of
+    verified shards; rebuilt data, bad flags and the error all as the
+    oracle's read_slice restatement."""
+    S = 6
+    data = batch_data(S, k, cell, first=5 + cell + k)
+    parity = oracle_batch_encode(c_oracle, k, m, data)
+    sums_np = _oracle_checksums(np.concatenate([data, parity], axis=1), bpc, ctype)
+    avail = [i for i in range(k + m) if (i < k and i not in missing) or (i >= k and i - k not in missing_parity)]
+    bd, bp = data.copy(), parity.copy()
+
+    def bend(s, shard, byte):
+        (bd[s, shard] if shard < k else bp[s, shard - k])[byte] ^= 0x5A
+
+    spare = len(avail) - k
+    bend(1, avail[0], 3)                       # first survivor
+    bend(2, avail[k - 1], cell - 1)            # last survivor, last byte
+    bend(3, avail[1], cell // 2)
+    if spare >= 2:
+        bend(3, avail[k], 0)                   # ... and its replacement too
+    for t in range(spare + 1):                 # stripe 5: one failure too many
+        bend(5, avail[t], 100 + t)
+    want_data, want_bad, oks = _verified_read_expect(k, m, bd, bp, set(missing), set(missing_parity), sums_np,
+                                                     bpc, ctype)
+    assert not oks[5] and oks[0] and oks[4]
+    cod = coder(k, m)
+    d, p = torch.from_numpy(bd).to(dev), torch.from_numpy(bp).to(dev)
+    out = torch.zeros_like(d)
+    sums = torch.from_numpy(sums_np).to(dev)
+    bad = torch.full((S, k + m), 7, dtype=torch.uint8, device=dev)
+    dp, ds = H.stripe_layout_ptrs(d, k)
+    pp, ps = H.stripe_layout_ptrs(p, m)
+    op, os_ = H.stripe_layout_ptrs(out, k)
+    ptrs = [None if i in missing else dp[i] for i in range(k)] + \
+        [None if j in missing_parity else pp[j] for j in range(m)]
+    with pytest.raises(H.ErasureCodingError):
+        cod.decode_verify_device(ctype, ptrs, ds + ps, op, os_, cell, S, bpc, sums.data_ptr(), bad.data_ptr(),
+                                 torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    o, b = out.cpu().numpy(), bad.cpu().numpy()
+    for s in range(S):
+        if not oks[s]:
+            continue  # the reference returns no row; flags there are partial by design
+        assert np.array_equal(b[s], want_bad[s]), s
+        for i in range(k):
+            if i in missing or want_bad[s, i]:
+                assert np.array_equal(o[s, i], want_data[s, i]), (s, i)
+            else:
+                assert not o[s, i].any(), (s, i)  # present + verified: not copied
+
+
+@pytest.mark.parametrize("ctype", CKSUM_TYPES)
+def test_decode_verify_null_type_is_plain_decode(dev, c_oracle, ctype):
+    k, m, cell, S = 6, 3, 1 << 14, 3
+    data = batch_data(S, k, cell, first=99)
+    parity = oracle_batch_encode(c_oracle, k, m, data)
+    d, p = torch.from_numpy(data).to(dev), torch.from_numpy(parity).to(dev)
+    out = torch.zeros_like(d)
+    sums = torch.zeros((S, k + m, cell // 512, 4), dtype=torch.uint8, device=dev)  # wrong sums: ignored
+    H.decode_verify_batch(coder(k, m), d, p, [0, 4], sums, out, H.CHECKSUM_NULL, 512)
+    torch.cuda.synchronize()
+    assert torch.equal(out[:, [0, 4]], d[:, [0, 4]])
+
+
+def test_decode_verify_full_size_properties(dev):
+    """RS(6,3) 1 MiB x 64: with shards {0,1,2} missing the fused verified
+    read equals a plain decode with no flags; with {0,1} missing, one flipped
+    byte in survivor 3 of stripe 5 is flagged and routed around (parity 2 is
+    read instead) and that data cell is rebuilt too."""
+    k, m, cell, S = 6, 3, 1 << 20, 64
+    c = coder(k, m)
+    d = torch.empty((S, k, cell), dtype=torch.uint8, device=dev)
+    d.random_(0, 256, generator=torch.Generator(device=dev).manual_seed(11))
+    p = torch.empty((S, m, cell), dtype=torch.uint8, device=dev)
+    H.encode_batch(c, d, p)
+    sums = H.checksum_batch(c, torch.cat([d, p], dim=1), H.CHECKSUM_CRC32C, 512)
+    out = torch.zeros_like(d)
+    bad = H.decode_verify_batch(c, d, p, [0, 1, 2], sums, out)
+    torch.cuda.synchronize()
+    assert not bad.any()
+    assert torch.equal(out[:, :3], d[:, :3])
+    d[5, 3, 12345] ^= 1
+    out.zero_()
+    bad = H.decode_verify_batch(c, d, p, [0, 1], sums, out)
+    torch.cuda.synchronize()
+    assert bad.nonzero().tolist() == [[5, 3]]
+    d[5, 3, 12345] ^= 1
+    assert torch.equal(out[:, :2], d[:, :2])
+    assert torch.equal(out[5, 3], d[5, 3])
+    assert not out[:5, 2:].any() and not out[6:, 2:].any()

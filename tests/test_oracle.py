@@ -218,3 +218,70 @@ def test_chunk_crc32c_c_vs_python(c_oracle):
             out = np.zeros(((n + bpc - 1) // bpc) * 4, dtype=np.uint8)
             c_oracle.orc_chunk_crc32c(data.ctypes.data, n, bpc, out.ctypes.data)
             assert out.tobytes() == O.chunk_crc32c(data.tobytes(), bpc)
+
+
+# ---- CRC32 = CRC_32_CKSUM (connection.rs:37) and the verified read --------
+
+def test_crc32_cksum_catalog_check(c_oracle):
+    """crc-catalog 2.4.0 CRC_32_CKSUM check value."""
+    assert O.crc32_cksum(b"123456789") == 0x765E7680
+    buf = np.frombuffer(b"123456789", dtype=np.uint8).copy()
+    assert c_oracle.orc_crc32_cksum(buf.ctypes.data, 9) == 0x765E7680
+
+
+def test_crc32_cksum_vs_posix_cksum_fixtures():
+    """POSIX cksum (coreutils, tests/golden/make_cksum.py) = CRC_32_CKSUM of
+    the message followed by its length, little-endian, minimal bytes."""
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(__file__), "golden", "cksum_vectors.json")) as f:
+        cases = json.load(f)["cases"]
+    assert len(cases) >= 10
+    for case in cases:
+        data = bytes.fromhex(case["hex"])
+        n, tail = len(data), b""
+        while n:
+            tail += bytes([n & 0xFF])
+            n >>= 8
+        assert O.crc32_cksum(data + tail) == case["posix_cksum"]
+
+
+@pytest.mark.parametrize("ctype", [O.CHECKSUM_CRC32, O.CHECKSUM_CRC32C])
+def test_chunk_checksum_c_vs_python(c_oracle, ctype):
+    for n in (1, 511, 512, 513, 4096, 5000):
+        data = splitmix64_bytes(n + 7, n)
+        for bpc in (512, 4096, 100):
+            out = np.zeros(((n + bpc - 1) // bpc) * 4, dtype=np.uint8)
+            c_oracle.orc_chunk_checksum(ctype, data.ctypes.data, n, bpc, out.ctypes.data)
+            assert out.tobytes() == O.chunk_checksums(data.tobytes(), bpc, ctype)
+
+
+def test_verified_read_row_semantics():
+    """block_reader.rs:480-525: a failing cell is skipped and the next shard
+    read; all data rebuilt; too many failures -> Not enough valid shards."""
+    k, m, n, bpc = 6, 3, 2048, 512
+    data = [splitmix64_bytes(100 + i, n) for i in range(k)]
+    cells = [d.tobytes() for d in data] + [p.tobytes() for p in O.encode(k, m, data)]
+    sums = [O.chunk_checksums(c, bpc, O.CHECKSUM_CRC32C) for c in cells]
+    # clean read: nothing bad
+    out, bad = O.verified_read_row(k, m, list(cells), sums, bpc, O.CHECKSUM_CRC32C)
+    assert out == cells[:k] and bad == [0] * (k + m)
+    # data cell 2 corrupted, data 4 unavailable: parity 0 and 1 are read
+    bent = list(cells)
+    bent[2] = bent[2][:700] + bytes([bent[2][700] ^ 1]) + bent[2][701:]
+    bent[4] = None
+    out, bad = O.verified_read_row(k, m, bent, sums, bpc, O.CHECKSUM_CRC32C)
+    assert out == cells[:k] and bad == [0, 0, 1, 0, 0, 0, 0, 0, 0]
+    # parity never read when not needed: corrupt parity 2 is not flagged
+    bent2 = list(bent)
+    bent2[8] = bytes(n)
+    _, bad = O.verified_read_row(k, m, bent2, sums, bpc, O.CHECKSUM_CRC32C)
+    assert bad[8] == 0
+    # m+1 cells lost or failed -> error
+    bent2[6] = bytes(n)
+    with pytest.raises(O.NotEnoughShards):
+        O.verified_read_row(k, m, bent2, sums, bpc, O.CHECKSUM_CRC32C)
+    # CHECKSUM_NULL verifies nothing: the corrupt cell is used as read
+    out, bad = O.verified_read_row(k, m, bent, sums, bpc, O.CHECKSUM_NULL)
+    assert bad == [0] * (k + m)
+    assert out[2] == bent[2] and out[4] != cells[4]
