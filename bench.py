@@ -375,6 +375,53 @@ def main():
             "crc_only_ms": round(t_c * 1e3, 3),
             "note": "CRC32C of all k+m cells per 512-B chunk (WritePacket::calculate_checksum), big-endian",
         }
+        if not args.encode_only and not mixed:
+            # read side: survivors' chunk sums verified while the missing data
+            # cells are rebuilt (hec_decode_verify_device: fused kernel, then a
+            # host look at the flags); vs. verify pass + decode pass
+            bad = torch.empty((S, k + m), dtype=torch.uint8, device=dev)
+            surv = [i for i in range(k + m) if shard_ptrs[i] is not None][:k]
+            sv_ptrs = [(dp + pp)[i] for i in surv]
+            sv_strides = [(ds + ps)[i] for i in surv]
+            sv_sums = sums[:, surv].contiguous()
+
+            # present data shards are repaired in place if they fail
+            vo_ptrs = [rp[i] if i in miss else dp[i] for i in range(k)]
+            vo_strides = [rs[0] if i in miss else ds[i] for i in range(k)]
+
+            def dec_verify():
+                coder.decode_verify_device(H.CHECKSUM_CRC32C, shard_ptrs, ds + ps, vo_ptrs, vo_strides, cell, S,
+                                           bpc, sums.data_ptr(), bad.data_ptr(), sp)
+
+            def verify_then_decode():
+                bad.zero_()
+                coder.checksum_verify_device(H.CHECKSUM_CRC32C, sv_ptrs, sv_strides, cell, S, bpc,
+                                             sv_sums.data_ptr(), bad.data_ptr(), sp)
+                decode()
+                torch.cuda.synchronize(dev)
+
+            for fn in (dec_verify, verify_then_decode):
+                fn()
+            torch.cuda.synchronize(dev)
+            tv = {}
+            for name, fn in (("unfused", verify_then_decode), ("fused", dec_verify)):
+                t_0 = time.perf_counter()
+                for _ in range(reps):
+                    fn()
+                torch.cuda.synchronize(dev)
+                tv[name] = (time.perf_counter() - t_0) / reps
+            assert not bad.any() and torch.equal(rec, data[:, :m]), "decode+verify mismatch"
+            e_ = len(miss)
+            result["crc32c"].update({
+                "decode_verify_GiBps": round(k * cell * S / tv["fused"] / GIB, 2),
+                "decode_verify_ms": round(tv["fused"] * 1e3, 3),
+                "decode_verify_hbm_TBps": round((k + e_) * cell * S / tv["fused"] / 1e12, 3),
+                "verify_then_decode_GiBps": round(k * cell * S / tv["unfused"] / GIB, 2),
+                "verify_then_decode_ms": round(tv["unfused"] * 1e3, 3),
+                "read_note": "CRC32C of the k survivors verified against their packet sums while data shards "
+                             f"{{{','.join(map(str, miss))}}} are rebuilt (ReadPacket::get_data + ec_decode); "
+                             "wall time of the synchronous call incl. the flag read-back",
+            })
 
     if args.host_path and rank == 0:
         hs = min(S, 256)

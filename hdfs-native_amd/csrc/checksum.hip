@@ -68,8 +68,11 @@ __device__ __forceinline__ const crc::Tables<KIND>& tables() {
 // Compute mode: store the big-endian sum.  Verify mode: flag the cell on a
 // mismatch (every flagging lane stores the same byte).
 __device__ __forceinline__ void emit_sum(const CrcArgs& a, uint64_t cell_idx, uint64_t chunk, uint32_t crc) {
-    const uint64_t stripe = cell_idx / a.n_shards;
-    const uint64_t cell = stripe * a.n_total + a.sid[cell_idx - stripe * a.n_shards];
+    uint64_t cell = cell_idx;
+    if (a.mapped) {  // launch cells are a subset of the sums layout
+        const uint64_t stripe = cell_idx / a.n_shards;
+        cell = stripe * a.n_total + a.sid[cell_idx - stripe * a.n_shards];
+    }
     const uint64_t at = cell * a.chunks_per_cell + chunk;
     if (a.expected) {
         if (reinterpret_cast<const uint32_t*>(a.expected)[at] != bswap32(crc)) a.bad[cell] = 1;
@@ -236,8 +239,11 @@ int launch_checksum(const CrcArgs& in, int device, hipStream_t stream) {
     if (a.kind != crc::kCrc32c && a.kind != crc::kCksum) return -1;
     if (a.expected && !a.bad) return -1;
     if (a.n_shards > uint32_t(kCrcMaxShards) || a.n_total < a.n_shards) return -1;
-    for (uint32_t i = 0; i < a.n_shards; i++)
+    a.mapped = a.n_total != a.n_shards;
+    for (uint32_t i = 0; i < a.n_shards; i++) {
         if (a.sid[i] >= a.n_total) return -1;
+        a.mapped |= a.sid[i] != i;
+    }
     a.chunks_per_cell = (a.cell_len + a.bytes_per_checksum - 1) / a.bytes_per_checksum;
     if (a.stripes == 0) return 0;
     bool aligned = a.cell_len % 16 == 0 && (reinterpret_cast<uintptr_t>(a.out) & 3u) == 0;

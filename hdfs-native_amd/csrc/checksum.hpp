@@ -20,6 +20,7 @@ struct CrcArgs {
     // connection.rs:477-504); out unused.
     uint8_t sid[kCrcMaxShards];
     uint32_t n_total;
+    uint32_t mapped;  // filled by the launcher: sid is not the identity
     uint8_t* out;
     const uint8_t* expected;
     uint8_t* bad;

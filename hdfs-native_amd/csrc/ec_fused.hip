@@ -112,6 +112,7 @@ __global__ __launch_bounds__(SCHEME == 1 ? 256 : 512) __attribute__((amdgpu_wave
         // `first` is a compile-time constant at every (unrolled) call site,
         // so the shard ids are scalar kernarg reads
         auto sum_cell = [&](int first) {
+            if constexpr (!VERIFY) return uint64_t(stripe) * (K + R) + first + sir;  // encode: identity layout
             const uint32_t sid = (SPR > 1 && sir > 0 && first + 1 < NSUM) ? cs.shard_id[first + 1] : cs.shard_id[first];
             return uint64_t(stripe) * cs.n_total + sid;
         };

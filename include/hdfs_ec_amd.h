@@ -211,8 +211,10 @@ int hec_checksum_verify_device(hec_coder_t *coder, int checksum_type, const uint
  * packets); a shard that fails is skipped and the next available one is
  * read instead, as read_slice drops a failing cell reader and starts the
  * next parity reader.  Every data shard that is missing or failed is
- * rebuilt into d_out[i] (out_strides as hec_decode_device); present data
- * shards that verify are not copied.  d_bad[s*(k+m) + i] = 1 marks the
+ * rebuilt into d_out[i] (out_strides as hec_decode_device; all k slots
+ * are required, and a present data shard's slot may be its own input
+ * buffer, which then is repaired in place); present data shards that
+ * verify are not copied.  d_bad[s*(k+m) + i] = 1 marks the
  * cells that failed (zeroed by the call; device memory).  When every stripe
  * verifies first time this is one fused pass over the survivors (k in
  * {2,3,6,10}, 512-B chunks, 16-B aligned); failing stripes are re-planned
