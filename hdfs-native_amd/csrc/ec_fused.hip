@@ -259,8 +259,8 @@ const void* encode_fn(int slabs, int scheme) {
 template <int K, int R>
 const void* verify_fn(int kind) {
     constexpr int SL = fused_slabs(K, R);
-    return kind == crc::kCrc32c ? reinterpret_cast<const void*>(&gf_fused_crc<K, R, SL, 4, crc::kCrc32c, true>)
-                                : reinterpret_cast<const void*>(&gf_fused_crc<K, R, SL, 4, crc::kCksum, true>);
+    return kind == crc::kCrc32c ? reinterpret_cast<const void*>(&gf_fused_crc<K, R, SL, 1, crc::kCrc32c, true>)
+                                : reinterpret_cast<const void*>(&gf_fused_crc<K, R, SL, 1, crc::kCksum, true>);
 }
 
 template <int K>
@@ -286,7 +286,11 @@ int launch_fused(const MatmulArgs& in, const FusedCrcArgs& cs, bool verify, int 
     const int slabs = verify                                               ? fused_slabs(a.k, a.r)
                       : (g_tune_fused_slabs == 4 || g_tune_fused_slabs == 8) ? g_tune_fused_slabs
                                                                              : fused_slabs(a.k, a.r);
-    const int scheme = (!verify && g_tune_crc_variant == 1) ? 1 : 4;  // checksum lookups (checksum_device.hpp)
+    // checksum lookups (checksum_device.hpp): slicing-by-8 in 256-thread
+    // blocks, 2 per CU, beats the bank-replicated tables in 512-thread blocks
+    // by 7-10 % here (profiles/r01_probe_fused_scheme.log); tune key 11 = 2
+    // selects the latter for encode
+    const int scheme = (!verify && g_tune_crc_variant == 2) ? 4 : 1;
     const int waves = scheme == 1 ? 4 : 8;
     const void* fn = nullptr;
     switch (a.k) {

@@ -268,8 +268,9 @@ int hec_decode_host_batch(hec_coder_t *coder, const uint8_t *const *h_vertical, 
  * key 8: tile order, stripes interleaved per group (1 = stripe-major; 0 = default)
  * key 9: 1 = hec_encode_crc_device as encode + separate CRC pass (0 = fused)
  * key 10: fused encode+CRC slabs per wave: 0 = default, 4 or 8
- * key 11: CRC lookups: 0 = default, 1 = slice-by-8 tables, 2 / 3 = bank-replicated
- *         slice-by-1 with 4 / 8 chains per lane; 9 = memory side only (WRONG sums)
+ * key 11: CRC lookups: 0 = default (slice-by-8), 1 = slice-by-8 tables, 2 / 3 =
+ *         bank-replicated slice-by-1 with 4 / 8 chains per lane (the fused kernels
+ *         take 2 for the 4-chain form); 9 = memory side only (WRONG sums)
  * key 12: CRC register prefetch depth in 8-KiB tasks: 0 = default (2), 1 or 2
  * Process-wide; affects launches made after the call. */
 int hec_tune_set(int key, int value);

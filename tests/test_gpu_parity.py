@@ -543,8 +543,10 @@ def test_crc32c_device_published_vector(dev):
     ("rs", 10, 4, 1 << 15, 3), ("rs", 10, 4, 70 * 512 + 256, 2), ("rs", 3, 2, 1 << 17, 3),
     ("rs", 2, 1, 8192 + 512, 4), ("rs", 12, 4, 1 << 14, 2), ("rs", 6, 3, 1000, 2), ("xor", 2, 1, 1 << 14, 3)])
 @pytest.mark.parametrize("fused", [0, 4, 8, None])
-def test_encode_crc_device(dev, c_oracle, codec, k, m, cell, S, fused):
-    """Fused encode+CRC (k in {2,3,6,10}) and the two-pass fallback (other k,
+@pytest.mark.parametrize("scheme", [0, 2])
+def test_encode_crc_device(dev, c_oracle, codec, k, m, cell, S, fused, scheme):
+    """Fused encode+CRC (k in {2,3,6,10}; slice-by-8 default or, tune key 11
+    = 2, bank-replicated CRC tables) and the two-pass fallback (other k,
     unaligned cell_len, or tune key 9) against oracle parity + oracle CRCs."""
     bpc = 512
     data = batch_data(S, k, cell, first=31 + cell)
@@ -563,12 +565,14 @@ def test_encode_crc_device(dev, c_oracle, codec, k, m, cell, S, fused):
     # fused: 0 = default slabs/wave, 4 / 8 forced; None = two-pass fallback
     H.tune_set(9, 1 if fused is None else 0)
     H.tune_set(10, fused or 0)
+    H.tune_set(11, scheme)
     try:
         cod.encode_crc_device(dp, ds, pp, ps, cell, S, bpc, sums.data_ptr(), torch.cuda.current_stream().cuda_stream)
         torch.cuda.synchronize()
     finally:
         H.tune_set(9, 0)
         H.tune_set(10, 0)
+        H.tune_set(11, 0)
     assert np.array_equal(p.cpu().numpy(), par)
     want = _oracle_sums(np.concatenate([data, par], axis=1), bpc)
     assert np.array_equal(sums.cpu().numpy(), want)
