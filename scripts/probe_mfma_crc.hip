@@ -73,6 +73,7 @@ static std::vector<int8_t> make_btiles() {
 struct ShiftTabs {
     uint32_t t[3][4][256];  // append 384 / 256 / 128 zero bytes
     uint32_t final512;
+    uint32_t slice[8][256];  // slicing-by-8 (hybrid mode)
 };
 static ShiftTabs make_shift() {
     ShiftTabs s;
@@ -89,6 +90,9 @@ static ShiftTabs make_shift() {
             }
     }
     s.final512 = host_zero(0xFFFFFFFFu, 512) ^ 0xFFFFFFFFu;
+    for (int i = 0; i < 256; i++) s.slice[0][i] = host_tab[i];
+    for (int k = 1; k < 8; k++)
+        for (int i = 0; i < 256; i++) s.slice[k][i] = host_tab[s.slice[k - 1][i] & 0xFF] ^ (s.slice[k - 1][i] >> 8);
     return s;
 }
 
@@ -97,7 +101,9 @@ static ShiftTabs make_shift() {
 // planes of MFMA -> ballots put quarter q's 32 bits in lane q -> zero-append
 // shifts + 2 xor shuffles -> one CRC per chunk.
 // MODE 0: full; 1: no MFMA (memory + staging side); 2: no global loads
-// after the first task (compute side).  PF: tasks of register prefetch.
+// after the first task (compute side); 3: hybrid -- quarters 0-31 by
+// slicing-by-8 LDS lookups (lanes 0-31), quarters 32-63 on the MFMA;
+// 4: hybrid without global loads.  PF: tasks of register prefetch.
 template <int BS, bool BREG, int PF = 1, int MODE = 0>
 __global__ __launch_bounds__(BS) void crc_mfma(const uint8_t* __restrict__ data, size_t tasks,
                                                uint32_t* __restrict__ out, const int8_t* __restrict__ btiles,
@@ -106,6 +112,9 @@ __global__ __launch_bounds__(BS) void crc_mfma(const uint8_t* __restrict__ data,
     __shared__ uint32_t s_shift[3][4][256];
     __shared__ __attribute__((aligned(16))) uint8_t s_stage[WAVES * STAGE];
     __shared__ __attribute__((aligned(16))) int8_t s_b[BREG ? 16 : 32 * 1024];
+    __shared__ uint32_t s_slice[MODE >= 3 ? 8 : 1][256];
+    if constexpr (MODE >= 3)
+        for (int t = threadIdx.x; t < 8 * 256; t += BS) (&s_slice[0][0])[t] = (&sh->slice[0][0])[t];
     for (int t = threadIdx.x; t < 3 * 4 * 256; t += BS) (&s_shift[0][0][0])[t] = (&sh->t[0][0][0])[t];
     if constexpr (!BREG)
         for (int t = threadIdx.x; t < 32 * 1024 / 16; t += BS)
@@ -134,10 +143,29 @@ __global__ __launch_bounds__(BS) void crc_mfma(const uint8_t* __restrict__ data,
             const uint32_t off = uint32_t(i) * 1024u + uint32_t(lane) * 16u;
             *reinterpret_cast<u32x4*>(stage + (off / 128) * PITCH + (off % 128)) = v[i];
         }
-        if (MODE != 2 && task + PF * step < tasks) load(task + PF * step, v);
+        if (MODE != 2 && MODE != 4 && task + PF * step < tasks) load(task + PF * step, v);
         __builtin_amdgcn_wave_barrier();
         asm volatile("" ::: "memory");
         uint32_t qv = 0;  // lane q: linear part of quarter q
+        constexpr int G0 = MODE >= 3 ? 1 : 0;  // hybrid: MFMA on row group 1 only
+        if constexpr (MODE >= 3) {
+            if (lane < 32) {
+                const uint8_t* row = stage + lane * PITCH;
+                uint32_t r = 0;
+#pragma unroll
+                for (int t = 0; t < 8; t++) {
+                    const u32x4 w = *reinterpret_cast<const u32x4*>(row + t * 16);
+#pragma unroll
+                    for (int h = 0; h < 2; h++) {
+                        const uint32_t lo = (h ? w.z : w.x) ^ r, hi = h ? w.w : w.y;
+                        r = s_slice[7][lo & 0xFF] ^ s_slice[6][(lo >> 8) & 0xFF] ^ s_slice[5][(lo >> 16) & 0xFF] ^
+                            s_slice[4][lo >> 24] ^ s_slice[3][hi & 0xFF] ^ s_slice[2][(hi >> 8) & 0xFF] ^
+                            s_slice[1][(hi >> 16) & 0xFF] ^ s_slice[0][hi >> 24];
+                    }
+                }
+                qv = r;
+            }
+        }
         // both row groups at once: two independent accumulation chains share
         // each B tile
         i32x16 acc[2] = {};
@@ -145,7 +173,7 @@ __global__ __launch_bounds__(BS) void crc_mfma(const uint8_t* __restrict__ data,
         for (int s = 0; s < 4; s++) {
             u32x4 a[2];
 #pragma unroll
-            for (int g = 0; g < 2; g++)
+            for (int g = G0; g < 2; g++)
                 a[g] = *reinterpret_cast<const u32x4*>(stage + (32 * g + (lane & 31)) * PITCH + 32 * s + 16 * (lane >> 5));
 #pragma unroll
             for (int b = 0; b < 8; b++) {
@@ -156,7 +184,7 @@ __global__ __launch_bounds__(BS) void crc_mfma(const uint8_t* __restrict__ data,
                 else
                     bb = *reinterpret_cast<const u32x4*>(s_b + ((s * 8 + b) * 64 + lane) * 16);
 #pragma unroll
-                for (int g = 0; g < 2; g++) {
+                for (int g = G0; g < 2; g++) {
                     const u32x4 am = u32x4{a[g].x & m, a[g].y & m, a[g].z & m, a[g].w & m};
                     if constexpr (MODE == 1)
                         acc[g][b] ^= am.x ^ bb.y;
@@ -167,7 +195,7 @@ __global__ __launch_bounds__(BS) void crc_mfma(const uint8_t* __restrict__ data,
             }
         }
 #pragma unroll
-        for (int g = 0; g < 2; g++) {
+        for (int g = G0; g < 2; g++) {
             // D[row][col]: col = lane&31 = CRC bit, row = (i&3) + 8*(i>>2) + 4*(lane>>5).
             // Ballots -> SGPRs; v_writelane reads an SGPR a VALU (v_cmp) just
             // wrote, which needs wait states that hipcc does not add inside asm
@@ -278,11 +306,12 @@ int main() {
     int cus = 256;
     for (int rep = 0; rep < 2; rep++) {
         run<256, true, 1, 0>("breg pf1 full", d, tasks, o, bt, st, cus * 2, host, hout);
-        run<256, true, 2, 0>("breg pf2 full", d, tasks, o, bt, st, cus * 2, host, hout);
-        run<256, true, 2, 1>("breg pf2 no-mfma", d, tasks, o, bt, st, cus * 2, host, hout);
-        run<256, true, 2, 2>("breg pf2 no-loads", d, tasks, o, bt, st, cus * 2, host, hout);
-        run<256, false, 2, 0>("blds pf2 full", d, tasks, o, bt, st, cus * 2, host, hout);
-        run<512, false, 2, 0>("blds bs512 pf2 full", d, tasks, o, bt, st, cus * 1, host, hout);
+        run<256, true, 1, 2>("breg pf1 no-loads", d, tasks, o, bt, st, cus * 2, host, hout);
+        run<256, true, 1, 3>("breg pf1 hybrid", d, tasks, o, bt, st, cus * 2, host, hout);
+        run<256, true, 2, 3>("breg pf2 hybrid", d, tasks, o, bt, st, cus * 2, host, hout);
+        run<256, true, 1, 4>("breg pf1 hybrid no-loads", d, tasks, o, bt, st, cus * 2, host, hout);
+        run<256, false, 2, 3>("blds pf2 hybrid", d, tasks, o, bt, st, cus * 2, host, hout);
+        run<512, false, 2, 3>("blds bs512 pf2 hybrid", d, tasks, o, bt, st, cus * 1, host, hout);
     }
     return 0;
 }
