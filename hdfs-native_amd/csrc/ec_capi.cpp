@@ -1059,7 +1059,8 @@ int hec_decode_verify_device(hec_coder_t* c, int checksum_type, const uint8_t* c
 // A value of 0 (-1 for key 2) restores the per-shape default.
 // key 1 = 16-B column chunks per lane (1|2|4), 2 = non-temporal loads/stores
 // (0|1), 3 = resident blocks per CU, 4 = threads per block (256|512),
-// 5 = pipeline (1 = register kernel, 2 = LDS-DMA prefetch kernel),
+// 5 = pipeline (1 = register kernel, 2 = LDS-DMA prefetch kernel, 3 = register
+//     double-buffered kernel),
 // 6 = chunk mapping (1 = block slabs, 2 = wave-contiguous runs), 7 = grid size,
 // 8 = tile-order group (stripes interleaved column-major; 1 = stripe-major),
 // 9 = 1: hec_encode_crc_device as two passes (encode, then CRC) instead of fused,
@@ -1067,11 +1068,13 @@ int hec_decode_verify_device(hec_coder_t* c, int checksum_type, const uint8_t* c
 // 11 = CRC lookup scheme (0 default, 1 slice-by-8 tables, 2 / 3 bank-replicated
 //      slice-by-1 with 4 / 8 chains per lane; 9 = loads + staging only, WRONG
 //      sums: measures the kernel's memory side),
-// 12 = CRC kernel register prefetch depth in tasks (0 default = 2, 1 or 2).
+// 12 = CRC kernel register prefetch depth in tasks (0 default = 2, 1 or 2),
+// 13 = store cache policy of the register double-buffered kernel (key 5 = 3)
+//      at RS(6,3) / RS(10,4): 0 nt, 1 sc1, 2 sc0 sc1, 3 nt sc1, 4 plain.
 int hec_tune_set(int key, int value) {
     switch (key) {
         case 1:
-            if (value != 0 && value != 1 && value != 2 && value != 4) return HEC_ERR_INVALID_ARG;
+            if (value < 0 || value > 4) return HEC_ERR_INVALID_ARG;
             hec::g_tune_unroll = value;
             return HEC_OK;
         case 2: hec::g_tune_nt = value < 0 ? -1 : (value ? 1 : 0); return HEC_OK;
@@ -1084,7 +1087,7 @@ int hec_tune_set(int key, int value) {
             hec::g_tune_block = value;
             return HEC_OK;
         case 5:
-            if (value < 0 || value > 2) return HEC_ERR_INVALID_ARG;
+            if (value < 0 || value > 3) return HEC_ERR_INVALID_ARG;
             hec::g_tune_pipeline = value;
             return HEC_OK;
         case 6:
@@ -1113,6 +1116,10 @@ int hec_tune_set(int key, int value) {
         case 12:
             if (value < 0 || value > 2) return HEC_ERR_INVALID_ARG;
             hec::g_tune_crc_prefetch = value;
+            return HEC_OK;
+        case 13:
+            if (value < 0 || value > 4) return HEC_ERR_INVALID_ARG;
+            hec::g_tune_store_pol = value;
             return HEC_OK;
         default: return HEC_ERR_INVALID_ARG;
     }

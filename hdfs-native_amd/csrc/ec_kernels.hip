@@ -23,6 +23,7 @@
 //    with LDS log/antilog lookups -- same results, correctness path.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 
 #include "ec_kernels.hpp"
@@ -311,6 +312,137 @@ __global__ __launch_bounds__(BS) void gf_matmul_dma(MatmulArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Register double-buffered kernel (compile-time K only).  Two register sets
+// of K x U chunks: the loads of tile t+1 are issued before tile t is
+// computed, so a wave always has one tile of loads in flight during its GF
+// math (the LDS-DMA kernel's overlap without the LDS round trip).
+//  * Loads and stores address as (uniform stripe base) + 32-bit lane offset
+//    (global_* saddr form), and the next tile's coordinates are computed
+//    while the accumulators are still live, before the stores: no VGPR
+//    temporary is written after a store is issued, so the waitcnt pass never
+//    has to drain the in-flight loads to protect store data registers.
+//  * Per input, the U chunks are walked u-outer with all R coefficient
+//    tables live, so only one chunk's selectors are live at a time.
+// ---------------------------------------------------------------------------
+template <int U>
+struct PipeCoords {
+    uint32_t stripe;
+    uint32_t off[U];  // byte offset of chunk u (clamped into the cell)
+    bool live[U];
+};
+
+template <int U, int BS>
+__device__ __forceinline__ PipeCoords<U> pipe_coords(const MatmulArgs& a, uint32_t tile) {
+    PipeCoords<U> c;
+    uint32_t tcol;
+    tile_coords(tile < a.total_tiles ? tile : a.total_tiles - 1, a, c.stripe, tcol);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const uint32_t col = tcol * (BS * U) + u * BS + threadIdx.x;
+        c.live[u] = tile < a.total_tiles && col < a.chunks;
+        c.off[u] = (col < a.chunks ? col : a.chunks - 1) * 16u;  // dead lanes fetch a valid chunk
+    }
+    return c;
+}
+
+template <int K, int U>
+__device__ __forceinline__ void pipe_load(const MatmulArgs& a, const PipeCoords<U>& c, u32x4 (&x)[U][K]) {
+#pragma unroll
+    for (int i = 0; i < K; i++) {
+        const uint8_t* base = a.in[i] + uint64_t(c.stripe) * a.in_stride[i];
+#pragma unroll
+        for (int u = 0; u < U; u++) x[u][i] = load16<true>(base + c.off[u]);
+    }
+}
+
+template <int K, int R, int U>
+__device__ __forceinline__ void pipe_compute(const u32x4 (&x)[U][K], const PermTable (*s_tab)[kMaxK],
+                                             u32x4 (&acc)[U][R]) {
+#pragma unroll
+    for (int u = 0; u < U; u++)
+#pragma unroll
+        for (int j = 0; j < R; j++) acc[u][j] = u32x4{0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < K; i++) {
+        uint32_t toff = uint32_t(i) * uint32_t(sizeof(PermTable));
+        asm volatile("" : "+v"(toff));
+#pragma unroll
+        for (int u = 0; u < U; u++)
+#pragma unroll
+            for (int j = 0; j < R; j++) asm volatile("" : "+v"(acc[u][j]) : "v"(toff));
+        uint32_t tb[R][5];
+#pragma unroll
+        for (int j = 0; j < R; j++) {
+            const PermTable& t =
+                *reinterpret_cast<const PermTable*>(reinterpret_cast<const char*>(&s_tab[j][0]) + toff);
+            tb[j][0] = t.t0lo;
+            tb[j][1] = t.t0hi;
+            tb[j][2] = t.t1lo;
+            tb[j][3] = t.t1hi;
+            tb[j][4] = t.t2;
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++)
+#pragma unroll
+            for (int d = 0; d < 4; d++) {
+                const Sel s = make_sel(x[u][i][d]);
+#pragma unroll
+                for (int j = 0; j < R; j++)
+                    acc[u][j][d] ^= gf_mul4(tb[j][0], tb[j][1], tb[j][2], tb[j][3], tb[j][4], s.s0, s.s1, s.s2);
+            }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+template <int R, int U, int POL>
+__device__ __forceinline__ void pipe_store(const MatmulArgs& a, const PipeCoords<U>& c, const u32x4 (&acc)[U][R]) {
+#pragma unroll
+    for (int j = 0; j < R; j++) {
+        uint8_t* base = a.out[j] + uint64_t(c.stripe) * a.out_stride[j];
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            if (c.live[u]) store16p<POL>(base + c.off[u], acc[u][j]);
+    }
+}
+
+template <int K, int R, int U, int BS, int POL = 0>
+__global__ __launch_bounds__(BS) void gf_matmul_pipe(MatmulArgs a) {
+    static_assert(K > 0, "pipelined kernel needs a compile-time input count");
+    __shared__ PermTable s_tab[R][kMaxK];
+    __shared__ uint8_t s_exp[512];
+    __shared__ uint8_t s_log[256];
+    __shared__ uint8_t s_coef[R * kMaxK];
+    prologue<R, BS>(a, K, s_tab, s_exp, s_log, s_coef);
+    const uint32_t total = a.total_tiles;
+    const uint32_t step = gridDim.x;
+    u32x4 xa[U][K], xb[U][K], acc[U][R];
+    // Tiles past the end load a clamped (valid) tile and store nothing.
+    uint32_t tile = blockIdx.x;
+    PipeCoords<U> ca = pipe_coords<U, BS>(a, tile);
+    PipeCoords<U> cb = pipe_coords<U, BS>(a, tile + step);
+    pipe_load<K, U>(a, ca, xa);
+    for (; tile < total; tile += 2 * step) {
+        pipe_load<K, U>(a, cb, xb);  // tile + step
+        __builtin_amdgcn_sched_barrier(0);
+        pipe_compute<K, R, U>(xa, s_tab, acc);
+        PipeCoords<U> cur = ca;
+        ca = pipe_coords<U, BS>(a, tile + 2 * step);
+        __builtin_amdgcn_sched_barrier(0);
+        pipe_store<R, U, POL>(a, cur, acc);
+        __builtin_amdgcn_sched_barrier(0);
+        if (tile + step >= total) break;  // wave-uniform
+        pipe_load<K, U>(a, ca, xa);  // tile + 2 step
+        __builtin_amdgcn_sched_barrier(0);
+        pipe_compute<K, R, U>(xb, s_tab, acc);
+        cur = cb;
+        cb = pipe_coords<U, BS>(a, tile + 3 * step);
+        __builtin_amdgcn_sched_barrier(0);
+        pipe_store<R, U, POL>(a, cur, acc);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Mixed-pattern decode: every stripe carries its own erasure pattern (plan
 // index), as a striped read over many block groups does.  Same register
 // kernel shape as gf_matmul_v16; per tile the block looks up the stripe's
@@ -569,6 +701,50 @@ const void* pick_dma(int k, int r, int unroll, int bs) {
     return dma_pick<2, 256>(k, r);
 }
 
+// Register double-buffered kernel: K in {2,3,6} at U in {1,2,3} (256
+// threads) and K = 10 at U in {1,2}.
+template <int K, int U>
+const void* pipe_pick_r(int r) {
+    switch (r) {
+        case 1: return reinterpret_cast<const void*>(&gf_matmul_pipe<K, 1, U, 256>);
+        case 2: return reinterpret_cast<const void*>(&gf_matmul_pipe<K, 2, U, 256>);
+        case 3: return reinterpret_cast<const void*>(&gf_matmul_pipe<K, 3, U, 256>);
+        default: return reinterpret_cast<const void*>(&gf_matmul_pipe<K, 4, U, 256>);
+    }
+}
+
+template <int U>
+const void* pipe_pick_k(int k, int r) {
+    switch (k) {
+        case 2: return pipe_pick_r<2, U>(r);
+        case 3: return pipe_pick_r<3, U>(r);
+        case 6: return pipe_pick_r<6, U>(r);
+        default: return nullptr;
+    }
+}
+
+template <int K, int R, int U>
+const void* pipe_pol(int pol) {
+    switch (pol) {
+        case 1: return reinterpret_cast<const void*>(&gf_matmul_pipe<K, R, U, 256, 1>);
+        case 2: return reinterpret_cast<const void*>(&gf_matmul_pipe<K, R, U, 256, 2>);
+        case 3: return reinterpret_cast<const void*>(&gf_matmul_pipe<K, R, U, 256, 3>);
+        default: return reinterpret_cast<const void*>(&gf_matmul_pipe<K, R, U, 256, 4>);
+    }
+}
+
+const void* pick_pipe(int k, int r, int unroll) {
+    // store-policy variants only at the bench shapes (RS(6,3), RS(10,4))
+    if (g_tune_store_pol > 0 && unroll <= 2 && ((k == 6 && r == 3) || (k == 10 && r == 4))) {
+        if (k == 6) return unroll == 2 ? pipe_pol<6, 3, 2>(g_tune_store_pol) : pipe_pol<6, 3, 1>(g_tune_store_pol);
+        return unroll == 2 ? pipe_pol<10, 4, 2>(g_tune_store_pol) : pipe_pol<10, 4, 1>(g_tune_store_pol);
+    }
+    if (k == 10) return unroll >= 2 ? pipe_pick_r<10, 2>(r) : pipe_pick_r<10, 1>(r);
+    if (unroll >= 3) return pipe_pick_k<3>(k, r);
+    if (unroll == 2) return pipe_pick_k<2>(k, r);
+    return pipe_pick_k<1>(k, r);
+}
+
 int g_num_cus[64] = {0};
 
 int num_cus(int dev) {
@@ -593,6 +769,7 @@ int g_tune_grid = 0;           // 0 = blocks_per_cu * CUs, else absolute block c
 int g_tune_group = 0;          // 0 = default (1), else stripes per tile-order group
 int g_tune_crc_unfused = 0;    // 1 = hec_encode_crc_device as two passes
 int g_tune_crc_variant = 0;    // 0 = default, 1 = slice-by-8 CRC, 2/3 = bank-replicated slice-by-1, 4/8 chains
+int g_tune_store_pol = 0;      // 0 = nt stores, else store16p policy (register double-buffered kernel)
 int g_tune_crc_prefetch = 0;   // 0 = default (2), else tasks of register prefetch per wave (1 or 2)
 int g_tune_fused_slabs = 0;    // 0 = default, 4 / 8 = slabs per wave of the fused encode+CRC
 
@@ -606,6 +783,7 @@ struct Shape {
     bool nt;
     bool dma;
     int map;  // chunk_col mapping (U=4, 256 threads only)
+    bool rpipe = false;  // register double-buffered kernel
 };
 
 Shape default_shape(int k, uint64_t cell_len) {
@@ -635,12 +813,21 @@ int launch_gf_matmul(const MatmulArgs& in, int device, hipStream_t stream) {
         if (g_tune_block) sh.block = g_tune_block;
         if (g_tune_nt >= 0) sh.nt = g_tune_nt != 0;
         if (g_tune_blocks_per_cu) sh.blocks_per_cu = g_tune_blocks_per_cu;
-        if (g_tune_pipeline) sh.dma = g_tune_pipeline == 2;
+        if (g_tune_pipeline) {
+            sh.dma = g_tune_pipeline == 2;
+            sh.rpipe = g_tune_pipeline == 3;
+        }
         if (g_tune_map) sh.map = g_tune_map - 1;
         if (g_tune_grid) sh.blocks_per_cu = 0;
         if (sh.block == 512 && sh.unroll > 2) sh.unroll = 2;
         const bool dma_ok = (a.k == 2 || a.k == 3 || a.k == 6 || a.k == 10);
         if (sh.dma && !dma_ok) sh.dma = false;
+        if (sh.rpipe && !dma_ok) sh.rpipe = false;
+        if (sh.rpipe) {
+            sh.dma = false;
+            sh.block = 256;
+            sh.unroll = std::min(sh.unroll, a.k == 10 ? 2 : 3);
+        }
         if (sh.dma) {
             if (a.k == 10) {
                 sh.unroll = 2;
@@ -655,15 +842,17 @@ int launch_gf_matmul(const MatmulArgs& in, int device, hipStream_t stream) {
         const uint64_t tps = (chunks + tile - 1) / tile;
         const uint64_t total = tps * a.stripes;
         if (chunks > 0xFFFFFFFFull || total > 0xFFFFFFFFull) return -1;
+        if (sh.rpipe && total > 0xFFF00000ull) return -1;  // tile + 3 * grid stays in 32 bits
         a.chunks = uint32_t(chunks);
         a.tiles_per_stripe = uint32_t(tps);
         a.total_tiles = uint32_t(total);
         // 4 stripes column-interleaved: +1-4 % over stripe-major at 1 MiB
         // cells (profiles/r01_probe_tile_order.log)
         a.group = g_tune_group > 0 ? uint32_t(g_tune_group) : 4u;
-        const void* fn = sh.dma ? pick_dma(a.k, a.r, sh.unroll, sh.block)
-                                : (sh.nt ? pick_shape<true>(a.k, a.r, sh.unroll, sh.block, sh.map)
-                                         : pick_shape<false>(a.k, a.r, sh.unroll, sh.block, sh.map));
+        const void* fn = sh.rpipe ? pick_pipe(a.k, a.r, sh.unroll)
+                         : sh.dma ? pick_dma(a.k, a.r, sh.unroll, sh.block)
+                                  : (sh.nt ? pick_shape<true>(a.k, a.r, sh.unroll, sh.block, sh.map)
+                                           : pick_shape<false>(a.k, a.r, sh.unroll, sh.block, sh.map));
         uint64_t grid = g_tune_grid ? uint64_t(g_tune_grid) : uint64_t(cus) * sh.blocks_per_cu;
         if (grid > total) grid = total;
         void* args[] = {&a};

@@ -275,6 +275,63 @@ def test_pipelines_vs_oracle(dev, c_oracle, pipeline, k, m, cell):
     assert torch.equal(out[:, :m], d[:, :m])
 
 
+@pytest.mark.parametrize("unroll", [1, 2, 3])
+@pytest.mark.parametrize("grid", [0, 1, 5, 6])
+@pytest.mark.parametrize("k,m", [(2, 1), (3, 2), (6, 3), (10, 4)])
+def test_register_double_buffer_vs_oracle(dev, c_oracle, unroll, grid, k, m):
+    # tune key 5 = 3: register double-buffered kernel.  Small grids walk many
+    # tiles per block (both register sets, odd and even tile counts, the
+    # clamped past-the-end prefetch); the cell leaves a partial last tile.
+    S, cell = 3, 3 * 65536 + 48
+    data = batch_data(S, k, cell, first=cell + 7 * k + unroll)
+    want = oracle_batch_encode(c_oracle, k, m, data)
+    d = torch.from_numpy(data).to(dev)
+    p = torch.zeros((S, m, cell), dtype=torch.uint8, device=dev)
+    try:
+        H.tune_set(5, 3)
+        H.tune_set(1, unroll)
+        H.tune_set(7, grid)
+        H.encode_batch(coder(k, m), d, p)
+        out = torch.zeros_like(d)
+        H.decode_batch(coder(k, m), d, p, list(range(m)), out)
+        torch.cuda.synchronize()
+    finally:
+        H.tune_set(5, 0)
+        H.tune_set(1, 0)
+        H.tune_set(7, 0)
+    assert np.array_equal(p.cpu().numpy(), want)
+    assert torch.equal(out[:, :m], d[:, :m])
+
+
+@pytest.mark.parametrize("pol", [1, 2, 3, 4])
+@pytest.mark.parametrize("unroll", [1, 2])
+@pytest.mark.parametrize("k,m", [(6, 3), (10, 4)])
+def test_store_policies_vs_oracle(dev, c_oracle, pol, unroll, k, m):
+    # tune key 13: cache policy of the double-buffered kernel's stores
+    # (sc1 / sc0 sc1 / nt sc1 / plain, inline-asm stores) at the bench shapes
+    S, cell = 5, 65536 + 32
+    data = batch_data(S, k, cell, first=pol * 31 + unroll)
+    want = oracle_batch_encode(c_oracle, k, m, data)
+    d = torch.from_numpy(data).to(dev)
+    p = torch.zeros((S, m, cell), dtype=torch.uint8, device=dev)
+    try:
+        H.tune_set(5, 3)
+        H.tune_set(1, unroll)
+        H.tune_set(13, pol)
+        H.tune_set(7, 7)
+        H.encode_batch(coder(k, m), d, p)
+        out = torch.zeros_like(d)
+        H.decode_batch(coder(k, m), d, p, list(range(m)), out)
+        torch.cuda.synchronize()
+    finally:
+        H.tune_set(5, 0)
+        H.tune_set(1, 0)
+        H.tune_set(13, 0)
+        H.tune_set(7, 0)
+    assert np.array_equal(p.cpu().numpy(), want)
+    assert torch.equal(out[:, :m], d[:, :m])
+
+
 @pytest.mark.parametrize("S,chunk,cell", [(9, 4, 65536), (23, 2, 65536), (7, 7, 4096 + 16), (5, 1, 1000)])
 def test_encode_host_batch_pinned(c_oracle, S, chunk, cell):
     # more chunks than device slots, partial last chunk, tails
