@@ -17,6 +17,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <new>
 #include <unordered_map>
 #include <vector>
@@ -1071,6 +1072,124 @@ int hec_decode_verify_device(hec_coder_t* c, int checksum_type, const uint8_t* c
 // 12 = CRC kernel register prefetch depth in tasks (0 default = 2, 1 or 2),
 // 13 = store cache policy of the register double-buffered kernel (key 5 = 3)
 //      at RS(6,3) / RS(10,4): 0 nt, 1 sc1, 2 sc0 sc1, 3 nt sc1, 4 plain.
+// ---- multi-GPU coder group -----------------------------------
+
+}  // extern "C"
+
+struct hec_group {
+    std::vector<hec_coder_t*> coders;  // one per slot
+};
+
+namespace {
+
+void group_range(size_t total, size_t n, size_t i, size_t* first, size_t* count) {
+    const size_t base = total / n, extra = total % n;  // hdfs_native_ec.dist.shard_range
+    *first = i * base + std::min(i, extra);
+    *count = base + (i < extra ? 1 : 0);
+}
+
+// Runs body(slot) for every slot, slots 1.. on their own threads and slot 0 on
+// the caller's; returns the lowest failing slot's status and copies its
+// hec_last_error() text into the caller's thread.
+template <class F>
+int group_run(hec_group* g, F&& body) {
+    const size_t n = g->coders.size();
+    std::vector<int> rc(n, HEC_OK);
+    std::vector<std::string> err(n);
+    auto run = [&](size_t i) {
+        rc[i] = body(i);
+        if (rc[i] != HEC_OK) err[i] = g_last_error;
+    };
+    std::vector<std::thread> th;
+    th.reserve(n);
+    for (size_t i = 1; i < n; i++) th.emplace_back(run, i);
+    run(0);
+    for (auto& t : th) t.join();
+    for (size_t i = 0; i < n; i++)
+        if (rc[i] != HEC_OK) {
+            std::snprintf(g_last_error, sizeof(g_last_error), "group slot %zu: %s", i, err[i].c_str());
+            return rc[i];
+        }
+    return HEC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hec_group_create(const char* codec, size_t data_units, size_t parity_units, const int* devices,
+                     size_t n_devices, hec_group_t** out) {
+    if (!out) return HEC_ERR_INVALID_ARG;
+    *out = nullptr;
+    if (!devices || n_devices == 0 || n_devices > 64) return HEC_ERR_INVALID_ARG;
+    return guarded([&] {
+        auto* g = new hec_group();
+        for (size_t i = 0; i < n_devices; i++) {
+            hec_coder_t* c = nullptr;
+            const int rc = hec_coder_create_codec(codec, data_units, parity_units, devices[i], &c);
+            if (rc != HEC_OK) {
+                hec_group_destroy(g);
+                return rc;
+            }
+            g->coders.push_back(c);
+        }
+        *out = g;
+        return HEC_OK;
+    });
+}
+
+void hec_group_destroy(hec_group_t* g) {
+    if (!g) return;
+    for (auto* c : g->coders) hec_coder_destroy(c);
+    delete g;
+}
+
+size_t hec_group_size(const hec_group_t* g) { return g ? g->coders.size() : 0; }
+
+hec_coder_t* hec_group_coder(hec_group_t* g, size_t slot) {
+    return (g && slot < g->coders.size()) ? g->coders[slot] : nullptr;
+}
+
+int hec_group_range(const hec_group_t* g, size_t total, size_t slot, size_t* first, size_t* count) {
+    if (!g || !first || !count || slot >= g->coders.size()) return HEC_ERR_INVALID_ARG;
+    group_range(total, g->coders.size(), slot, first, count);
+    return HEC_OK;
+}
+
+int hec_group_encode_host_batch(hec_group_t* g, const uint8_t* h_data, uint8_t* h_parity, size_t cell_len,
+                                size_t stripes, size_t chunk_stripes) {
+    if (!g || !h_data || !h_parity || cell_len == 0 || chunk_stripes == 0) return HEC_ERR_INVALID_ARG;
+    if (stripes == 0) return HEC_OK;
+    return guarded([&] {
+        return group_run(g, [&](size_t i) {
+            hec_coder_t* c = g->coders[i];
+            size_t first, count;
+            group_range(stripes, g->coders.size(), i, &first, &count);
+            if (count == 0) return int(HEC_OK);
+            return hec_encode_host_batch(c, h_data + first * c->k * cell_len, h_parity + first * c->m * cell_len,
+                                         cell_len, count, chunk_stripes);
+        });
+    });
+}
+
+int hec_group_decode_host_batch(hec_group_t* g, const uint8_t* const* h_vertical, size_t cell_len, size_t rows,
+                                uint8_t* h_file, size_t chunk_rows) {
+    if (!g || !h_vertical || !h_file || cell_len == 0 || chunk_rows == 0) return HEC_ERR_INVALID_ARG;
+    if (rows == 0) return HEC_OK;
+    return guarded([&] {
+        return group_run(g, [&](size_t i) {
+            hec_coder_t* c = g->coders[i];
+            size_t first, count;
+            group_range(rows, g->coders.size(), i, &first, &count);
+            if (count == 0) return int(HEC_OK);
+            const uint8_t* vert[HEC_MAX_DATA_UNITS + HEC_MAX_PARITY_UNITS];
+            for (size_t s = 0; s < c->k + c->m; s++)
+                vert[s] = h_vertical[s] ? h_vertical[s] + first * cell_len : nullptr;
+            return hec_decode_host_batch(c, vert, cell_len, count, h_file + first * c->k * cell_len, chunk_rows);
+        });
+    });
+}
+
 int hec_tune_set(int key, int value) {
     switch (key) {
         case 1:

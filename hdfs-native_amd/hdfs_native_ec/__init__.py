@@ -44,7 +44,8 @@ EXPORTS = [
     "hec_encode_host_batch", "hec_tune_set", "hec_decode_mixed_workspace_size",
     "hec_decode_device_mixed", "hec_coder_create_codec", "hec_decode_host_batch",
     "hec_crc32c_device", "hec_encode_crc_device", "hec_checksum_device", "hec_checksum_verify_device",
-    "hec_decode_verify_device",
+    "hec_decode_verify_device", "hec_group_create", "hec_group_destroy", "hec_group_size", "hec_group_coder",
+    "hec_group_range", "hec_group_encode_host_batch", "hec_group_decode_host_batch",
 ]
 
 
@@ -123,6 +124,13 @@ def _load() -> ctypes.CDLL:
         "hec_tune_set": ([I, I], I),
         "hec_decode_mixed_workspace_size": ([P, S], S),
         "hec_decode_device_mixed": ([P, PP, SP, PP, SP, ctypes.POINTER(ctypes.c_uint64), S, S, P, S, P], I),
+        "hec_group_create": ([ctypes.c_char_p, S, S, ctypes.POINTER(I), S, ctypes.POINTER(P)], I),
+        "hec_group_destroy": ([P], None),
+        "hec_group_size": ([P], S),
+        "hec_group_coder": ([P, S], P),
+        "hec_group_range": ([P, S, S, SP, SP], I),
+        "hec_group_encode_host_batch": ([P, P, P, S, S, S], I),
+        "hec_group_decode_host_batch": ([P, PP, S, S, P, S], I),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)
@@ -454,3 +462,60 @@ def decode_batch(coder: Coder, data, parity, missing: Sequence[int], out, stream
     miss = set(missing)
     ptrs = [None if i in miss else dp[i] for i in range(k)] + pp
     coder.decode_device(ptrs, ds + ps, op, os_, data.shape[2], data.shape[0], s.cuda_stream)
+
+
+class _Borrowed(Coder):
+    """A group slot's coder: the group owns (and destroys) the handle."""
+
+    def __init__(self, handle, k, m, device, codec):  # noqa: D107 (no super().__init__: no new coder)
+        self._h = handle
+        self.codec, self.data_units, self.parity_units, self.device = codec, k, m, device
+
+    def close(self) -> None:
+        self._h = None
+
+
+class CoderGroup:
+    """Multi-GPU coder group (hec_group_*): a batch split into
+    contiguous stripe ranges, one per device, each on its own host thread."""
+
+    def __init__(self, data_units: int, parity_units: int, devices: Sequence[int], codec: str = "rs"):
+        h = ctypes.c_void_p()
+        devs = (ctypes.c_int * len(devices))(*devices)
+        _check(lib.hec_group_create(codec.encode(), data_units, parity_units, devs, len(devices), ctypes.byref(h)))
+        self._h = h
+        self.data_units, self.parity_units, self.devices, self.codec = data_units, parity_units, list(devices), codec
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            lib.hec_group_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __len__(self) -> int:
+        return lib.hec_group_size(self._h)
+
+    def coder(self, slot: int) -> Coder:
+        h = lib.hec_group_coder(self._h, slot)
+        if not h:
+            raise IndexError(slot)
+        return _Borrowed(ctypes.c_void_p(h), self.data_units, self.parity_units, self.devices[slot], self.codec)
+
+    def range(self, total: int, slot: int):
+        first, count = ctypes.c_size_t(), ctypes.c_size_t()
+        _check(lib.hec_group_range(self._h, total, slot, ctypes.byref(first), ctypes.byref(count)))
+        return first.value, count.value
+
+    def encode_host_batch(self, h_data_addr: int, h_parity_addr: int, cell_len: int, stripes: int,
+                          chunk_stripes: int) -> None:
+        _check(lib.hec_group_encode_host_batch(self._h, ctypes.c_void_p(h_data_addr), ctypes.c_void_p(h_parity_addr),
+                                               cell_len, stripes, chunk_stripes))
+
+    def decode_host_batch(self, vertical_addrs, cell_len: int, rows: int, h_file_addr: int, chunk_rows: int) -> None:
+        _check(lib.hec_group_decode_host_batch(self._h, _pp([a or 0 for a in vertical_addrs]), cell_len, rows,
+                                               ctypes.c_void_p(h_file_addr), chunk_rows))

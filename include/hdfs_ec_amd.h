@@ -257,12 +257,46 @@ int hec_encode_host_batch(hec_coder_t *coder, const uint8_t *h_data, uint8_t *h_
 int hec_decode_host_batch(hec_coder_t *coder, const uint8_t *const *h_vertical, size_t cell_len, size_t rows,
                           uint8_t *h_file, size_t chunk_rows);
 
+/* ---- Multi-GPU coder group --------------------------------- *
+ * Stripes are independent, so a batch is split into contiguous stripe ranges,
+ * one per device, and each range runs on its own device's coder from its own
+ * host thread (own streams and 3-slot pipeline), with no collective and no
+ * device-to-device traffic.  This is the in-process form of the stripe
+ * sharding the bench does with one process per GPU.  Range of device slot i
+ * for `total` stripes: sizes differ by at most one and tile [0, total) in slot
+ * order (hec_group_range).  A device may appear more than once (several
+ * coders on one GPU).  The group calls are synchronous; on failure they
+ * return the status of the lowest failing slot (hec_last_error() of the
+ * calling thread carries its detail) after every slot has finished. */
+typedef struct hec_group hec_group_t;
+
+/* codec "rs" or "xor" as hec_coder_create_codec; n_devices in 1..64. */
+int hec_group_create(const char *codec, size_t data_units, size_t parity_units, const int *devices,
+                     size_t n_devices, hec_group_t **out);
+void hec_group_destroy(hec_group_t *group);
+size_t hec_group_size(const hec_group_t *group);
+/* Slot i's coder (owned by the group), for device-resident calls on that GPU. */
+hec_coder_t *hec_group_coder(hec_group_t *group, size_t slot);
+/* Slot i's contiguous share [*first, *first + *count) of `total` stripes. */
+int hec_group_range(const hec_group_t *group, size_t total, size_t slot, size_t *first, size_t *count);
+
+/* hec_encode_host_batch over the group: slot i encodes its stripe range of
+ * the [stripe][k][cell] host batch into the same rows of h_parity. */
+int hec_group_encode_host_batch(hec_group_t *group, const uint8_t *h_data, uint8_t *h_parity, size_t cell_len,
+                                size_t stripes, size_t chunk_stripes);
+
+/* hec_decode_host_batch over the group: slot i decodes its row range (its
+ * part of every vertical buffer) into its rows of h_file. */
+int hec_group_decode_host_batch(hec_group_t *group, const uint8_t *const *h_vertical, size_t cell_len,
+                                size_t rows, uint8_t *h_file, size_t chunk_rows);
+
 /* ---- Measurement knobs (not part of the reference interface) ---------- *
- * key 1: 16-B column chunks per lane per tile (1, 2 or 4; 0 = default)
+ * key 1: 16-B column chunks per lane per tile (1, 2, 3 or 4; 0 = default)
  * key 2: non-temporal global loads/stores (0 or 1; -1 = default on)
  * key 3: resident blocks per CU for the grid (1..16; 0 = default)
  * key 4: threads per block (256 or 512; 0 = default)
- * key 5: kernel pipeline (1 = register, 2 = LDS-DMA prefetch; 0 = default)
+ * key 5: kernel pipeline (1 = register, 2 = LDS-DMA prefetch, 3 = register
+ *        double-buffered; 0 = default)
  * key 6: chunk mapping (1 = block slabs, 2 = wave-contiguous runs; 0 = default)
  * key 7: absolute grid size in blocks (0 = default)
  * key 8: tile order, stripes interleaved per group (1 = stripe-major; 0 = default)
@@ -272,6 +306,8 @@ int hec_decode_host_batch(hec_coder_t *coder, const uint8_t *const *h_vertical, 
  *         bank-replicated slice-by-1 with 4 / 8 chains per lane (the fused kernels
  *         take 2 for the 4-chain form); 9 = memory side only (WRONG sums)
  * key 12: CRC register prefetch depth in 8-KiB tasks: 0 = default (2), 1 or 2
+ * key 13: store cache policy of the double-buffered kernel at RS(6,3) / RS(10,4):
+ *         0 = nt (default), 1 = sc1, 2 = sc0 sc1, 3 = nt sc1, 4 = plain
  * Process-wide; affects launches made after the call. */
 int hec_tune_set(int key, int value);
 

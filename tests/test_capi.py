@@ -109,3 +109,24 @@ def test_codec_names_validated():
     assert H.lib.hec_coder_create_codec(b"rs-legacy", 6, 3, 0, ctypes.byref(h)) == H.HEC_ERR_UNSUPPORTED_CODEC
     assert H.lib.hec_coder_create_codec(b"xor", 2, 2, 0, ctypes.byref(h)) == H.HEC_ERR_INVALID_ARG
     assert not h.value
+
+
+def test_group_argument_checks_need_no_device():
+    # hec_group_* (SURVEY §8e): bad arguments are statuses, never a crash
+    out = ctypes.c_void_p()
+    devs = (ctypes.c_int * 2)(0, 0)
+    assert H.lib.hec_group_create(b"rs", 6, 3, devs, 0, ctypes.byref(out)) == H.HEC_ERR_INVALID_ARG
+    assert H.lib.hec_group_create(b"rs", 6, 3, None, 2, ctypes.byref(out)) == H.HEC_ERR_INVALID_ARG
+    assert H.lib.hec_group_create(b"rs", 6, 3, devs, 65, ctypes.byref(out)) == H.HEC_ERR_INVALID_ARG
+    assert H.lib.hec_group_create(b"rs", 6, 3, devs, 2, None) == H.HEC_ERR_INVALID_ARG
+    assert H.lib.hec_group_size(None) == 0
+    assert not H.lib.hec_group_coder(None, 0)
+    first, count = ctypes.c_size_t(), ctypes.c_size_t()
+    assert H.lib.hec_group_range(None, 10, 0, ctypes.byref(first), ctypes.byref(count)) == H.HEC_ERR_INVALID_ARG
+    assert H.lib.hec_group_encode_host_batch(None, None, None, 16, 1, 1) == H.HEC_ERR_INVALID_ARG
+    assert H.lib.hec_group_decode_host_batch(None, None, 16, 1, None, 1) == H.HEC_ERR_INVALID_ARG
+    H.lib.hec_group_destroy(None)
+    if not gpu_available():
+        assert H.lib.hec_group_create(b"rs", 6, 3, devs, 2, ctypes.byref(out)) == H.HEC_ERR_DEVICE
+        assert not out.value
+

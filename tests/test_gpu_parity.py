@@ -839,3 +839,131 @@ def test_decode_verify_full_size_properties(dev):
     assert torch.equal(out[:, :2], d[:, :2])
     assert torch.equal(out[5, 3], d[5, 3])
     assert not out[:5, 2:].any() and not out[6:, 2:].any()
+
+
+def test_concurrent_threads_shared_and_private_coders(dev, c_oracle):
+    # The reference Coder is Send + Sync and is called from many tokio workers
+    # at once.  Eight threads (ctypes drops the GIL around every
+    # call): half share one coder's host-buffer API (internal lock, shared
+    # plan cache), half own a coder; every thread also runs the device API on
+    # its own stream.  All results bit-exact against the oracle.
+    import threading
+
+    import ec_oracle as EO
+    k, m = 6, 3
+    shared = H.Coder(k, m, 0)
+    errors = []
+
+    def worker(t):
+        try:
+            rng = np.random.default_rng(0x7EAD + t)
+            c = shared if t % 2 == 0 else H.Coder(k, m, 0)
+            stream = torch.cuda.Stream(device=dev)
+            for it in range(5):
+                n = int(rng.integers(1, 70000))
+                data = [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(k)]
+                par = [np.frombuffer(p, dtype=np.uint8) for p in c.encode(data)]
+                want = EO.c_encode(c_oracle, k, m, data)
+                assert all(np.array_equal(par[j], want[j]) for j in range(m)), f"t{t} encode"
+                lost = rng.choice(k + m, size=int(rng.integers(1, m + 1)), replace=False)
+                shards = [None if i in lost else (data[i] if i < k else par[i - k]).tobytes()
+                          for i in range(k + m)]
+                c.decode(shards)
+                for i in range(k):
+                    assert np.array_equal(np.frombuffer(shards[i], dtype=np.uint8), data[i]), f"t{t} decode"
+                # device API on this thread's stream (allocation, copies and
+                # kernels all ordered on it)
+                S, cell = 3, 4096 * int(rng.integers(1, 9)) + 16 * int(rng.integers(0, 4))
+                miss = sorted(int(i) for i in rng.choice(k, size=m, replace=False))
+                with torch.cuda.stream(stream):
+                    d = torch.from_numpy(batch_data(S, k, cell, first=1000 * t + it)).to(dev)
+                    p = torch.zeros((S, m, cell), dtype=torch.uint8, device=dev)
+                    out = torch.zeros_like(d)
+                    H.encode_batch(c, d, p)
+                    H.decode_batch(c, d, p, miss, out)
+                stream.synchronize()
+                wantb = oracle_batch_encode(c_oracle, k, m, d.cpu().numpy())
+                assert np.array_equal(p.cpu().numpy(), wantb), f"t{t} encode_device"
+                for i in miss:
+                    assert torch.equal(out[:, i], d[:, i]), f"t{t} decode_device"
+            if c is not shared:
+                c.close()
+        except Exception as e:  # surfaced below
+            errors.append(repr(e))
+
+    threads = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join(timeout=100)
+    assert not any(th.is_alive() for th in threads), "a worker hung"
+    assert not errors, errors
+    shared.close()
+
+
+# ---- multi-GPU coder group (hec_group_*) ----------------------
+# The box has one GPU: a group that lists device 0 several times runs several
+# coders (own streams, own host threads) on it -- the same partitioning and
+# threading as one slot per GPU.
+
+@pytest.mark.parametrize("slots,S,chunk,cell", [(1, 5, 2, 65536), (3, 10, 2, 65536), (4, 3, 1, 4096 + 16),
+                                                (8, 13, 3, 1000)])
+def test_group_encode_host_batch(c_oracle, slots, S, chunk, cell):
+    k, m = 6, 3
+    g = H.CoderGroup(k, m, [0] * slots)
+    data = batch_data(S, k, cell, first=70 + slots)
+    want = oracle_batch_encode(c_oracle, k, m, data)
+    h_in = torch.from_numpy(data).pin_memory()
+    h_out = torch.zeros((S, m, cell), dtype=torch.uint8).pin_memory()
+    g.encode_host_batch(h_in.data_ptr(), h_out.data_ptr(), cell, S, chunk)
+    assert np.array_equal(h_out.numpy(), want)
+    g.close()
+
+
+@pytest.mark.parametrize("k,m,lost", [(6, 3, (0, 1, 2)), (10, 4, (1, 5, 9, 12)), (3, 2, ())])
+@pytest.mark.parametrize("slots,rows", [(2, 7), (3, 2), (5, 9)])
+def test_group_decode_host_batch_file_order(c_oracle, k, m, lost, slots, rows):
+    cell = 4096 + 16
+    file = splitmix64_bytes(rows * 77 + k + slots, rows * k * cell)
+    data = file.reshape(rows, k, cell)
+    par = oracle_batch_encode(c_oracle, k, m, data)
+    vertical = [np.ascontiguousarray(data[:, i, :]).ravel() for i in range(k)] + \
+               [np.ascontiguousarray(par[:, j, :]).ravel() for j in range(m)]
+    hv = [None if i in lost else torch.from_numpy(vertical[i]).pin_memory() for i in range(k + m)]
+    out = torch.zeros(rows * k * cell, dtype=torch.uint8).pin_memory()
+    g = H.CoderGroup(k, m, [0] * slots)
+    g.decode_host_batch([None if t is None else t.data_ptr() for t in hv], cell, rows, out.data_ptr(), 2)
+    assert np.array_equal(out.numpy(), file)
+    g.close()
+
+
+def test_group_errors_and_slot_coders(dev, c_oracle):
+    with pytest.raises(H.DeviceError):
+        H.CoderGroup(6, 3, [0, 4096])  # no such device: the slots created so far are released
+    with pytest.raises(H.UnsupportedErasureCodingPolicy):
+        H.CoderGroup(6, 3, [0], codec="rs-legacy")
+    g = H.CoderGroup(6, 3, [0, 0, 0])
+    assert len(g) == 3
+    from hdfs_native_ec.dist import shard_range
+    for total in (0, 1, 2, 10, 2048, 65537):
+        assert [g.range(total, i) for i in range(3)] == [shard_range(total, 3, i) for i in range(3)]
+    # every slot's coder serves the device-resident API on its GPU
+    S, cell = 9, 8192
+    data = batch_data(S, 6, cell, first=5)
+    want = oracle_batch_encode(c_oracle, 6, 3, data)
+    d = torch.from_numpy(data).to(dev)
+    p = torch.zeros((S, 3, cell), dtype=torch.uint8, device=dev)
+    for slot in range(3):
+        first, count = g.range(S, slot)
+        H.encode_batch(g.coder(slot), d[first:first + count], p[first:first + count])
+    torch.cuda.synchronize()
+    assert np.array_equal(p.cpu().numpy(), want)
+    # too many losses: every slot reports it, the call returns the status
+    cell, rows = 4096, 4
+    hv = [torch.zeros(rows * cell, dtype=torch.uint8).pin_memory() for _ in range(9)]
+    ptrs = [t.data_ptr() for t in hv]
+    ptrs[0] = ptrs[1] = ptrs[2] = ptrs[3] = None
+    out = torch.zeros(rows * 6 * cell, dtype=torch.uint8).pin_memory()
+    with pytest.raises(H.ErasureCodingError):
+        g.decode_host_batch(ptrs, cell, rows, out.data_ptr(), 1)
+    g.close()
