@@ -11,6 +11,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
+#include <vector>
 
 #include "../../hdfs-native_amd/csrc/hdfs_ec.hpp"
 
@@ -139,6 +141,37 @@ static int gpu_mode() {
             }
         }
         std::printf("rs(%zu,%zu) striped write/read round trips done\n", k, m);
+    }
+    // Concurrent callers (the reference's Coder is Send + Sync, called from
+    // many tokio workers at once): 8 native threads share one Coder through
+    // striped writes and faulty reads of different files.
+    {
+        const size_t k = 6, m = 3;
+        EcSchema s{"rs", k, m, cell};
+        Coder shared(k, m);
+        std::vector<int> bad(8, 0);
+        std::vector<std::thread> th;
+        for (int t = 0; t < 8; t++)
+            th.emplace_back([&, t] {
+                try {
+                    for (int it = 0; it < 3; it++) {
+                        const size_t size = cell * k * size_t(1 + (t + it) % 3) + size_t(4 * t);
+                        const Bytes file = counter_file(size);
+                        const std::vector<Bytes> shards = write_block_group(s, file);
+                        const Bytes back = read_block_group(s, shards, size, size_t((t + it) % m + 1), shared);
+                        if (back != file) bad[t]++;
+                    }
+                } catch (...) {
+                    bad[t]++;
+                }
+            });
+        for (auto& x : th) x.join();
+        for (int t = 0; t < 8; t++)
+            if (bad[t]) {
+                std::printf("FAIL concurrent thread %d\n", t);
+                failures++;
+            }
+        std::printf("8 threads on one shared coder done\n");
     }
     // unsupported codec on the read path (mod.rs:74-78)
     try {
