@@ -103,7 +103,7 @@ __device__ __forceinline__ void load_task(const CrcArgs& a, uint64_t groups, uin
 
 template <int SCHEME>
 struct CrcShape : crcdev::TableLayout<SCHEME> {
-    static constexpr int kBlock = SCHEME <= 1 ? 256 : 512;
+    static constexpr int kBlock = SCHEME == 16 ? 1024 : (SCHEME <= 1 || SCHEME == 11) ? 256 : 512;
     static constexpr int kWaves = kBlock / 64;
 };
 
@@ -116,7 +116,6 @@ __global__ __launch_bounds__(CrcShape<SCHEME>::kBlock) void checksum_chunks512(C
     __shared__ uint32_t s_tables[Sh::kWords];
     __shared__ __attribute__((aligned(16))) uint8_t s_stage[Sh::kWaves * STAGE];
     uint32_t* s_main = s_tables;
-    const uint32_t(*s_shift)[4][256] = reinterpret_cast<const uint32_t(*)[4][256]>(s_tables + Sh::kShiftOff);
     crcdev::stage_tables<SCHEME, BS>(s_tables, tables<KIND>());
     __syncthreads();
     const uint32_t kfinal = tables<KIND>().final512;
@@ -153,14 +152,15 @@ __global__ __launch_bounds__(CrcShape<SCHEME>::kBlock) void checksum_chunks512(C
             val = *reinterpret_cast<const uint32_t*>(stage + lane * PITCH);
         } else if (full) {
             uint32_t r = crcdev::quarter<SCHEME, REFL>(s_main, stage + lane * PITCH, lane);
-            if (qi < 3) r = crcdev::apply_shift(s_shift[qi], r);
+            if (qi < 3) r = crcdev::shift_quarter<SCHEME>(s_tables, qi, r);
             val = r;
         } else if (live && qi == 0) {
             // short last chunk of the cell: this lane walks it whole, bytewise
             const uint32_t len = uint32_t(a.cell_len - cstart);
             uint32_t r = Spec::kInit;
             for (uint32_t p = 0; p < len; p++)
-                r = crcdev::byte_step<REFL, (SCHEME <= 1 ? 1 : 32)>(s_main, r, stage[(4 * c + p / Q) * PITCH + (p % Q)]);
+                r = crcdev::byte_step<REFL, crcdev::ByteTable<SCHEME>::stride>(s_main + crcdev::ByteTable<SCHEME>::off, r,
+                                                                              stage[(4 * c + p / Q) * PITCH + (p % Q)]);
             val = r ^ Spec::kXorout;
         }
         val ^= __shfl_xor(val, 1);
@@ -225,8 +225,10 @@ const void* crc_fn(int pf) {
 
 template <int KIND>
 const void* crc_pick(int scheme, int pf) {
-    return scheme == 1   ? crc_fn<KIND, 1>(pf)
-           : scheme == 4 ? crc_fn<KIND, 4>(pf)
+    return scheme == 1    ? crc_fn<KIND, 1>(pf)
+           : scheme == 16 ? reinterpret_cast<const void*>(&checksum_chunks512<KIND, 16, 1>)
+           : scheme == 11 ? crc_fn<KIND, 11>(pf)
+           : scheme == 4  ? crc_fn<KIND, 4>(pf)
            : scheme == 8 ? crc_fn<KIND, 8>(pf)
                          : crc_fn<KIND, 0>(pf);
 }
@@ -255,13 +257,21 @@ int launch_checksum(const CrcArgs& in, int device, hipStream_t stream) {
     if (aligned && a.bytes_per_checksum == 512) {
         a.groups_per_cell = (a.chunks_per_cell + 15) / 16;
         const uint64_t tasks = a.groups_per_cell * a.n_shards * a.stripes;
-        // default: slicing-by-8, 2 tasks of prefetch.  Interleaved A/B
-        // (profiles/r01_probe_crc.log): 4.91 TB/s vs 4.80 (replicated, 4
-        // chains) and 4.64 (8 chains); the memory side alone reaches 6.4.
-        const int scheme = g_tune_crc_variant == 2 ? 4 : g_tune_crc_variant == 3 ? 8 : g_tune_crc_variant == 9 ? 0 : 1;
-        const int pf = g_tune_crc_prefetch == 1 ? 1 : 2;
-        const int waves = scheme <= 1 ? CrcShape<1>::kWaves : CrcShape<4>::kWaves;
-        const int per_cu = scheme <= 1 ? 2 : 1;  // LDS: 56 KiB / ~144 KiB per block
+        // default: 11-bit slicing (6 LDS lookups per 8 bytes), 2 tasks of
+        // prefetch.  Interleaved A/B (profiles/r01d_probe_crc_w11.log): 5.32
+        // TB/s vs 4.84-4.89 for slicing-by-8 (profiles/r01_probe_crc.log: 4.91
+        // vs 4.80 replicated, 4 chains, and 4.64, 8 chains; 4.64 for
+        // slicing-by-8 at 4 waves per SIMD, r01d_probe_crc_1024.log); the
+        // memory side alone reaches 6.4.
+        const int scheme = g_tune_crc_variant == 1   ? 1
+                           : g_tune_crc_variant == 2 ? 4
+                           : g_tune_crc_variant == 3 ? 8
+                           : g_tune_crc_variant == 4 ? 16
+                           : g_tune_crc_variant == 9 ? 0
+                                                     : 11;
+        const int pf = g_tune_crc_prefetch == 1 ? 1 : 2;  // scheme 16: always 1 (128 VGPRs at 4 waves/SIMD)
+        const int waves = scheme == 16 ? CrcShape<16>::kWaves : crcdev::sliced(scheme) ? CrcShape<1>::kWaves : CrcShape<4>::kWaves;
+        const int per_cu = (crcdev::sliced(scheme) && scheme != 16) ? 2 : 1;  // LDS: 56 / 77.5 KiB; ~144 / ~154 KiB
         uint64_t grid = (tasks + waves - 1) / waves;
         if (grid > uint64_t(cus) * per_cu) grid = uint64_t(cus) * per_cu;
         const void* fn = a.kind == crc::kCrc32c ? crc_pick<crc::kCrc32c>(scheme, pf) : crc_pick<crc::kCksum>(scheme, pf);

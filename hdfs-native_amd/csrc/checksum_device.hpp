@@ -38,6 +38,27 @@ __device__ __forceinline__ uint32_t apply_shift(const uint32_t (*t)[256], uint32
     return t[0][r & 0xFF] ^ t[1][(r >> 8) & 0xFF] ^ t[2][(r >> 16) & 0xFF] ^ t[3][r >> 24];
 }
 
+// 8 message bytes through the 11-bit field tables (checksum_tables.hpp w11),
+// packed in LDS at word offsets 0, 2048, 4096, 5120, 7168, 9216.
+template <bool REFL>
+__device__ __forceinline__ uint32_t step8_w11(const uint32_t* t, uint32_t crc, uint32_t lo, uint32_t hi) {
+    lo ^= REFL ? crc : __builtin_bswap32(crc);
+    return t[lo & 0x7FF] ^ t[2048 + ((lo >> 11) & 0x7FF)] ^ t[4096 + (lo >> 22)] ^ t[5120 + (hi & 0x7FF)] ^
+           t[7168 + ((hi >> 11) & 0x7FF)] ^ t[9216 + (hi >> 22)];
+}
+
+template <bool REFL>
+__device__ __forceinline__ uint32_t quarter_w11(const uint32_t* t, const uint8_t* row) {
+    uint32_t r = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const v4u w = *reinterpret_cast<const v4u*>(row + i * 16);
+        r = step8_w11<REFL>(t, r, w.x, w.y);
+        r = step8_w11<REFL>(t, r, w.z, w.w);
+    }
+    return r;
+}
+
 template <bool REFL>
 __device__ __forceinline__ uint32_t quarter_s8(const uint32_t (*tab)[256], const uint8_t* row) {
     uint32_t r = 0;
@@ -89,33 +110,80 @@ __device__ __forceinline__ uint32_t byte_step(const uint32_t* t0, uint32_t r, ui
     return REFL ? t0[((r ^ b) & 0xFF) * STRIDE] ^ (r >> 8) : t0[(((r >> 24) ^ b) & 0xFF) * STRIDE] ^ (r << 8);
 }
 
-// slice[8][256] (scheme 1) | rep[256][32] (schemes 4, 8) ; shift[3][4][256] ;
-// seg[7][4][256] (schemes 4, 8)
+// r -> shifted state from nibble tables t[8][16] (8 lookups instead of 4)
+__device__ __forceinline__ uint32_t apply_shift_nib(const uint32_t (*t)[16], uint32_t r) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int q = 0; q < 8; q++) v ^= t[q][(r >> (4 * q)) & 15];
+    return v;
+}
+
+// Schemes: 1 = slicing-by-8 (256-thread blocks); 11 = 11-bit slicing (6
+// lookups per 8 bytes from 40 KiB of tables, nibble shift tables; 256-thread
+// blocks, 2 per CU); 16 = slicing-by-8 in
+// 1024-thread blocks (4 waves per SIMD) with nibble shift tables so the
+// tables (9.5 KiB) and 16 wave images (144 KiB) fit one CU's LDS; 4 / 8 =
+// bank-replicated slicing-by-1; 0 = memory side only.
+constexpr bool sliced(int scheme) { return scheme <= 1 || scheme == 16 || scheme == 11; }
+constexpr bool nib_shift(int scheme) { return scheme == 16 || scheme == 11; }
+
+// slice[8][256] (schemes 1, 16) | rep[256][32] (schemes 4, 8) ; shift[3][4][256]
+// (shift_nib[3][8][16] for scheme 16) ; seg[7][4][256] (schemes 4, 8)
 template <int SCHEME>
 struct TableLayout {
-    static constexpr int kMainWords = SCHEME <= 1 ? 8 * 256 : 256 * 32;
+    static constexpr int kMainWords = SCHEME == 11 ? 4 * 2048 + 2 * 1024 : sliced(SCHEME) ? 8 * 256 : 256 * 32;
     static constexpr int kShiftOff = kMainWords;
-    static constexpr int kSegOff = kShiftOff + 3 * 4 * 256;
-    static constexpr int kWords = kSegOff + (SCHEME <= 1 ? 0 : 7 * 4 * 256);
+    static constexpr int kShiftWords = nib_shift(SCHEME) ? 3 * 8 * 16 : 3 * 4 * 256;
+    static constexpr int kSegOff = kShiftOff + kShiftWords;
+    static constexpr int kWords = kSegOff + (sliced(SCHEME) ? 0 : 7 * 4 * 256);
 };
+
+// Where the classic byte table (slice[0]) sits in a scheme's LDS image, for
+// byte-serial tails: slice[0][x] = t[off + x * stride].  Scheme 11 has no
+// byte table, but its field 5 (hi bits 22..31) holds it: byte 7 of the
+// step is field bits 2..9, so slice[0][x] = w11[5][x << 2].
+template <int SCHEME>
+struct ByteTable {
+    static constexpr int off = SCHEME == 11 ? 9216 : 0;
+    static constexpr int stride = SCHEME == 11 ? 4 : sliced(SCHEME) ? 1 : 32;
+};
+
+// Moves quarter qi's linear CRC (qi < 3) to its place in the 512-B chunk.
+template <int SCHEME>
+__device__ __forceinline__ uint32_t shift_quarter(const uint32_t* s, int qi, uint32_t r) {
+    if constexpr (nib_shift(SCHEME))
+        return apply_shift_nib(reinterpret_cast<const uint32_t(*)[8][16]>(s + TableLayout<SCHEME>::kShiftOff)[qi], r);
+    else
+        return apply_shift(reinterpret_cast<const uint32_t(*)[4][256]>(s + TableLayout<SCHEME>::kShiftOff)[qi], r);
+}
 
 // Fills a block's LDS table image (TableLayout<SCHEME>) from the constant
 // tables; caller synchronises.
 template <int SCHEME, int BS, typename T>
 __device__ __forceinline__ void stage_tables(uint32_t* s, const T& tab) {
-    if constexpr (SCHEME <= 1) {
+    if constexpr (SCHEME == 11) {
+        constexpr int off[6] = {0, 2048, 4096, 5120, 7168, 9216}, len[6] = {2048, 2048, 1024, 2048, 2048, 1024};
+#pragma unroll
+        for (int f = 0; f < 6; f++)
+            for (int t = threadIdx.x; t < len[f]; t += BS) s[off[f] + t] = tab.w11[f][t];
+    } else if constexpr (sliced(SCHEME)) {
         for (int t = threadIdx.x; t < 8 * 256; t += BS) s[t] = (&tab.slice[0][0])[t];
     } else {
         for (int t = threadIdx.x; t < 256 * 32; t += BS) s[t] = tab.slice[0][t / 32];
         for (int t = threadIdx.x; t < 7 * 4 * 256; t += BS) s[TableLayout<SCHEME>::kSegOff + t] = (&tab.seg[0][0][0])[t];
     }
-    for (int t = threadIdx.x; t < 3 * 4 * 256; t += BS) s[TableLayout<SCHEME>::kShiftOff + t] = (&tab.shift[0][0][0])[t];
+    if constexpr (nib_shift(SCHEME))
+        for (int t = threadIdx.x; t < 3 * 8 * 16; t += BS) s[TableLayout<SCHEME>::kShiftOff + t] = (&tab.shift_nib[0][0][0])[t];
+    else
+        for (int t = threadIdx.x; t < 3 * 4 * 256; t += BS) s[TableLayout<SCHEME>::kShiftOff + t] = (&tab.shift[0][0][0])[t];
 }
 
 // Linear part of the quarter at `row` under the block's LDS tables.
 template <int SCHEME, bool REFL>
 __device__ __forceinline__ uint32_t quarter(const uint32_t* s, const uint8_t* row, int lane) {
-    if constexpr (SCHEME <= 1)
+    if constexpr (SCHEME == 11)
+        return quarter_w11<REFL>(s, row);
+    else if constexpr (sliced(SCHEME))
         return quarter_s8<REFL>(reinterpret_cast<const uint32_t(*)[256]>(s), row);
     else
         return quarter_rep<SCHEME, REFL>(reinterpret_cast<const uint32_t(*)[32]>(s),

@@ -56,6 +56,13 @@ struct Tables {
     uint32_t slice[8][256]{};
     uint32_t shift[3][4][256]{};  // [0] = 384 B, [1] = 256 B, [2] = 128 B
     uint32_t seg[7][4][256]{};    // [i] = 16*(7-i) B: 112, 96, ..., 16
+    uint32_t shift_nib[3][8][16]{};  // shift[] as nibble tables (1.5 KiB: the 1024-thread CRC kernel)
+    // 11-bit slicing: the 8-byte step's 64 message bits (lo = bytes 0-3, hi =
+    // 4-7, little-endian) in six fields lo[0:11] lo[11:22] lo[22:32] hi[0:11]
+    // hi[11:22] hi[22:32]; w11[f][x] = XOR of the single-bit columns of the
+    // byte tables, slice[7 - j/8][1 << j%8] for message bit j.  6 lookups per
+    // 8 bytes instead of 8 (fields 2 and 5 use 1024 entries).
+    uint32_t w11[6][2048]{};
     uint32_t final512 = 0;
 
     // one byte through the register
@@ -95,7 +102,24 @@ struct Tables {
         for (int s = 1; s < 8; s++)
             for (int i = 0; i < 256; i++) slice[s][i] = zero_bytes(slice[0], slice[s - 1][i], 1);
         for (int k = 0; k < 3; k++) zero_shift_table(slice[0], 128 * (3 - k), shift[k]);
+        for (int k = 0; k < 3; k++)  // nibble q of r: XOR of the byte table's single-bit columns
+            for (int q = 0; q < 8; q++)
+                for (int x = 0; x < 16; x++) {
+                    uint32_t v = 0;
+                    for (int b = 0; b < 4; b++)
+                        if (x & (1 << b)) v ^= shift[k][q / 2][1 << (4 * (q % 2) + b)];
+                    shift_nib[k][q][x] = v;
+                }
         for (int i = 0; i < 7; i++) zero_shift_table(slice[0], 16 * (7 - i), seg[i]);
+        for (int f = 0; f < 6; f++) {
+            const int j0 = (f / 3) * 32 + (f % 3) * 11, bits = (f % 3) == 2 ? 10 : 11;
+            for (int x = 0; x < (1 << bits); x++) {
+                uint32_t v = 0;
+                for (int b = 0; b < bits; b++)
+                    if (x & (1 << b)) v ^= slice[7 - (j0 + b) / 8][1 << ((j0 + b) % 8)];
+                w11[f][x] = v;
+            }
+        }
         final512 = zero_bytes(slice[0], S::kInit, 512) ^ S::kXorout;
     }
 };

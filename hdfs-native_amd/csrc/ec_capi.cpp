@@ -1066,8 +1066,11 @@ int hec_decode_verify_device(hec_coder_t* c, int checksum_type, const uint8_t* c
 // 8 = tile-order group (stripes interleaved column-major; 1 = stripe-major),
 // 9 = 1: hec_encode_crc_device as two passes (encode, then CRC) instead of fused,
 // 10 = slabs per wave of the fused encode+CRC kernel (0 default, 4 or 8),
-// 11 = CRC lookup scheme (0 default, 1 slice-by-8 tables, 2 / 3 bank-replicated
-//      slice-by-1 with 4 / 8 chains per lane; 9 = loads + staging only, WRONG
+// 11 = CRC lookup scheme (0 default: 11-bit slicing in the CRC kernels,
+//      slice-by-8 in the fused ones; 1 slice-by-8 tables, 2 / 3 bank-replicated
+//      slice-by-1 with 4 / 8 chains per lane, 4 = slice-by-8 in 1024-thread
+//      blocks (4 waves per SIMD, CRC kernel only), 5 = 11-bit slicing (6 lookups
+//      per 8 bytes; CRC kernel only); 9 = loads + staging only, WRONG
 //      sums: measures the kernel's memory side),
 // 12 = CRC kernel register prefetch depth in tasks (0 default = 2, 1 or 2),
 // 13 = store cache policy of the register double-buffered kernel (key 5 = 3)
@@ -1229,7 +1232,7 @@ int hec_tune_set(int key, int value) {
             hec::g_tune_fused_slabs = value;
             return HEC_OK;
         case 11:
-            if ((value < 0 || value > 3) && value != 9) return HEC_ERR_INVALID_ARG;
+            if ((value < 0 || value > 5) && value != 9) return HEC_ERR_INVALID_ARG;
             hec::g_tune_crc_variant = value;
             return HEC_OK;
         case 12:

@@ -56,27 +56,26 @@ __device__ __forceinline__ const crc::Tables<KIND>& fused_tables() {
 //     sit at the same index (shard_id = survivor shard numbers), a mismatch
 //     sets bad[stripe * n_total + shard_id[s]].
 template <int K, int R, int SLABS, int SCHEME, int KIND, bool VERIFY>
-__global__ __launch_bounds__(SCHEME == 1 ? 256 : 512) __attribute__((amdgpu_waves_per_eu(2, 2))) void gf_fused_crc(
+__global__ __launch_bounds__(crcdev::sliced(SCHEME) ? 256 : 512) __attribute__((amdgpu_waves_per_eu(2, 2))) void gf_fused_crc(
     MatmulArgs a, FusedCrcArgs cs) {
     using TL = crcdev::TableLayout<SCHEME>;
     using Spec = crc::Spec<KIND>;
     constexpr bool REFL = Spec::kReflected;
-    constexpr int BS = SCHEME == 1 ? 256 : 512, WAVES = BS / 64;
+    constexpr int BS = crcdev::sliced(SCHEME) ? 256 : 512, WAVES = BS / 64;
     constexpr int PITCH = 144, STAGE = 64 * PITCH, SPR = 8 / SLABS;
     constexpr int NSUM = VERIFY ? K : K + R;  // checksummed shards
     constexpr uint32_t WAVE_BYTES = SLABS * 1024u, TILE_BYTES = WAVES * WAVE_BYTES;
     constexpr bool PF = R * SLABS <= 24;  // register prefetch of the next shard
-    __shared__ PermTable s_tab[R][kMaxK];
+    __shared__ PermTable s_tab[R][K];  // K columns: scheme 11 needs 2 x 79 KiB per CU
     __shared__ uint8_t s_exp[512];
     __shared__ uint8_t s_log[256];
     __shared__ uint8_t s_coef[R * kMaxK];
     __shared__ uint32_t s_ctabs[TL::kWords];
     __shared__ __attribute__((aligned(16))) uint8_t s_stage[WAVES * STAGE];
-    prologue<R, BS>(a, K, s_tab, s_exp, s_log, s_coef);
+    prologue<R, BS, K>(a, K, s_tab, s_exp, s_log, s_coef);
     crcdev::stage_tables<SCHEME, BS>(s_ctabs, fused_tables<KIND>());
     __syncthreads();
     const uint32_t kfinal = fused_tables<KIND>().final512;
-    const uint32_t(*s_shift)[4][256] = reinterpret_cast<const uint32_t(*)[4][256]>(s_ctabs + TL::kShiftOff);
 
     const uint64_t cell_len = a.cell_len;
     const uint64_t nck = (cell_len + 511) / 512;  // checksum chunks per cell
@@ -125,15 +124,15 @@ __global__ __launch_bounds__(SCHEME == 1 ? 256 : 512) __attribute__((amdgpu_wave
             uint32_t val = 0;
             if (full && sir < count) {
                 uint32_t r = crcdev::quarter<SCHEME, REFL>(s_ctabs, stage + lane * PITCH, lane);
-                if (qi < 3) r = crcdev::apply_shift(s_shift[qi], r);
+                if (qi < 3) r = crcdev::shift_quarter<SCHEME>(s_ctabs, qi, r);
                 val = r;
             } else if (live_c && qi == 0) {
                 // short last chunk of the cell: this lane walks it whole, bytewise
                 const uint32_t len = uint32_t(cell_len - cbyte);
                 uint32_t r = Spec::kInit;
                 for (uint32_t b = 0; b < len; b++)
-                    r = crcdev::byte_step<REFL, (SCHEME == 1 ? 1 : 32)>(s_ctabs, r,
-                                                                       stage[(lane + b / 128) * PITCH + (b % 128)]);
+                    r = crcdev::byte_step<REFL, crcdev::ByteTable<SCHEME>::stride>(
+                        s_ctabs + crcdev::ByteTable<SCHEME>::off, r, stage[(lane + b / 128) * PITCH + (b % 128)]);
                 val = r ^ Spec::kXorout;
             }
             val ^= __shfl_xor(val, 1);
@@ -256,8 +255,10 @@ const void* encode_fn(int slabs, int scheme) {
 }
 
 // verify: default slabs and lookup scheme only, both checksum kinds
+// (the 11-bit slicing of the CRC kernel, scheme 11, was measured here too and
+// lost: profiles/r01d_probe_fused_w11_*.log)
 template <int K, int R>
-const void* verify_fn(int kind) {
+const void* verify_fn(int kind, int) {
     constexpr int SL = fused_slabs(K, R);
     return kind == crc::kCrc32c ? reinterpret_cast<const void*>(&gf_fused_crc<K, R, SL, 1, crc::kCrc32c, true>)
                                 : reinterpret_cast<const void*>(&gf_fused_crc<K, R, SL, 1, crc::kCksum, true>);
@@ -266,10 +267,10 @@ const void* verify_fn(int kind) {
 template <int K>
 const void* pick_r(bool verify, int r, int slabs, int scheme, int kind) {
     switch (r) {
-        case 1: return verify ? verify_fn<K, 1>(kind) : encode_fn<K, 1>(slabs, scheme);
-        case 2: return verify ? verify_fn<K, 2>(kind) : encode_fn<K, 2>(slabs, scheme);
-        case 3: return verify ? verify_fn<K, 3>(kind) : encode_fn<K, 3>(slabs, scheme);
-        default: return verify ? verify_fn<K, 4>(kind) : encode_fn<K, 4>(slabs, scheme);
+        case 1: return verify ? verify_fn<K, 1>(kind, scheme) : encode_fn<K, 1>(slabs, scheme);
+        case 2: return verify ? verify_fn<K, 2>(kind, scheme) : encode_fn<K, 2>(slabs, scheme);
+        case 3: return verify ? verify_fn<K, 3>(kind, scheme) : encode_fn<K, 3>(slabs, scheme);
+        default: return verify ? verify_fn<K, 4>(kind, scheme) : encode_fn<K, 4>(slabs, scheme);
     }
 }
 
@@ -291,7 +292,7 @@ int launch_fused(const MatmulArgs& in, const FusedCrcArgs& cs, bool verify, int 
     // by 7-10 % here (profiles/r01_probe_fused_scheme.log); tune key 11 = 2
     // selects the latter for encode
     const int scheme = (!verify && g_tune_crc_variant == 2) ? 4 : 1;
-    const int waves = scheme == 1 ? 4 : 8;
+    const int waves = crcdev::sliced(scheme) ? 4 : 8;
     const void* fn = nullptr;
     switch (a.k) {
         case 2: fn = pick_r<2>(verify, a.r, slabs, scheme, cs.kind); break;
@@ -312,7 +313,7 @@ int launch_fused(const MatmulArgs& in, const FusedCrcArgs& cs, bool verify, int 
     a.total_tiles = uint32_t(total);
     a.group = g_tune_group > 0 ? uint32_t(g_tune_group) : 4u;
     // LDS: ~61 KiB per 256-thread block (two per CU) / ~131 KiB per 512-thread block (one)
-    uint64_t grid = uint64_t(cus_of(device)) * (scheme == 1 ? 2 : 1);
+    uint64_t grid = uint64_t(cus_of(device)) * (crcdev::sliced(scheme) ? 2 : 1);
     if (grid > total) grid = total;
     FusedCrcArgs c = cs;
     void* args[] = {&a, &c};

@@ -132,8 +132,9 @@ __device__ __forceinline__ void store16p(uint8_t* p, u32x4 v) {
 }
 
 // Stage log/antilog + coefficient rows in LDS, build the perm tables.
-template <int R, int BS>
-__device__ __forceinline__ void prologue(const MatmulArgs& a, int k, PermTable (*s_tab)[kMaxK], uint8_t* s_exp,
+// KC = columns of the caller's s_tab (kMaxK, or K where LDS is tight).
+template <int R, int BS, int KC = kMaxK>
+__device__ __forceinline__ void prologue(const MatmulArgs& a, int k, PermTable (*s_tab)[KC], uint8_t* s_exp,
                                          uint8_t* s_log, uint8_t* s_coef) {
     static_assert(BS >= 256 && BS % 256 == 0, "prologue assumes >= 256 threads");
     const int tid = threadIdx.x;

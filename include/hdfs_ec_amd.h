@@ -302,9 +302,11 @@ int hec_group_decode_host_batch(hec_group_t *group, const uint8_t *const *h_vert
  * key 8: tile order, stripes interleaved per group (1 = stripe-major; 0 = default)
  * key 9: 1 = hec_encode_crc_device as encode + separate CRC pass (0 = fused)
  * key 10: fused encode+CRC slabs per wave: 0 = default, 4 or 8
- * key 11: CRC lookups: 0 = default (slice-by-8), 1 = slice-by-8 tables, 2 / 3 =
+ * key 11: CRC lookups: 0 = default (11-bit slicing in the checksum kernels,
+ *         slice-by-8 in the fused ones), 1 = slice-by-8 tables, 5 = 11-bit slicing, 2 / 3 =
  *         bank-replicated slice-by-1 with 4 / 8 chains per lane (the fused kernels
- *         take 2 for the 4-chain form); 9 = memory side only (WRONG sums)
+ *         take 2 for the 4-chain form); 4 = slice-by-8 in 1024-thread blocks, 4 waves
+ *         per SIMD (checksum kernels only); 9 = memory side only (WRONG sums)
  * key 12: CRC register prefetch depth in 8-KiB tasks: 0 = default (2), 1 or 2
  * key 13: store cache policy of the double-buffered kernel at RS(6,3) / RS(10,4):
  *         0 = nt (default), 1 = sc1, 2 = sc0 sc1, 3 = nt sc1, 4 = plain

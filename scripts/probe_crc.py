@@ -1,7 +1,8 @@
 """Measurement tool (GPU box): CRC32C-per-chunk kernel variants (tune key 11
 scheme x key 12 prefetch) on 9 x 1 MiB cells x S stripes, interleaved over
 ROUNDS rounds so clock/thermal drift hits every variant alike; prints the
-median per variant.  Also the target of scripts/pmc_crc.sh."""
+median per variant (PROBE_VARIANTS="scheme:prefetch,..." to pick).  Also the
+target of scripts/pmc_crc.sh."""
 import os
 import statistics
 import sys
@@ -19,7 +20,9 @@ dev = torch.device("cuda:0")
 cells = torch.empty((S, n, cell), dtype=torch.uint8, device=dev)
 cells.random_(0, 256, generator=torch.Generator(device=dev).manual_seed(1))
 coder = H.Coder(6, 3, 0)
-variants = [(v, p) for v in (1, 2, 3, 9) for p in (1, 2)]
+# "scheme:prefetch,..." (tune keys 11:12); default: every scheme x prefetch
+variants = ([tuple(int(x) for x in v.split(":")) for v in os.environ["PROBE_VARIANTS"].split(",")]
+            if os.environ.get("PROBE_VARIANTS") else [(v, p) for v in (1, 2, 3, 4, 9) for p in (1, 2)])
 ref = H.crc32c_batch(coder, cells)
 times = {v: [] for v in variants}
 for _ in range(ROUNDS):

@@ -571,7 +571,7 @@ def _oracle_sums(cells: np.ndarray, bpc: int) -> np.ndarray:
 
 @pytest.mark.parametrize("cell,bpc,n", [(512 * 64, 512, 3), (512 * 70 + 256, 512, 2), (1 << 16, 512, 9),
                                         (4096, 4096, 2), (1000, 512, 3), (3 * 512 + 16, 512, 1), (2048, 100, 2)])
-@pytest.mark.parametrize("variant,pf", [(0, 0), (1, 1), (2, 2), (3, 1), (3, 2)])
+@pytest.mark.parametrize("variant,pf", [(0, 0), (1, 1), (2, 2), (3, 1), (3, 2), (4, 0), (5, 1), (5, 2)])
 def test_crc32c_device_vs_oracle(dev, cell, bpc, n, variant, pf):
     """All CRC lookup schemes (tune key 11) and prefetch depths (key 12)
     against the oracle."""
@@ -676,7 +676,7 @@ def _oracle_checksums(cells: np.ndarray, bpc: int, ctype: int) -> np.ndarray:
 @pytest.mark.parametrize("ctype", CKSUM_TYPES)
 @pytest.mark.parametrize("cell,bpc,n", [(512 * 64, 512, 3), (512 * 70 + 256, 512, 2), (1000, 512, 3),
                                         (4096, 4096, 2), (2048, 100, 2)])
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
 def test_checksum_device_vs_oracle(dev, ctype, cell, bpc, n, variant):
     S = 3
     cells = batch_data(S, n, cell, first=cell + bpc + ctype)
