@@ -51,7 +51,9 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0),
                     help="also time the oracle stripe-parallel on T threads (default $OMP_NUM_THREADS: the "
                          "box's CPU share; 0/1 = single-threaded only)")
-    ap.add_argument("--host-path", action="store_true", help="also measure the pinned H2D+encode+D2H pipeline")
+    ap.add_argument("--host-path", type=int, default=-1,
+                    help="also measure the PCIe-inclusive pinned-host pipelines (H2D + encode + D2H, and the "
+                         "striped-read decode into file order): 1 = yes, 0 = no, -1 = default (yes at N=1)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--tune", default="", help="key=value,... passed to hec_tune_set (measurement)")
     ap.add_argument("--encode-only", action="store_true")
@@ -423,7 +425,11 @@ def main():
                              "wall time of the synchronous call incl. the flag read-back",
             })
 
-    if args.host_path and rank == 0:
+    host_path = args.host_path if args.host_path >= 0 else int(world == 1)
+    if host_path and rank == 0 and not mixed:
+        # The path starts and ends in host memory (DataNode sockets in, write
+        # pipeline out): pinned host buffers through the coder's 3-slot
+        # H2D / kernel / D2H pipelines.  Never `value`.
         hs = min(S, 256)
         h_in = data[:hs].cpu().pin_memory()
         h_out = torch.empty((hs, m, cell), dtype=torch.uint8).pin_memory()
@@ -434,9 +440,24 @@ def main():
             coder.encode_host_batch(h_in.data_ptr(), h_out.data_ptr(), cell, hs, 16)
         th = (time.perf_counter() - th0) / reps
         assert torch.equal(h_out, parity[:hs].cpu())
+        # read side: the reader's per-shard vertical buffers (data shards
+        # 0..m-1 lost) -> file-order rows with the lost cells rebuilt
+        vert = [None if i < m else h_in[:, i].contiguous().pin_memory() for i in range(k)] + \
+               [h_out[:, j].contiguous().pin_memory() for j in range(m)]
+        h_file = torch.empty((hs, k, cell), dtype=torch.uint8).pin_memory()
+        vaddr = [None if v is None else v.data_ptr() for v in vert]
+        coder.decode_host_batch(vaddr, cell, hs, h_file.data_ptr(), 16)
+        td0 = time.perf_counter()
+        for _ in range(reps):
+            coder.decode_host_batch(vaddr, cell, hs, h_file.data_ptr(), 16)
+        td = (time.perf_counter() - td0) / reps
+        assert torch.equal(h_file, h_in)
         result["host_path"] = {"encode_GiBps_pcie_inclusive": round(k * cell * hs / th / GIB, 2),
+                               "decode_GiBps_pcie_inclusive": round(k * cell * hs / td / GIB, 2),
                                "stripes": hs, "chunk_stripes": 16,
-                               "note": "pinned host -> H2D -> encode -> D2H -> pinned host, 2-slot overlap"}
+                               "note": "pinned host -> H2D -> kernel -> D2H -> pinned host, 3-slot pipelines "
+                                       "(hec_encode_host_batch; hec_decode_host_batch with data shards "
+                                       f"0..{m - 1} lost, file-order rows out); data GiB/s, never `value`"}
 
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         result["cpu_baseline"] = cpu_baseline(k, m, cell, args.cpu_seconds, 1)

@@ -7,7 +7,7 @@ tag=${1:-r01}
 out=gpurun_out/prof_$tag
 mkdir -p $out
 export TMPDIR=/tmp
-B="python3 bench.py --steps 10 --warmup 3 --cpu-seconds 0 --spinup 0.3"
+B="python3 bench.py --steps 10 --warmup 3 --cpu-seconds 0 --spinup 0.3 --host-path 0"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/trace -o run --output-format csv -- $B > $out/bench_trace.log 2>&1 || exit 1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex gf_matmul -d $out/fetch -o run --output-format csv -- $B > $out/bench_fetch.log 2>&1 || exit 2
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex gf_matmul -d $out/write -o run --output-format csv -- $B > $out/bench_write.log 2>&1 || exit 3
