@@ -1103,10 +1103,21 @@ int group_run(hec_group* g, F&& body) {
         rc[i] = body(i);
         if (rc[i] != HEC_OK) err[i] = g_last_error;
     };
+    // Slots whose thread cannot be started run inline after slot 0; every
+    // started thread is joined before returning (a joinable std::thread that
+    // is destroyed would terminate the process across the ABI).
     std::vector<std::thread> th;
+    std::vector<size_t> inline_slots;
     th.reserve(n);
-    for (size_t i = 1; i < n; i++) th.emplace_back(run, i);
+    for (size_t i = 1; i < n; i++) {
+        try {
+            th.emplace_back(run, i);
+        } catch (...) {
+            inline_slots.push_back(i);
+        }
+    }
     run(0);
+    for (size_t i : inline_slots) run(i);
     for (auto& t : th) t.join();
     for (size_t i = 0; i < n; i++)
         if (rc[i] != HEC_OK) {
