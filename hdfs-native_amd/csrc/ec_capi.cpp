@@ -679,11 +679,13 @@ int hec_encode_host_batch(hec_coder_t* c, const uint8_t* h_data, uint8_t* h_pari
 
 // Pipelined pinned-host decode straight into file order (the reader's
 // ec_decode + cell split + concatenation, ec/mod.rs:62-89 and
-// block_reader.rs:480-554, in one pass).  Slot layout: file region
-// [chunk][k][cell] + parity region [m][chunk][cell].  Present data cells are
-// copied H2D straight into their file-order slots (2D copies), missing ones
-// are written there by the decode kernel, and the file region goes back D2H
-// in one contiguous copy.
+// block_reader.rs:480-554, in one pass).  The k survivors go H2D, one
+// contiguous copy per shard per chunk; the decode kernel writes the e missing
+// cells to a compact region; only those come back D2H, each as a 2D copy into
+// its file slots.  The present data
+// cells never make the round trip: host threads copy them from the vertical
+// buffers into their file slots while the DMA engines run, so PCIe carries
+// k cells in and e cells out per row instead of k in and k out.
 int hec_decode_host_batch(hec_coder_t* c, const uint8_t* const* h_vertical, size_t cell_len, size_t rows,
                           uint8_t* h_file, size_t chunk_rows) {
     if (!c || !h_vertical || !h_file || cell_len == 0 || chunk_rows == 0) return HEC_ERR_INVALID_ARG;
@@ -694,66 +696,105 @@ int hec_decode_host_batch(hec_coder_t* c, const uint8_t* const* h_vertical, size
         for (size_t i = 0; i < k + m; i++) present[i] = h_vertical[i] != nullptr;
         const DecodePlan& p = cached_plan(c, present);
         if (p.status != HEC_OK) return p.status;
-        std::lock_guard<std::mutex> lk(c->host_mu);
-        DeviceGuard g(c->device);
-        if (!g.ok) return fail(HEC_ERR_DEVICE, "hipSetDevice", hipErrorInvalidDevice);
-        constexpr int kSlots = hec_coder::kSlots;
-        chunk_rows = std::min(chunk_rows, rows);
-        const size_t file_bytes = chunk_rows * k * cell_len;
-        const size_t par_bytes = chunk_rows * m * cell_len;
-        const size_t slot_bytes = file_bytes + par_bytes;
-        int rc = ensure_dbuf(c, kSlots * slot_bytes);
-        if (rc != HEC_OK) return rc;
-        hipStream_t h2d = c->copy_stream[0], d2h = c->copy_stream[1];
-        const size_t nchunks = (rows + chunk_rows - 1) / chunk_rows;
-        for (size_t q = 0; q < nchunks; q++) {
-            const int slot = int(q % kSlots);
-            uint8_t* dfile = c->dbuf + slot * slot_bytes;
-            uint8_t* dpar = dfile + file_bytes;
-            const size_t r0 = q * chunk_rows;
-            const size_t nr = std::min(chunk_rows, rows - r0);
-            // slot reuse: the D2H of chunk q-3 (which follows its kernel) is done
-            if (q >= size_t(kSlots)) HEC_HIP(hipStreamWaitEvent(h2d, c->ev_out[slot], 0), HEC_ERR_DEVICE);
-            for (size_t i = 0; i < k; i++)
-                if (h_vertical[i])
-                    HEC_HIP(hipMemcpy2DAsync(dfile + i * cell_len, k * cell_len, h_vertical[i] + r0 * cell_len,
-                                             cell_len, cell_len, nr, hipMemcpyHostToDevice, h2d),
-                            HEC_ERR_DEVICE);
-            for (size_t j = 0; j < m; j++)
-                if (h_vertical[k + j] && std::find(p.survivors.begin(), p.survivors.end(), k + j) != p.survivors.end())
-                    HEC_HIP(hipMemcpyAsync(dpar + j * chunk_rows * cell_len, h_vertical[k + j] + r0 * cell_len,
+
+        // host side: present data cells -> file slots, rows split over up to
+        // 4 threads (the caller's thread takes the first share)
+        auto copy_rows = [&](size_t ra, size_t rb) {
+            for (size_t r = ra; r < rb; r++)
+                for (size_t i = 0; i < k; i++)
+                    if (h_vertical[i])
+                        std::memcpy(h_file + (r * k + i) * cell_len, h_vertical[i] + r * cell_len, cell_len);
+        };
+        const size_t copy_bytes = rows * (k - p.missing.size()) * cell_len;
+        const size_t max_threads = hec::g_tune_host_copy_threads > 0 ? size_t(hec::g_tune_host_copy_threads) : 4;
+        const size_t nthreads = std::min<size_t>(max_threads, std::max<size_t>(1, copy_bytes >> 24));  // >= 16 MiB each
+        std::vector<std::thread> copiers;
+        auto join_copiers = [&] {
+            for (auto& t : copiers) t.join();
+            copiers.clear();
+        };
+        size_t own_a = 0, own_b = rows;
+        if (nthreads > 1) {
+            copiers.reserve(nthreads - 1);
+            for (size_t t = 1; t < nthreads; t++) {
+                const size_t ra = rows * t / nthreads, rb = rows * (t + 1) / nthreads;
+                try {
+                    copiers.emplace_back(copy_rows, ra, rb);
+                } catch (...) {
+                    copy_rows(ra, rb);  // no thread: copy inline
+                }
+            }
+            own_b = rows / nthreads;
+        }
+        if (p.missing.empty()) {  // nothing to rebuild: a pure host copy
+            copy_rows(own_a, own_b);
+            join_copiers();
+            return HEC_OK;
+        }
+
+        int rc = [&]() -> int {
+            std::lock_guard<std::mutex> lk(c->host_mu);
+            DeviceGuard g(c->device);
+            if (!g.ok) return fail(HEC_ERR_DEVICE, "hipSetDevice", hipErrorInvalidDevice);
+            constexpr int kSlots = hec_coder::kSlots;
+            chunk_rows = std::min(chunk_rows, rows);
+            // slot: the k survivors shard-major [k][chunk][cell] (one
+            // contiguous H2D per survivor), then the e rebuilt cells
+            // [e][chunk][cell] (one 2D D2H per missing shard into its file slots)
+            const size_t e = p.missing.size();
+            const size_t shard_bytes = chunk_rows * cell_len;
+            const size_t slot_bytes = (k + e) * shard_bytes;
+            int rc2 = ensure_dbuf(c, kSlots * slot_bytes);
+            if (rc2 != HEC_OK) return rc2;
+            hipStream_t h2d = c->copy_stream[0], d2h = c->copy_stream[1];
+            const size_t nchunks = (rows + chunk_rows - 1) / chunk_rows;
+            for (size_t q = 0; q < nchunks; q++) {
+                const int slot = int(q % kSlots);
+                uint8_t* dsurv = c->dbuf + slot * slot_bytes;
+                uint8_t* dmiss = dsurv + k * shard_bytes;
+                const size_t r0 = q * chunk_rows;
+                const size_t nr = std::min(chunk_rows, rows - r0);
+                // slot reuse: the D2H of chunk q-3 (which follows its kernel) is done
+                if (q >= size_t(kSlots)) HEC_HIP(hipStreamWaitEvent(h2d, c->ev_out[slot], 0), HEC_ERR_DEVICE);
+                for (size_t r = 0; r < k; r++)
+                    HEC_HIP(hipMemcpyAsync(dsurv + r * shard_bytes, h_vertical[p.survivors[r]] + r0 * cell_len,
                                            nr * cell_len, hipMemcpyHostToDevice, h2d),
                             HEC_ERR_DEVICE);
-            HEC_HIP(hipEventRecord(c->ev_in[slot], h2d), HEC_ERR_DEVICE);
-            HEC_HIP(hipStreamWaitEvent(c->stream, c->ev_in[slot], 0), HEC_ERR_DEVICE);
-            if (!p.missing.empty()) {
+                HEC_HIP(hipEventRecord(c->ev_in[slot], h2d), HEC_ERR_DEVICE);
+                HEC_HIP(hipStreamWaitEvent(c->stream, c->ev_in[slot], 0), HEC_ERR_DEVICE);
                 const uint8_t* in[HEC_MAX_DATA_UNITS];
                 size_t ist[HEC_MAX_DATA_UNITS];
                 uint8_t* out[HEC_MAX_DATA_UNITS];
                 size_t ost[HEC_MAX_DATA_UNITS];
                 for (size_t r = 0; r < k; r++) {
-                    const size_t sh = p.survivors[r];
-                    in[r] = sh < k ? dfile + sh * cell_len : dpar + (sh - k) * chunk_rows * cell_len;
-                    ist[r] = sh < k ? k * cell_len : cell_len;
+                    in[r] = dsurv + r * shard_bytes;
+                    ist[r] = cell_len;
                 }
-                for (size_t r = 0; r < p.missing.size(); r++) {
-                    out[r] = dfile + p.missing[r] * cell_len;
-                    ost[r] = k * cell_len;
+                for (size_t r = 0; r < e; r++) {
+                    out[r] = dmiss + r * shard_bytes;
+                    ost[r] = cell_len;
                 }
-                rc = matmul_batch(c->device, p.matrix.data(), p.missing.size(), k, in, ist, out, ost, cell_len, nr,
-                                  c->stream);
-                if (rc != HEC_OK) return rc;
+                rc2 = matmul_batch(c->device, p.matrix.data(), e, k, in, ist, out, ost, cell_len, nr, c->stream);
+                if (rc2 != HEC_OK) return rc2;
+                HEC_HIP(hipEventRecord(c->ev_k[slot], c->stream), HEC_ERR_DEVICE);
+                HEC_HIP(hipStreamWaitEvent(d2h, c->ev_k[slot], 0), HEC_ERR_DEVICE);
+                for (size_t r = 0; r < e; r++)  // rebuilt cells only, into their file slots
+                    HEC_HIP(hipMemcpy2DAsync(h_file + (r0 * k + p.missing[r]) * cell_len, k * cell_len,
+                                             dmiss + r * shard_bytes, cell_len, cell_len, nr, hipMemcpyDeviceToHost,
+                                             d2h),
+                            HEC_ERR_DEVICE);
+                HEC_HIP(hipEventRecord(c->ev_out[slot], d2h), HEC_ERR_DEVICE);
             }
-            HEC_HIP(hipEventRecord(c->ev_k[slot], c->stream), HEC_ERR_DEVICE);
-            HEC_HIP(hipStreamWaitEvent(d2h, c->ev_k[slot], 0), HEC_ERR_DEVICE);
-            HEC_HIP(hipMemcpyAsync(h_file + r0 * k * cell_len, dfile, nr * k * cell_len, hipMemcpyDeviceToHost, d2h),
-                    HEC_ERR_DEVICE);
-            HEC_HIP(hipEventRecord(c->ev_out[slot], d2h), HEC_ERR_DEVICE);
-        }
-        HEC_HIP(hipStreamSynchronize(h2d), HEC_ERR_DEVICE);
-        HEC_HIP(hipStreamSynchronize(c->stream), HEC_ERR_DEVICE);
-        HEC_HIP(hipStreamSynchronize(d2h), HEC_ERR_DEVICE);
-        return HEC_OK;
+            // every chunk is enqueued (the waits are device-side): the caller's
+            // host share runs while the DMA engines and the kernel work
+            copy_rows(own_a, own_b);
+            HEC_HIP(hipStreamSynchronize(h2d), HEC_ERR_DEVICE);
+            HEC_HIP(hipStreamSynchronize(c->stream), HEC_ERR_DEVICE);
+            HEC_HIP(hipStreamSynchronize(d2h), HEC_ERR_DEVICE);
+            return HEC_OK;
+        }();
+        join_copiers();  // always, also on a device error (never leave a joinable thread)
+        return rc;
     });
 }
 
@@ -1074,7 +1115,8 @@ int hec_decode_verify_device(hec_coder_t* c, int checksum_type, const uint8_t* c
 //      sums: measures the kernel's memory side),
 // 12 = CRC kernel register prefetch depth in tasks (0 default = 2, 1 or 2),
 // 13 = store cache policy of the register double-buffered kernel (key 5 = 3)
-//      at RS(6,3) / RS(10,4): 0 nt, 1 sc1, 2 sc0 sc1, 3 nt sc1, 4 plain.
+//      at RS(6,3) / RS(10,4): 0 nt, 1 sc1, 2 sc0 sc1, 3 nt sc1, 4 plain,
+// 14 = host threads copying present data cells in hec_decode_host_batch (0 = default 4).
 // ---- multi-GPU coder group -----------------------------------
 
 }  // extern "C"
@@ -1253,6 +1295,10 @@ int hec_tune_set(int key, int value) {
         case 13:
             if (value < 0 || value > 4) return HEC_ERR_INVALID_ARG;
             hec::g_tune_store_pol = value;
+            return HEC_OK;
+        case 14:
+            if (value < 0 || value > 64) return HEC_ERR_INVALID_ARG;
+            hec::g_tune_host_copy_threads = value;
             return HEC_OK;
         default: return HEC_ERR_INVALID_ARG;
     }

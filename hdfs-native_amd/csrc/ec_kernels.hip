@@ -769,6 +769,7 @@ int g_tune_grid = 0;           // 0 = blocks_per_cu * CUs, else absolute block c
 int g_tune_group = 0;          // 0 = default (1), else stripes per tile-order group
 int g_tune_crc_unfused = 0;    // 1 = hec_encode_crc_device as two passes
 int g_tune_crc_variant = 0;    // 0 = default, 1 = slice-by-8 CRC, 2/3 = bank-replicated slice-by-1, 4/8 chains
+int g_tune_host_copy_threads = 0;  // 0 = default (4)
 int g_tune_store_pol = 0;      // 0 = nt stores, else store16p policy (register double-buffered kernel)
 int g_tune_crc_prefetch = 0;   // 0 = default (2), else tasks of register prefetch per wave (1 or 2)
 int g_tune_fused_slabs = 0;    // 0 = default, 4 / 8 = slabs per wave of the fused encode+CRC

@@ -310,6 +310,8 @@ int hec_group_decode_host_batch(hec_group_t *group, const uint8_t *const *h_vert
  * key 12: CRC register prefetch depth in 8-KiB tasks: 0 = default (2), 1 or 2
  * key 13: store cache policy of the double-buffered kernel at RS(6,3) / RS(10,4):
  *         0 = nt (default), 1 = sc1, 2 = sc0 sc1, 3 = nt sc1, 4 = plain
+ * key 14: host threads that copy the present data cells in hec_decode_host_batch
+ *         (0 = default 4)
  * Process-wide; affects launches made after the call. */
 int hec_tune_set(int key, int value);
 
