@@ -1,0 +1,39 @@
+/* asan_capi.c -- host-side AddressSanitizer + LeakSanitizer run over the C
+ * ABI paths that need no GPU: every coding matrix up to RS(32,16), the
+ * inversion, the decode plan of all 2^14 presence masks of RS(10,4), and the
+ * coder / group creation failure paths (no device in the container: each
+ * must return a status and leak nothing).  Built and run by
+ * scripts/asan_host.sh (tests/test_capi.py).  Device code is not sanitized
+ * (no GPU ASan on this pool). */
+#include <stdio.h>
+#include <string.h>
+#include "hdfs_ec_amd.h"
+int main(void) {
+    uint8_t m[14 * 10];
+    int bad = 0;
+    for (size_t k = 1; k <= 32; k++)
+        for (size_t p = 1; p <= 16; p++) {
+            uint8_t buf[48 * 32];
+            if (hec_gen_rs_matrix(k, p, buf) != HEC_OK) bad++;
+        }
+    if (hec_gen_rs_matrix(10, 4, m) != HEC_OK) bad++;
+    uint8_t sub[100];
+    memcpy(sub, m + 40, 60);      /* rows 4..9 (identity part) */
+    memcpy(sub + 60, m + 100, 40); /* + parity rows 10..13: a decodable 10 x 10 submatrix */
+    int rc = hec_matrix_invert(sub, 10);
+    uint8_t present[14]; size_t e, surv[10], miss[10]; uint8_t mat[100];
+    for (unsigned mask = 0; mask < (1u << 14); mask++) {
+        for (int i = 0; i < 14; i++) present[i] = (mask >> i) & 1;
+        int r = hec_decode_plan(10, 4, present, &e, surv, miss, mat);
+        if (r != HEC_OK && r != HEC_ERR_NOT_ENOUGH_SHARDS) bad++;
+    }
+    hec_group_t* g = 0; int devs[2] = {0, 0};
+    if (hec_group_create("rs", 6, 3, devs, 0, &g) != HEC_ERR_INVALID_ARG) bad++;
+    (void)hec_group_create("rs", 6, 3, devs, 2, &g);  /* no GPU here: a status, never a crash */
+    hec_group_destroy(g);
+    hec_coder_t* c = 0;
+    (void)hec_coder_create(6, 3, 0, &c);
+    hec_coder_destroy(c);
+    printf("invert rc=%d bad=%d last_error=%s\n", rc, bad, hec_last_error());
+    return bad != 0;
+}
