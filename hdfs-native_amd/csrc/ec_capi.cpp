@@ -1102,7 +1102,7 @@ int hec_decode_verify_device(hec_coder_t* c, int checksum_type, const uint8_t* c
 // key 1 = 16-B column chunks per lane (1|2|4), 2 = non-temporal loads/stores
 // (0|1), 3 = resident blocks per CU, 4 = threads per block (256|512),
 // 5 = pipeline (1 = register kernel, 2 = LDS-DMA prefetch kernel, 3 = register
-//     double-buffered kernel),
+//     double-buffered kernel, 4 = output-burst kernel),
 // 6 = chunk mapping (1 = block slabs, 2 = wave-contiguous runs), 7 = grid size,
 // 8 = tile-order group (stripes interleaved column-major; 1 = stripe-major),
 // 9 = 1: hec_encode_crc_device as two passes (encode, then CRC) instead of fused,
@@ -1116,7 +1116,8 @@ int hec_decode_verify_device(hec_coder_t* c, int checksum_type, const uint8_t* c
 // 12 = CRC kernel register prefetch depth in tasks (0 default = 2, 1 or 2),
 // 13 = store cache policy of the register double-buffered kernel (key 5 = 3)
 //      at RS(6,3) / RS(10,4): 0 nt, 1 sc1, 2 sc0 sc1, 3 nt sc1, 4 plain,
-// 14 = host threads copying present data cells in hec_decode_host_batch (0 = default 4).
+// 14 = host threads copying present data cells in hec_decode_host_batch (0 = default 4),
+// 15 = column tiles per store burst of the output-burst kernel (key 5 = 4): 2 or 3.
 // ---- multi-GPU coder group -----------------------------------
 
 }  // extern "C"
@@ -1262,7 +1263,7 @@ int hec_tune_set(int key, int value) {
             hec::g_tune_block = value;
             return HEC_OK;
         case 5:
-            if (value < 0 || value > 3) return HEC_ERR_INVALID_ARG;
+            if (value < 0 || value > 4) return HEC_ERR_INVALID_ARG;
             hec::g_tune_pipeline = value;
             return HEC_OK;
         case 6:
@@ -1299,6 +1300,10 @@ int hec_tune_set(int key, int value) {
         case 14:
             if (value < 0 || value > 64) return HEC_ERR_INVALID_ARG;
             hec::g_tune_host_copy_threads = value;
+            return HEC_OK;
+        case 15:
+            if (value != 0 && value != 2 && value != 3) return HEC_ERR_INVALID_ARG;
+            hec::g_tune_burst_tiles = value;
             return HEC_OK;
         default: return HEC_ERR_INVALID_ARG;
     }

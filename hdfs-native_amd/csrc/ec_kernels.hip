@@ -312,6 +312,98 @@ __global__ __launch_bounds__(BS) void gf_matmul_dma(MatmulArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Output-burst kernel (measurement variant, tune key 5 = 4): a block takes T
+// adjacent column tiles of one stripe, parks each tile's R x U accumulators
+// in LDS (every lane its own 16-B pieces: no barrier), and only after the T
+// tiles issues all the stores, stream by stream -- T x 16 KiB contiguous per
+// output stream per block instead of 16 KiB, and T tiles of pure reads
+// between write bursts.  tiles_per_stripe / total_tiles count super-tiles.
+// ---------------------------------------------------------------------------
+template <int K, int R, int T>
+__global__ __launch_bounds__(256) void gf_matmul_burst(MatmulArgs a) {
+    constexpr int U = 4, BS = 256;
+    constexpr uint32_t TILE = BS * U;
+    __shared__ PermTable s_tab[R][kMaxK];
+    __shared__ uint8_t s_exp[512];
+    __shared__ uint8_t s_log[256];
+    __shared__ uint8_t s_coef[R * kMaxK];
+    __shared__ u32x4 s_out[T][R][U][BS];
+    prologue<R, BS>(a, K, s_tab, s_exp, s_log, s_coef);
+    const uint32_t chunks = a.chunks;
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t st = blockIdx.x; st < a.total_tiles; st += gridDim.x) {
+        uint32_t stripe, scol;
+        tile_coords(st, a, stripe, scol);
+        int nt = 0;
+#pragma unroll
+        for (int t = 0; t < T; t++) {
+            const uint32_t base = (scol * T + t) * TILE;
+            if (base >= chunks) break;  // block-uniform
+            nt = t + 1;
+            asm volatile("" ::: "memory");
+            u32x4 x[U][K];
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const uint32_t col = base + u * BS + tid;
+                const uint64_t off = uint64_t(col < chunks ? col : 0) * 16u;
+#pragma unroll
+                for (int i = 0; i < K; i++) x[u][i] = load16<true>(a.in[i] + uint64_t(stripe) * a.in_stride[i] + off);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            u32x4 acc[U][R];
+#pragma unroll
+            for (int u = 0; u < U; u++)
+#pragma unroll
+                for (int j = 0; j < R; j++) acc[u][j] = u32x4{0, 0, 0, 0};
+#pragma unroll
+            for (int i = 0; i < K; i++) {
+                uint32_t toff = uint32_t(i) * uint32_t(sizeof(PermTable));
+                asm volatile("" : "+v"(toff));
+#pragma unroll
+                for (int u = 0; u < U; u++)
+#pragma unroll
+                    for (int j = 0; j < R; j++) asm volatile("" : "+v"(acc[u][j]) : "v"(toff));
+                Sel sl[U][4];
+#pragma unroll
+                for (int u = 0; u < U; u++)
+#pragma unroll
+                    for (int d = 0; d < 4; d++) sl[u][d] = make_sel(x[u][i][d]);
+#pragma unroll
+                for (int j = 0; j < R; j++) {
+                    const PermTable& tb =
+                        *reinterpret_cast<const PermTable*>(reinterpret_cast<const char*>(&s_tab[j][0]) + toff);
+                    const uint32_t t0lo = tb.t0lo, t0hi = tb.t0hi, t1lo = tb.t1lo, t1hi = tb.t1hi, t2 = tb.t2;
+#pragma unroll
+                    for (int u = 0; u < U; u++)
+#pragma unroll
+                        for (int d = 0; d < 4; d++)
+                            acc[u][j][d] ^= gf_mul4(t0lo, t0hi, t1lo, t1hi, t2, sl[u][d].s0, sl[u][d].s1, sl[u][d].s2);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+#pragma unroll
+            for (int u = 0; u < U; u++)
+#pragma unroll
+                for (int j = 0; j < R; j++) s_out[t][j][u][tid] = acc[u][j];
+        }
+        // the burst: every parked tile, one output stream after the other
+#pragma unroll
+        for (int j = 0; j < R; j++) {
+            uint8_t* ob = a.out[j] + uint64_t(stripe) * a.out_stride[j];
+#pragma unroll
+            for (int t = 0; t < T; t++) {
+                if (t >= nt) break;
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    const uint32_t col = (scol * T + t) * TILE + u * BS + tid;
+                    if (col < chunks) store16<true>(ob + uint64_t(col) * 16u, s_out[t][j][u][tid]);
+                }
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Register double-buffered kernel (compile-time K only).  Two register sets
 // of K x U chunks: the loads of tile t+1 are issued before tile t is
 // computed, so a wave always has one tile of loads in flight during its GF
@@ -733,6 +825,26 @@ const void* pipe_pol(int pol) {
     }
 }
 
+// Output-burst kernel: K in {2,3,6}, R * T <= 9 (T x R x 16 KiB of LDS).
+template <int T>
+const void* burst_pick(int k, int r) {
+    auto f = [](auto kk, auto rr) { return reinterpret_cast<const void*>(&gf_matmul_burst<kk.value, rr.value, T>); };
+    using std::integral_constant;
+    if (r > 9 / T) return nullptr;
+    switch (k) {
+        case 2: return r == 1 ? f(integral_constant<int, 2>{}, integral_constant<int, 1>{})
+                     : r == 2 ? f(integral_constant<int, 2>{}, integral_constant<int, 2>{})
+                              : f(integral_constant<int, 2>{}, integral_constant<int, (9 / T >= 3 ? 3 : 2)>{});
+        case 3: return r == 1 ? f(integral_constant<int, 3>{}, integral_constant<int, 1>{})
+                     : r == 2 ? f(integral_constant<int, 3>{}, integral_constant<int, 2>{})
+                              : f(integral_constant<int, 3>{}, integral_constant<int, (9 / T >= 3 ? 3 : 2)>{});
+        case 6: return r == 1 ? f(integral_constant<int, 6>{}, integral_constant<int, 1>{})
+                     : r == 2 ? f(integral_constant<int, 6>{}, integral_constant<int, 2>{})
+                              : f(integral_constant<int, 6>{}, integral_constant<int, (9 / T >= 3 ? 3 : 2)>{});
+        default: return nullptr;
+    }
+}
+
 const void* pick_pipe(int k, int r, int unroll) {
     // store-policy variants only at the bench shapes (RS(6,3), RS(10,4))
     if (g_tune_store_pol > 0 && unroll <= 2 && ((k == 6 && r == 3) || (k == 10 && r == 4))) {
@@ -769,6 +881,7 @@ int g_tune_grid = 0;           // 0 = blocks_per_cu * CUs, else absolute block c
 int g_tune_group = 0;          // 0 = default (1), else stripes per tile-order group
 int g_tune_crc_unfused = 0;    // 1 = hec_encode_crc_device as two passes
 int g_tune_crc_variant = 0;    // 0 = default, 1 = slice-by-8 CRC, 2/3 = bank-replicated slice-by-1, 4/8 chains
+int g_tune_burst_tiles = 0;         // output-burst kernel: column tiles per burst (2 or 3)
 int g_tune_host_copy_threads = 0;  // 0 = default (4)
 int g_tune_store_pol = 0;      // 0 = nt stores, else store16p policy (register double-buffered kernel)
 int g_tune_crc_prefetch = 0;   // 0 = default (2), else tasks of register prefetch per wave (1 or 2)
@@ -824,6 +937,14 @@ int launch_gf_matmul(const MatmulArgs& in, int device, hipStream_t stream) {
         const bool dma_ok = (a.k == 2 || a.k == 3 || a.k == 6 || a.k == 10);
         if (sh.dma && !dma_ok) sh.dma = false;
         if (sh.rpipe && !dma_ok) sh.rpipe = false;
+        // output-burst kernel (tune key 5 = 4, key 15 = T in {2, 3}): U = 4, 256 threads
+        const int burst_t = g_tune_pipeline == 4 ? (g_tune_burst_tiles == 3 ? 3 : 2) : 0;
+        const void* burst_fn = burst_t == 3 ? burst_pick<3>(a.k, a.r) : burst_t == 2 ? burst_pick<2>(a.k, a.r) : nullptr;
+        if (burst_fn) {
+            sh.dma = sh.rpipe = false;
+            sh.unroll = 4;
+            sh.block = 256;
+        }
         if (sh.rpipe) {
             sh.dma = false;
             sh.block = 256;
@@ -839,7 +960,7 @@ int launch_gf_matmul(const MatmulArgs& in, int device, hipStream_t stream) {
                 sh.unroll = 2;
             }
         }
-        const uint64_t tile = uint64_t(sh.block) * sh.unroll;
+        const uint64_t tile = uint64_t(sh.block) * sh.unroll * (burst_fn ? burst_t : 1);  // burst: super-tiles
         const uint64_t tps = (chunks + tile - 1) / tile;
         const uint64_t total = tps * a.stripes;
         if (chunks > 0xFFFFFFFFull || total > 0xFFFFFFFFull) return -1;
@@ -850,7 +971,8 @@ int launch_gf_matmul(const MatmulArgs& in, int device, hipStream_t stream) {
         // 4 stripes column-interleaved: +1-4 % over stripe-major at 1 MiB
         // cells (profiles/r01_probe_tile_order.log)
         a.group = g_tune_group > 0 ? uint32_t(g_tune_group) : 4u;
-        const void* fn = sh.rpipe ? pick_pipe(a.k, a.r, sh.unroll)
+        const void* fn = burst_fn ? burst_fn
+                         : sh.rpipe ? pick_pipe(a.k, a.r, sh.unroll)
                          : sh.dma ? pick_dma(a.k, a.r, sh.unroll, sh.block)
                                   : (sh.nt ? pick_shape<true>(a.k, a.r, sh.unroll, sh.block, sh.map)
                                            : pick_shape<false>(a.k, a.r, sh.unroll, sh.block, sh.map));

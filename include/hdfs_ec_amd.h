@@ -296,7 +296,7 @@ int hec_group_decode_host_batch(hec_group_t *group, const uint8_t *const *h_vert
  * key 3: resident blocks per CU for the grid (1..16; 0 = default)
  * key 4: threads per block (256 or 512; 0 = default)
  * key 5: kernel pipeline (1 = register, 2 = LDS-DMA prefetch, 3 = register
- *        double-buffered; 0 = default)
+ *        double-buffered, 4 = output bursts of key-15 column tiles; 0 = default)
  * key 6: chunk mapping (1 = block slabs, 2 = wave-contiguous runs; 0 = default)
  * key 7: absolute grid size in blocks (0 = default)
  * key 8: tile order, stripes interleaved per group (1 = stripe-major; 0 = default)
@@ -312,6 +312,7 @@ int hec_group_decode_host_batch(hec_group_t *group, const uint8_t *const *h_vert
  *         0 = nt (default), 1 = sc1, 2 = sc0 sc1, 3 = nt sc1, 4 = plain
  * key 14: host threads that copy the present data cells in hec_decode_host_batch
  *         (0 = default 4)
+ * key 15: column tiles per store burst of the output-burst kernel: 2 (default) or 3
  * Process-wide; affects launches made after the call. */
 int hec_tune_set(int key, int value);
 

@@ -303,6 +303,33 @@ def test_register_double_buffer_vs_oracle(dev, c_oracle, unroll, grid, k, m):
     assert torch.equal(out[:, :m], d[:, :m])
 
 
+@pytest.mark.parametrize("tiles", [2, 3])
+@pytest.mark.parametrize("grid", [0, 1, 5])
+@pytest.mark.parametrize("k,m", [(2, 1), (3, 2), (6, 3)])
+def test_output_burst_vs_oracle(dev, c_oracle, tiles, grid, k, m):
+    # tune key 5 = 4: outputs parked in LDS, stored in bursts of `tiles`
+    # column tiles; partial super-tiles at the cell end, many per block
+    S, cell = 3, 3 * 65536 + 48
+    data = batch_data(S, k, cell, first=cell + 11 * k + tiles)
+    want = oracle_batch_encode(c_oracle, k, m, data)
+    d = torch.from_numpy(data).to(dev)
+    p = torch.zeros((S, m, cell), dtype=torch.uint8, device=dev)
+    try:
+        H.tune_set(5, 4)
+        H.tune_set(15, tiles)
+        H.tune_set(7, grid)
+        H.encode_batch(coder(k, m), d, p)
+        out = torch.zeros_like(d)
+        H.decode_batch(coder(k, m), d, p, list(range(m)), out)
+        torch.cuda.synchronize()
+    finally:
+        H.tune_set(5, 0)
+        H.tune_set(15, 0)
+        H.tune_set(7, 0)
+    assert np.array_equal(p.cpu().numpy(), want)
+    assert torch.equal(out[:, :m], d[:, :m])
+
+
 @pytest.mark.parametrize("pol", [1, 2, 3, 4])
 @pytest.mark.parametrize("unroll", [1, 2])
 @pytest.mark.parametrize("k,m", [(6, 3), (10, 4)])
