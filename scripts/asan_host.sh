@@ -10,7 +10,7 @@ HIPCC=/opt/rocm/bin/hipcc
 CLANG=/opt/rocm/lib/llvm/bin/clang
 $HIPCC -O1 -g -std=c++17 -fPIC --offload-arch=gfx950 -Xarch_host -fsanitize=address \
     -Xarch_host -fno-omit-frame-pointer -x hip -c "$root/hdfs-native_amd/csrc/ec_capi.cpp" -o "$out/capi_asan.o"
-$HIPCC -shared -fPIC --offload-arch=gfx950 -fsanitize=address -o "$out/libhec_asan.so" "$out/capi_asan.o" \
+$HIPCC -shared -fPIC --offload-arch=gfx950 -fno-gpu-sanitize -fsanitize=address -o "$out/libhec_asan.so" "$out/capi_asan.o" \
     "$root/hdfs-native_amd/build/ec_kernels.o" "$root/hdfs-native_amd/build/ec_fused.o" \
     "$root/hdfs-native_amd/build/checksum.o"
 $CLANG -g -fsanitize=address -I"$root/include" "$root/tests/cpp/asan_capi.c" -o "$out/asan_capi" \
