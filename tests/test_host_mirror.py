@@ -14,17 +14,20 @@ BIN = os.path.join(PKG_DIR, "build", "test_host_mirror")
 
 
 SRCS = [os.path.join(PKG_DIR, "..", "tests", "cpp", "test_host_mirror.cpp"),
-        os.path.join(PKG_DIR, "csrc", "hdfs_ec.hpp"), os.path.join(PKG_DIR, "..", "include", "hdfs_ec_amd.h"),
-        os.path.join(PKG_DIR, "lib", "libhdfs_ec_amd.so")]
+        os.path.join(PKG_DIR, "csrc", "hdfs_ec.hpp"), os.path.join(PKG_DIR, "..", "include", "hdfs_ec_amd.h")]
 
 
 @pytest.fixture(scope="module")
 def binary():
-    # Build the driver only when it is missing or older than its own inputs:
-    # `make tests` would also walk the library's object files, which do not
-    # travel to the GPU box, and rebuild the whole engine there.
+    # Rebuilt only when missing or older than its own sources.  It links the
+    # engine dynamically, so a rebuilt .so needs no relink; and the compile is
+    # a direct g++ line, not `make`, whose rule would also walk the engine's
+    # object files -- they do not travel to the GPU box, so make would
+    # rebuild the whole engine there.
     if not os.path.exists(BIN) or os.path.getmtime(BIN) < max(os.path.getmtime(p) for p in SRCS):
-        subprocess.check_call(["make", "-s", "-C", PKG_DIR, "build/test_host_mirror"])
+        os.makedirs(os.path.dirname(BIN), exist_ok=True)
+        subprocess.check_call(["g++", "-O2", "-std=c++17", "-Wall", "-Wextra", "-pthread", "-o", BIN, SRCS[0],
+                               "-L" + os.path.join(PKG_DIR, "lib"), "-lhdfs_ec_amd", "-Wl,-rpath,$ORIGIN/../lib"])
     return BIN
 
 
