@@ -1117,7 +1117,8 @@ int hec_decode_verify_device(hec_coder_t* c, int checksum_type, const uint8_t* c
 // 13 = store cache policy of the register double-buffered kernel (key 5 = 3)
 //      at RS(6,3) / RS(10,4): 0 nt, 1 sc1, 2 sc0 sc1, 3 nt sc1, 4 plain,
 // 14 = host threads copying present data cells in hec_decode_host_batch (0 = default 4),
-// 15 = column tiles per store burst of the output-burst kernel (key 5 = 4): 2 or 3.
+// 15 = column tiles per store burst of the output-burst kernel (key 5 = 4): 2 or 3,
+// 16 = 1: XCD-contiguous block -> tile mapping in the register kernel.
 // ---- multi-GPU coder group -----------------------------------
 
 }  // extern "C"
@@ -1304,6 +1305,9 @@ int hec_tune_set(int key, int value) {
         case 15:
             if (value != 0 && value != 2 && value != 3) return HEC_ERR_INVALID_ARG;
             hec::g_tune_burst_tiles = value;
+            return HEC_OK;
+        case 16:
+            hec::g_tune_xcd_remap = value ? 1 : 0;
             return HEC_OK;
         default: return HEC_ERR_INVALID_ARG;
     }

@@ -60,7 +60,11 @@ __global__ __launch_bounds__(BS) void gf_matmul_v16(MatmulArgs a) {
     const uint32_t total = a.total_tiles;
     constexpr uint32_t TILE = BS * U;
 
-    for (uint32_t tile = blockIdx.x; tile < total; tile += gridDim.x) {
+    // Blocks are dispatched round-robin over the 8 XCDs (block b -> XCD b % 8);
+    // xcd_remap gives XCD x's blocks the contiguous logical range
+    // [x * grid/8, (x+1) * grid/8) (launcher: grid % 8 == 0)
+    const uint32_t first = a.xcd_remap ? (blockIdx.x % 8u) * (gridDim.x / 8u) + blockIdx.x / 8u : blockIdx.x;
+    for (uint32_t tile = first; tile < total; tile += gridDim.x) {
         uint32_t stripe, tcol;
         tile_coords(tile, a, stripe, tcol);
         // Keep the per-coefficient table reads inside the loop (LDS broadcast
@@ -881,6 +885,7 @@ int g_tune_grid = 0;           // 0 = blocks_per_cu * CUs, else absolute block c
 int g_tune_group = 0;          // 0 = default (1), else stripes per tile-order group
 int g_tune_crc_unfused = 0;    // 1 = hec_encode_crc_device as two passes
 int g_tune_crc_variant = 0;    // 0 = default, 1 = slice-by-8 CRC, 2/3 = bank-replicated slice-by-1, 4/8 chains
+int g_tune_xcd_remap = 0;           // 1 = XCD-contiguous block -> tile mapping
 int g_tune_burst_tiles = 0;         // output-burst kernel: column tiles per burst (2 or 3)
 int g_tune_host_copy_threads = 0;  // 0 = default (4)
 int g_tune_store_pol = 0;      // 0 = nt stores, else store16p policy (register double-buffered kernel)
@@ -978,6 +983,7 @@ int launch_gf_matmul(const MatmulArgs& in, int device, hipStream_t stream) {
                                            : pick_shape<false>(a.k, a.r, sh.unroll, sh.block, sh.map));
         uint64_t grid = g_tune_grid ? uint64_t(g_tune_grid) : uint64_t(cus) * sh.blocks_per_cu;
         if (grid > total) grid = total;
+        a.xcd_remap = (g_tune_xcd_remap && grid % 8 == 0) ? 1u : 0u;
         void* args[] = {&a};
         const hipError_t e = hipLaunchKernel(fn, dim3(uint32_t(grid)), dim3(sh.block), args, 0, stream);
         if (e != hipSuccess) return int(e);

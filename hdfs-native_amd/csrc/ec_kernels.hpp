@@ -28,6 +28,7 @@ struct MatmulArgs {
     uint32_t tiles_per_stripe;
     uint32_t total_tiles;
     uint32_t group;               // tile order: G stripes column-interleaved (1 = stripe-major)
+    uint32_t xcd_remap;           // register kernel: 1 = the 8 XCDs' blocks take contiguous tile runs
 };
 
 // One coefficient's v_perm_b32 product tables (see ec_kernels.hip): c*x =
@@ -86,6 +87,7 @@ extern int g_tune_crc_unfused;    // 1 = encode + separate CRC pass
 extern int g_tune_crc_variant;    // 0 = default, 1 = slice-by-8, 2/3 = bank-replicated slice-by-1, 4/8 chains
 extern int g_tune_crc_prefetch;   // 0 = default, 1 / 2 tasks of register prefetch (CRC kernel)
 extern int g_tune_fused_slabs;    // 0 = default, else 4 / 8 slabs per wave (fused encode+CRC)
+extern int g_tune_xcd_remap;           // 1 = XCD-contiguous block -> tile mapping (register kernel)
 extern int g_tune_burst_tiles;          // output-burst kernel (key 5 = 4): tiles per burst, 2 or 3
 extern int g_tune_host_copy_threads;  // 0 = default (4): hec_decode_host_batch's host copy threads
 extern int g_tune_store_pol;      // 0 = nt stores, 1..4 = sc1 | sc0 sc1 | nt sc1 | plain (pipelined kernel)

@@ -313,6 +313,8 @@ int hec_group_decode_host_batch(hec_group_t *group, const uint8_t *const *h_vert
  * key 14: host threads that copy the present data cells in hec_decode_host_batch
  *         (0 = default 4)
  * key 15: column tiles per store burst of the output-burst kernel: 2 (default) or 3
+ * key 16: 1 = the register kernel maps blocks to tiles XCD-contiguously (each XCD's
+ *         blocks take one contiguous run of tiles; 0 = round-robin, default)
  * Process-wide; affects launches made after the call. */
 int hec_tune_set(int key, int value);
 

@@ -220,7 +220,8 @@ def test_gf_matmul_device_arbitrary_matrix(dev):
 @pytest.mark.parametrize("knob", [((1, 1),), ((1, 2),), ((1, 4),), ((2, 0),), ((3, 2),), ((4, 512), (1, 1)),
                                   ((4, 512), (1, 2)), ((1, 4), (2, 0), (3, 3)), ((5, 2),), ((5, 2), (1, 2)),
                                   ((5, 2), (4, 512)), ((5, 2), (3, 2)), ((5, 1),), ((6, 2),), ((6, 2), (7, 100)),
-                                  ((7, 3),), ((8, 2),), ((8, 3),), ((8, 4), (5, 2)), ((8, 64),)])
+                                  ((7, 3),), ((8, 2),), ((8, 3),), ((8, 4), (5, 2)), ((8, 64),), ((16, 1),),
+                                  ((16, 1), (7, 16)), ((16, 1), (7, 12))])
 def test_tuning_variants_bit_identical(dev, c_oracle, knob):
     k, m, S, cell = 6, 3, 5, 8192 + 16
     data = batch_data(S, k, cell, first=21)
@@ -243,6 +244,7 @@ def test_tuning_variants_bit_identical(dev, c_oracle, knob):
         H.tune_set(6, 0)
         H.tune_set(7, 0)
         H.tune_set(8, 0)
+        H.tune_set(16, 0)
     assert np.array_equal(p.cpu().numpy(), want)
     for i in (0, 2, 4):
         assert torch.equal(out[:, i], d[:, i])
