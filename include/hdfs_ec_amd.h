@@ -251,9 +251,11 @@ int hec_encode_host_batch(hec_coder_t *coder, const uint8_t *h_data, uint8_t *h_
  * = its cells of `rows` consecutive rows, rows*cell_len bytes; NULL =
  * missing).  Writes the k*cell_len*rows file bytes, in file (row) order, to
  * h_file: present data cells are copied, missing ones reconstructed
- * (first-k-present survivors).  Same 3-slot pipeline as the encode;
- * HEC_ERR_NOT_ENOUGH_SHARDS when a data shard is missing and fewer than k
- * shards are present.  Synchronous. */
+ * (first-k-present survivors).  The k survivors stream H2D through the same
+ * 3-slot pipeline as the encode and only the rebuilt cells come back D2H;
+ * the present data cells are copied host-side (up to 4 threads) while the
+ * DMA runs.  HEC_ERR_NOT_ENOUGH_SHARDS when a data shard is missing and fewer
+ * than k shards are present.  Synchronous. */
 int hec_decode_host_batch(hec_coder_t *coder, const uint8_t *const *h_vertical, size_t cell_len, size_t rows,
                           uint8_t *h_file, size_t chunk_rows);
 
