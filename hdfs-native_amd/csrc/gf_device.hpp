@@ -51,6 +51,13 @@ __device__ void build_perm_table(PermTable* t, uint8_t c, const uint8_t* s_exp, 
     t->pad0 = t->pad1 = t->pad2 = 0;
 }
 
+// a ^ b ^ c in one VALU op (v_bitop3_b32, truth table 0x96).  hipcc mostly
+// emits two v_xor_b32 for it; spelled out, the GF math drops from 3 to 2
+// XOR-type ops per (dword, coefficient).
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
 // c * x for the four bytes of x.  v_perm_b32(S0=hi, S1=lo, sel): selector
 // byte 0..3 picks a byte of lo, 4..7 a byte of hi.
 __device__ __forceinline__ uint32_t gf_mul4(uint32_t t0lo, uint32_t t0hi, uint32_t t1lo, uint32_t t1hi,
@@ -58,7 +65,7 @@ __device__ __forceinline__ uint32_t gf_mul4(uint32_t t0lo, uint32_t t0hi, uint32
     uint32_t a = __builtin_amdgcn_perm(t0hi, t0lo, s0);
     uint32_t b = __builtin_amdgcn_perm(t1hi, t1lo, s1);
     uint32_t c = __builtin_amdgcn_perm(t2, t2, s2);
-    return a ^ b ^ c;
+    return xor3(a, b, c);
 }
 
 struct Sel {

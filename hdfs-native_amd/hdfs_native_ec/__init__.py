@@ -19,7 +19,8 @@ import os
 from typing import List, Optional, Sequence
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libhdfs_ec_amd.so")
+LIB_PATH = os.environ.get("HEC_LIB_PATH") or os.path.join(os.path.dirname(_HERE), "lib", "libhdfs_ec_amd.so")
+# HEC_LIB_PATH: another in-tree build of the engine, for same-box A/B measurements
 
 HEC_OK = 0
 HEC_ERR_INVALID_ARG = -1
