@@ -73,27 +73,30 @@ __global__ __launch_bounds__(BS) void gf_matmul_v16(MatmulArgs a) {
         if constexpr (K > 0) {
             // Compile-time K: every shard's loads for all U chunks are issued
             // before any arithmetic (K*U x 1 KiB in flight per wave).
+            // 32-bit lane offsets from wave-uniform stripe bases: the loads
+            // and stores take the saddr form, with no per-access 64-bit VALU
+            // address add (the launcher keeps cells below 4 GiB here)
             u32x4 x[U][K];
             bool live[U];
-            uint64_t offs[U];
+            uint32_t offs[U];
 #pragma unroll
             for (int u = 0; u < U; u++) {
                 const uint32_t col = chunk_col<U, BS, MAP>(tcol * TILE, u, threadIdx.x);
                 live[u] = col < chunks;
-                offs[u] = uint64_t(live[u] ? col : 0) * 16u;
+                offs[u] = (live[u] ? col : 0u) * 16u;
             }
             if constexpr (MAP == 0) {
 #pragma unroll
                 for (int u = 0; u < U; u++)
 #pragma unroll
                     for (int i = 0; i < K; i++)
-                        x[u][i] = load16<NT>(a.in[i] + uint64_t(stripe) * a.in_stride[i] + offs[u]);
+                        x[u][i] = load16<NT>((a.in[i] + uint64_t(stripe) * a.in_stride[i]) + offs[u]);
             } else {
 #pragma unroll
                 for (int i = 0; i < K; i++)
 #pragma unroll
                     for (int u = 0; u < U; u++)
-                        x[u][i] = load16<NT>(a.in[i] + uint64_t(stripe) * a.in_stride[i] + offs[u]);
+                        x[u][i] = load16<NT>((a.in[i] + uint64_t(stripe) * a.in_stride[i]) + offs[u]);
             }
             __builtin_amdgcn_sched_barrier(0);
             u32x4 acc[U][R];
@@ -138,7 +141,7 @@ __global__ __launch_bounds__(BS) void gf_matmul_v16(MatmulArgs a) {
                     if (!live[u]) continue;
 #pragma unroll
                     for (int j = 0; j < R; j++)
-                        store16<NT>(a.out[j] + uint64_t(stripe) * a.out_stride[j] + offs[u], acc[u][j]);
+                        store16<NT>((a.out[j] + uint64_t(stripe) * a.out_stride[j]) + offs[u], acc[u][j]);
                 }
             } else {
 #pragma unroll
@@ -146,7 +149,7 @@ __global__ __launch_bounds__(BS) void gf_matmul_v16(MatmulArgs a) {
 #pragma unroll
                     for (int u = 0; u < U; u++) {
                         if (!live[u]) continue;
-                        store16<NT>(a.out[j] + uint64_t(stripe) * a.out_stride[j] + offs[u], acc[u][j]);
+                        store16<NT>((a.out[j] + uint64_t(stripe) * a.out_stride[j]) + offs[u], acc[u][j]);
                     }
             }
         } else {
@@ -218,10 +221,10 @@ __global__ __launch_bounds__(BS) void gf_matmul_dma(MatmulArgs a) {
         for (int u = 0; u < U; u++) {
             uint32_t col = tcol * TILE + u * BS + wave * 64 + lane;
             col = col < chunks ? col : chunks - 1;  // dead lanes fetch a valid chunk, never stored
-            const uint64_t off = uint64_t(col) * 16u;
+            const uint32_t off = col * 16u;           // cells < 4 GiB (launcher): saddr + 32-bit offset
 #pragma unroll
             for (int i = 0; i < K; i++) {
-                const uint8_t* src = a.in[i] + uint64_t(stripe) * a.in_stride[i] + off;
+                const uint8_t* src = (a.in[i] + uint64_t(stripe) * a.in_stride[i]) + off;
                 __builtin_amdgcn_global_load_lds(
                     reinterpret_cast<const void*>(src),
                     (__attribute__((address_space(3))) void*)(stage + (i * U + u) * PIECE), 16, 0,
@@ -294,20 +297,20 @@ __global__ __launch_bounds__(BS) void gf_matmul_dma(MatmulArgs a) {
         if (full) {
 #pragma unroll
             for (int u = 0; u < U; u++) {
-                const uint64_t off = uint64_t(tcol * TILE + u * BS + threadIdx.x) * 16u;
+                const uint32_t off = (tcol * TILE + u * BS + threadIdx.x) * 16u;
 #pragma unroll
                 for (int j = 0; j < R; j++)
-                    store16<true>(a.out[j] + uint64_t(stripe) * a.out_stride[j] + off, acc[u][j]);
+                    store16<true>((a.out[j] + uint64_t(stripe) * a.out_stride[j]) + off, acc[u][j]);
             }
         } else {
 #pragma unroll
             for (int u = 0; u < U; u++) {
                 const uint32_t col = tcol * TILE + u * BS + threadIdx.x;
                 if (col >= chunks) continue;
-                const uint64_t off = uint64_t(col) * 16u;
+                const uint32_t off = col * 16u;
 #pragma unroll
                 for (int j = 0; j < R; j++)
-                    store16<true>(a.out[j] + uint64_t(stripe) * a.out_stride[j] + off, acc[u][j]);
+                    store16<true>((a.out[j] + uint64_t(stripe) * a.out_stride[j]) + off, acc[u][j]);
             }
         }
         prev_full = full;
@@ -923,7 +926,9 @@ int launch_gf_matmul(const MatmulArgs& in, int device, hipStream_t stream) {
         aligned &= ((reinterpret_cast<uintptr_t>(a.in[i]) | a.in_stride[i]) & 15u) == 0;
     for (int j = 0; j < a.r; j++)
         aligned &= ((reinterpret_cast<uintptr_t>(a.out[j]) | a.out_stride[j]) & 15u) == 0;
-    const uint64_t chunks = aligned ? a.cell_len / 16 : 0;
+    // vector kernels address a cell with 32-bit lane offsets: cells of 4 GiB
+    // or more (HDFS cell sizes are int32) take the byte kernel
+    const uint64_t chunks = (aligned && a.cell_len < (uint64_t(1) << 32)) ? a.cell_len / 16 : 0;
     const int cus = num_cus(device);
 
     if (chunks > 0) {
