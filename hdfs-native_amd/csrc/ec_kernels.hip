@@ -909,7 +909,10 @@ struct Shape {
 };
 
 Shape default_shape(int k, uint64_t cell_len) {
-    if (k > 6) return {2, 512, 2, true, false, 0};  // RS(10,4): 20 x 1 KiB loads in flight per wave already
+    // RS(10,4): 20 x 1 KiB loads in flight per wave already.  One 512-thread
+    // block is resident per CU; a grid of 8 per CU (8 rounds) beats 2 by 3 %
+    // at 256-512 stripes and ties at 2048 (profiles/r01f_probe_bpc_k10_*.log)
+    if (k > 6) return {2, 512, 8, true, false, 0};
     // RS(3,2), RS(6,3): one wave per SIMD, 4 x 1 KiB per stream per wave.
     // Small cells (many short stripes) gain 2-3 % from the LDS-DMA prefetch;
     // 1 MiB cells lose ~5 % with it (profiles/r01_probe_dma_pipeline.log).
