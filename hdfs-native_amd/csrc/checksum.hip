@@ -273,7 +273,8 @@ int launch_checksum(const CrcArgs& in, int device, hipStream_t stream) {
         const int waves = scheme == 16 ? CrcShape<16>::kWaves : crcdev::sliced(scheme) ? CrcShape<1>::kWaves : CrcShape<4>::kWaves;
         const int per_cu = (crcdev::sliced(scheme) && scheme != 16) ? 2 : 1;  // LDS: 56 / 77.5 KiB; ~144 / ~154 KiB
         uint64_t grid = (tasks + waves - 1) / waves;
-        if (grid > uint64_t(cus) * per_cu) grid = uint64_t(cus) * per_cu;
+        const uint64_t cap = g_tune_grid ? uint64_t(g_tune_grid) : uint64_t(cus) * per_cu;
+        if (grid > cap) grid = cap;
         const void* fn = a.kind == crc::kCrc32c ? crc_pick<crc::kCrc32c>(scheme, pf) : crc_pick<crc::kCksum>(scheme, pf);
         e = hipLaunchKernel(fn, dim3(uint32_t(grid)), dim3(uint32_t(waves * 64)), args, 0, stream);
     } else {

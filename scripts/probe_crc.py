@@ -23,6 +23,8 @@ coder = H.Coder(6, 3, 0)
 # "scheme:prefetch,..." (tune keys 11:12); default: every scheme x prefetch
 variants = ([tuple(int(x) for x in v.split(":")) for v in os.environ["PROBE_VARIANTS"].split(",")]
             if os.environ.get("PROBE_VARIANTS") else [(v, p) for v in (1, 2, 3, 4, 9) for p in (1, 2)])
+for kv in filter(None, os.environ.get("PROBE_TUNE", "").split(",")):  # extra hec_tune_set keys, e.g. 7=2048
+    H.tune_set(*(int(v) for v in kv.split("=")))
 ref = H.crc32c_batch(coder, cells)
 times = {v: [] for v in variants}
 for _ in range(ROUNDS):

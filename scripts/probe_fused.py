@@ -52,6 +52,8 @@ def ver():
                                sums.data_ptr(), bad.data_ptr(), sp)
 
 
+for kv in filter(None, os.environ.get("PROBE_TUNE", "").split(",")):  # extra hec_tune_set keys, e.g. 7=2048
+    H.tune_set(*(int(v) for v in kv.split("=")))
 H.tune_set(11, 0)
 enc()
 torch.cuda.synchronize()
