@@ -916,8 +916,13 @@ Shape default_shape(int k, uint64_t cell_len) {
     // RS(3,2), RS(6,3): one wave per SIMD, 4 x 1 KiB per stream per wave.
     // Small cells (many short stripes) gain 2-3 % from the LDS-DMA prefetch;
     // 1 MiB cells lose ~5 % with it (profiles/r01_probe_dma_pipeline.log).
+    // The LDS-DMA kernel (one block resident per CU) runs a grid of 2 per CU:
+    // +3.3 % at 64 KiB x 16384 stripes, +1 % at x 65536, against 1 per CU
+    // (profiles/r01f_probe_grid_64k_*.log); the register kernel keeps exactly
+    // the resident blocks (2 per CU: -9 % at 1 MiB).
     const bool small = cell_len <= (256u << 10);
-    return {4, 256, 1, true, small && (k == 2 || k == 3 || k == 6), 0};
+    const bool dma = small && (k == 2 || k == 3 || k == 6);
+    return {4, 256, dma ? 2 : 1, true, dma, 0};
 }
 
 }  // namespace
