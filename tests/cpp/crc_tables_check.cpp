@@ -1,0 +1,105 @@
+// crc_tables_check.cpp -- host-side check of the compile-time CRC tables the
+// GPU kernels use (hdfs-native_amd/csrc/checksum_tables.hpp): for CRC32C and
+// CRC32 (CRC_32_CKSUM), the per-512-B-chunk checksum is recomputed on the CPU
+// three ways with the kernels' own algebra --
+//   s8  : 4 quarters by slicing-by-8 from state 0, placed with the
+//         "append 384/256/128 zero bytes" byte tables, + final512;
+//   w11 : the same quarters by 11-bit slicing, placed with the nibble tables;
+//   byte: the classic byte-serial loop, from the table slot the 11-bit
+//         scheme's tail reads (w11[5][x << 2]);
+// and printed as hex, one line per chunk, for tests/test_oracle.py to compare
+// with the oracle.  Input: splitmix64 bytes (seed argv[1], chunks argv[2]).
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "../../hdfs-native_amd/csrc/checksum_tables.hpp"
+
+using namespace hec::crc;
+
+static uint64_t splitmix(uint64_t& s) {
+    uint64_t z = (s += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+static uint32_t le32(const uint8_t* p) { return p[0] | (p[1] << 8) | (p[2] << 16) | (uint32_t(p[3]) << 24); }
+
+template <int KIND>
+struct Check {
+    static constexpr bool REFL = Spec<KIND>::kReflected;
+    const Tables<KIND>& t;
+    explicit Check(const Tables<KIND>& tt) : t(tt) {}
+
+    uint32_t pre(uint32_t crc) const { return REFL ? crc : __builtin_bswap32(crc); }
+    uint32_t q_s8(const uint8_t* q) const {
+        uint32_t r = 0;
+        for (int i = 0; i < 128; i += 8) {
+            const uint32_t lo = le32(q + i) ^ pre(r), hi = le32(q + i + 4);
+            r = t.slice[7][lo & 0xFF] ^ t.slice[6][(lo >> 8) & 0xFF] ^ t.slice[5][(lo >> 16) & 0xFF] ^
+                t.slice[4][lo >> 24] ^ t.slice[3][hi & 0xFF] ^ t.slice[2][(hi >> 8) & 0xFF] ^
+                t.slice[1][(hi >> 16) & 0xFF] ^ t.slice[0][hi >> 24];
+        }
+        return r;
+    }
+    uint32_t q_w11(const uint8_t* q) const {
+        uint32_t r = 0;
+        for (int i = 0; i < 128; i += 8) {
+            const uint32_t lo = le32(q + i) ^ pre(r), hi = le32(q + i + 4);
+            r = t.w11[0][lo & 0x7FF] ^ t.w11[1][(lo >> 11) & 0x7FF] ^ t.w11[2][lo >> 22] ^ t.w11[3][hi & 0x7FF] ^
+                t.w11[4][(hi >> 11) & 0x7FF] ^ t.w11[5][hi >> 22];
+        }
+        return r;
+    }
+    uint32_t shift_byte(int k, uint32_t r) const {
+        return t.shift[k][0][r & 0xFF] ^ t.shift[k][1][(r >> 8) & 0xFF] ^ t.shift[k][2][(r >> 16) & 0xFF] ^
+               t.shift[k][3][r >> 24];
+    }
+    uint32_t shift_nib(int k, uint32_t r) const {
+        uint32_t v = 0;
+        for (int q = 0; q < 8; q++) v ^= t.shift_nib[k][q][(r >> (4 * q)) & 15];
+        return v;
+    }
+    uint32_t chunk(const uint8_t* c, bool w11) const {
+        uint32_t v = 0;
+        for (int qi = 0; qi < 4; qi++) {
+            const uint32_t r = w11 ? q_w11(c + 128 * qi) : q_s8(c + 128 * qi);
+            v ^= qi < 3 ? (w11 ? shift_nib(qi, r) : shift_byte(qi, r)) : r;
+        }
+        return v ^ t.final512;
+    }
+    uint32_t chunk_bytes(const uint8_t* c) const {  // tail loop, 11-bit scheme's table slot
+        uint32_t r = Spec<KIND>::kInit;
+        for (int i = 0; i < 512; i++) {
+            const uint32_t idx = REFL ? ((r ^ c[i]) & 0xFF) : (((r >> 24) ^ c[i]) & 0xFF);
+            r = REFL ? (t.w11[5][idx << 2] ^ (r >> 8)) : (t.w11[5][idx << 2] ^ (r << 8));
+        }
+        return r ^ Spec<KIND>::kXorout;
+    }
+};
+
+static const Tables<kCrc32c> kT32c;
+static const Tables<kCksum> kTck;
+
+int main(int argc, char** argv) {
+    uint64_t seed = argc > 1 ? std::strtoull(argv[1], nullptr, 0) : 1;
+    const int chunks = argc > 2 ? std::atoi(argv[2]) : 8;
+    std::vector<uint8_t> data(size_t(chunks) * 512);
+    for (size_t i = 0; i < data.size(); i += 8) {
+        const uint64_t v = splitmix(seed);
+        for (int b = 0; b < 8; b++) data[i + b] = uint8_t(v >> (8 * b));
+    }
+    Check<kCrc32c> c32c(kT32c);
+    Check<kCksum> cck(kTck);
+    for (int k = 0; k < chunks; k++) {
+        const uint8_t* c = data.data() + 512 * k;
+        std::printf("%08x %08x %08x %08x %08x %08x\n", c32c.chunk(c, false), c32c.chunk(c, true),
+                    c32c.chunk_bytes(c), cck.chunk(c, false), cck.chunk(c, true), cck.chunk_bytes(c));
+    }
+    std::fflush(stdout);
+    // the data itself, for the oracle side
+    std::fwrite(data.data(), 1, data.size(), stderr);
+    return 0;
+}

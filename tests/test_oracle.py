@@ -285,3 +285,31 @@ def test_verified_read_row_semantics():
     out, bad = O.verified_read_row(k, m, bent, sums, bpc, O.CHECKSUM_NULL)
     assert bad == [0] * (k + m)
     assert out[2] == bent[2] and out[4] != cells[4]
+
+
+def test_device_crc_tables_vs_oracle(tmp_path):
+    """The compile-time tables the CRC kernels read (csrc/checksum_tables.hpp)
+    recombined on the host with the kernels' own algebra (slicing-by-8 and
+    11-bit quarters placed by zero-append tables, plus the byte-serial tail
+    slot) give the oracle's per-512-B-chunk CRC32C and CRC32 bit for bit."""
+    import os
+    import shutil
+    import subprocess
+    gxx = shutil.which("g++")
+    if gxx is None:
+        pytest.skip("g++ not available")
+    src = os.path.join(os.path.dirname(__file__), "cpp", "crc_tables_check.cpp")
+    exe = str(tmp_path / "crc_tables_check")
+    subprocess.run([gxx, "-std=c++17", "-O2", "-o", exe, src], check=True)
+    chunks = 24
+    res = subprocess.run([exe, "0x5eed", str(chunks)], check=True, capture_output=True)
+    data = res.stderr
+    assert len(data) == 512 * chunks
+    lines = res.stdout.decode().split()
+    assert len(lines) == 6 * chunks
+    for i in range(chunks):
+        c = data[512 * i:512 * (i + 1)]
+        want32c = O.chunk_checksums(c, 512, O.CHECKSUM_CRC32C).hex()
+        want32 = O.chunk_checksums(c, 512, O.CHECKSUM_CRC32).hex()
+        assert lines[6 * i:6 * i + 3] == [want32c] * 3, i
+        assert lines[6 * i + 3:6 * i + 6] == [want32] * 3, i
