@@ -12,8 +12,15 @@ per stripe for the encode and again for the decode -- the reference
 Criterion convention Throughput::Bytes(6 x slice) (rust/benches/ec.rs:30,42).
 
 Multi-GPU: stripes are independent, so every rank codes its own batch of
-`--stripes` stripes (weak scaling) with no data-path collective; the
+`--stripes` stripes (weak scaling) -- or its contiguous share of
+`--global-stripes` (strong scaling) -- with no data-path collective; the
 process group is used only for the barrier and the max-over-ranks time.
+`--gpus N` without a launcher's WORLD_SIZE starts N ranks itself
+(torch.distributed.run, before anything touches the GPU).
+
+`--ref-cases` instead mirrors rust/benches/ec.rs (matrix inversion, rs-encode
+of 6 x 16 MiB, decode with 1/2/3 data slices missing) with the CPU port timed
+in the same run.
 
 Prints ONE JSON line on rank 0.
 """
@@ -22,6 +29,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import threading
 import time
@@ -34,15 +43,16 @@ METRIC = "GiB/s device-resident RS(6,3) encode+decode, 1 MiB cells, at 1/2/4/8 M
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 HBM_COPY_GBS = 6290.0  # measured float4 copy, same guide
 GIB = float(1 << 30)
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic_configs.json")
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--k", type=int, default=6)
-    ap.add_argument("--m", type=int, default=3)
+    ap.add_argument("--k", "--data-units", dest="k", type=int, default=6)
+    ap.add_argument("--m", "--parity-units", dest="m", type=int, default=3)
     ap.add_argument("--cell", type=int, default=1 << 20)
     ap.add_argument("--stripes", type=int, default=1024, help="stripes per GPU (weak scaling)")
     ap.add_argument("--global-stripes", type=int, default=0,
@@ -52,9 +62,9 @@ def parse():
                     help="also time the oracle stripe-parallel on T threads (default $OMP_NUM_THREADS: the "
                          "box's CPU share; 0/1 = single-threaded only)")
     ap.add_argument("--host-path", type=int, default=-1,
-                    help="also measure the PCIe-inclusive pinned-host pipelines (H2D + encode + D2H, and the "
-                         "striped-read decode into file order): 1 = yes, 0 = no, -1 = default (yes at N=1)")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+                    help="also measure the PCIe-inclusive paths (pinned pipelines and the per-call drop-in): "
+                         "1 = yes, 0 = no, -1 = default (yes at N=1)")
+    ap.add_argument("--traffic", default=TRAFFIC_FILE)
     ap.add_argument("--tune", default="", help="key=value,... passed to hec_tune_set (measurement)")
     ap.add_argument("--encode-only", action="store_true")
     ap.add_argument("--decode-mode", default="uniform", choices=["uniform", "mixed"],
@@ -62,9 +72,31 @@ def parse():
                          "1..m missing data shards per stripe (hec_decode_device_mixed)")
     ap.add_argument("--crc", action="store_true",
                     help="also time encode + CRC32C per 512-B chunk of all k+m cells (hec_encode_crc_device)")
+    ap.add_argument("--corrupt", default="0.01,0.1",
+                    help="with --crc: fractions of stripes with one corrupt survivor for the verified read")
+    ap.add_argument("--ref-cases", action="store_true",
+                    help="mirror rust/benches/ec.rs instead of the headline step (one JSON line)")
     ap.add_argument("--backend", default="nccl", help="process-group backend (nccl = RCCL; gloo for rehearsals)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher / rank / reduction plumbing only: no GPU, no engine, value null (CPU tests)")
     ap.add_argument("--spinup", type=float, default=0.5, help="untimed seconds of steps before warmup")
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def spawn_ranks(args) -> int:
+    """`--gpus N` run directly: start N ranks with torch.distributed.run
+    (loopback rendezvous) and return their exit status.  Runs before this
+    process touches the GPU."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    # torch.distributed.run's own parser prefix-matches "--m" (ambiguous with
+    # its --master-* / --max-* options) even after the script: pass the long name
+    fwd = ["--parity-units" + a[3:] if a == "--m" or a.startswith("--m=") else a for a in sys.argv[1:]]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + fwd
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.call(cmd, env=env)
 
 
 def host_info():
@@ -82,7 +114,8 @@ def host_info():
         usable = len(os.sched_getaffinity(0))
     except AttributeError:
         usable = os.cpu_count()
-    return {"cpu_model": model, "nproc": os.cpu_count(), "usable_cpus": usable}
+    return {"cpu_model": model, "nproc": os.cpu_count(), "usable_cpus": usable,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
 
 
 def cpu_baseline(k, m, cell, seconds, threads=1):
@@ -129,15 +162,232 @@ def cpu_baseline(k, m, cell, seconds, threads=1):
     for data, _, rec, *_ in bufs:
         assert np.array_equal(rec[:m], data[:m]), "cpu baseline decode mismatch"
     n = sum(counts)
-    return {"value": round(2 * n * k * cell / GIB / el, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
-            "sample": f"{n} x (encode + decode 0..{m - 1} missing) of one RS({k},{m}) stripe per thread, "
-                      f"{cell} B cells, {el:.1f} s on {threads} thread(s), C restatement oracle/ec_oracle.c "
-                      f"(reference Rust path unbuildable here)",
-            "host": host_info()}
+    hi = host_info()
+    res = {"value": round(2 * n * k * cell / GIB / el, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
+           "sample": f"{n} x (encode + decode 0..{m - 1} missing) of one RS({k},{m}) stripe per thread, "
+                     f"{cell} B cells, {el:.1f} s on {threads} thread(s), C restatement oracle/ec_oracle.c "
+                     f"(reference Rust path unbuildable here)",
+           "host": hi}
+    if threads > 1 and hi["usable_cpus"] and threads < hi["usable_cpus"]:
+        res["cores_reason"] = (f"the GPU box allots this run a {threads}-CPU share per GPU (OMP_NUM_THREADS="
+                               f"{hi['omp_num_threads']}; worker pools are sized to it) although "
+                               f"{hi['usable_cpus']} CPUs are visible")
+    return res
+
+
+def traffic_for(path, k, m, cell, stripes, mode):
+    """PMC HBM bytes per launch for this exact config, from the committed
+    per-config profile (scripts/profile_configs.py: FETCH_SIZE / WRITE_SIZE
+    passes of this same command on this tree), else None."""
+    if not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        tr = json.load(f)
+    for c in tr.get("configs", []):
+        if (c["k"], c["m"], c["cell"], c["stripes"], c.get("decode_mode", "uniform")) == (k, m, cell, stripes, mode):
+            return c["hbm_bytes_per_launch"], f"{os.path.relpath(path, ROOT)}:{c['config']} ({tr.get('tag')})"
+    return None, None
+
+
+def dry_run(args, world, rank):
+    """Plumbing only: ranks, rendezvous, the barrier and the max/sum
+    reductions bench.py uses, the JSON line -- no GPU and no engine."""
+    import torch.distributed as dist
+
+    from hdfs_native_ec.dist import max_over_ranks, shard_range, sum_over_ranks
+    if world > 1:
+        dist.init_process_group("gloo")
+    if args.global_stripes:
+        first, S = shard_range(args.global_stripes, world, rank)
+    else:
+        first, S = rank * args.stripes, args.stripes
+    t0 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    el = max_over_ranks(time.perf_counter() - t0)
+    total = sum_over_ranks(float(S))
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "GiB/s", "n_gpus": world, "dry_run": True,
+                          "scaling": "strong" if args.global_stripes else "weak",
+                          "config": {"k": args.k, "m": args.m, "cell_bytes": args.cell, "stripes_per_gpu": S,
+                                     "global_stripes": args.global_stripes or S * world,
+                                     "stripes_summed_over_ranks": int(total)},
+                          "max_elapsed_s": el}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def per_call_leg(H, k, m, cell, calls, oracle_lib):
+    """The drop-in exactly as the reference calls it: one Coder::encode per
+    row (CellBuffer::encode, block_writer.rs:838) and one Coder::decode per
+    row (ec/mod.rs:71-72), pageable host buffers, synchronous; the CPU port
+    per call beside it."""
+    import ctypes
+
+    import numpy as np
+
+    from hdfs_native_ec.synth import batch_data
+    coder = H.Coder(k, m, 0)
+    data = batch_data(1, k, cell, first=99)[0]
+    par = np.empty((m, cell), dtype=np.uint8)
+    rec = np.empty((k, cell), dtype=np.uint8)
+    ins = (ctypes.c_void_p * k)(*[data[i].ctypes.data for i in range(k)])
+    outs = (ctypes.c_void_p * m)(*[par[j].ctypes.data for j in range(m)])
+    shards = (ctypes.c_void_p * (k + m))(*([0] * m + [data[i].ctypes.data for i in range(m, k)] +
+                                            [par[j].ctypes.data for j in range(m)]))
+    recs = (ctypes.c_void_p * (k + m))(*([rec[i].ctypes.data for i in range(k)] + [0] * m))
+    lib = H.lib
+    res = {}
+    for name, fn in (("engine", lambda: (lib.hec_encode(coder.handle, ins, cell, outs),
+                                         lib.hec_decode(coder.handle, shards, cell, recs))),
+                     ("cpu_port", lambda: (oracle_lib.orc_encode(k, m, ins, cell, outs),
+                                           oracle_lib.orc_decode(k, m, shards, cell, recs)))):
+        n = calls if name == "engine" else max(2, calls // 16)
+        for _ in range(2):
+            rc = fn()
+            assert rc == (0, 0), f"{name} per-call rc {rc}"
+        te = td = 0.0
+        for _ in range(n):
+            t0 = time.perf_counter()
+            a = (lib.hec_encode(coder.handle, ins, cell, outs) if name == "engine"
+                 else oracle_lib.orc_encode(k, m, ins, cell, outs))
+            t1 = time.perf_counter()
+            b = (lib.hec_decode(coder.handle, shards, cell, recs) if name == "engine"
+                 else oracle_lib.orc_decode(k, m, shards, cell, recs))
+            t2 = time.perf_counter()
+            assert a == 0 and b == 0
+            te += t1 - t0
+            td += t2 - t1
+        assert np.array_equal(rec[:m], data[:m]), f"{name} per-call decode mismatch"
+        res[name] = {"encode_GiBps": round(n * k * cell / te / GIB, 3), "decode_GiBps": round(n * k * cell / td / GIB, 3),
+                     "encode_us_per_call": round(te / n * 1e6, 1), "decode_us_per_call": round(td / n * 1e6, 1),
+                     "calls": n}
+    coder.close()
+    res["note"] = (f"one RS({k},{m}) row of {cell} B cells per call, pageable host buffers: hec_encode then "
+                   f"hec_decode with data shards 0..{m - 1} missing (the Rust shim's per-row calls); cpu_port = "
+                   "oracle/ec_oracle.c on one core, same calls")
+    return res
+
+
+def ref_cases(args):
+    """rust/benches/ec.rs:5-64 mirrored: matrix-inversion/invert (RS(6,3)
+    rows 3..8), rs-encode/encode (one stripe of 6 x 16 MiB), and
+    rs-decode/decode-{1,2,3}-slice (data shards 0 / 0,1 / 0,1,2 missing).
+    Throughput is the reference's Throughput::Bytes(6 x slice).  Each case:
+    the engine device-resident (one stripe, hec_*_device + stream sync), the
+    engine's host drop-in (hec_encode / hec_decode on pageable buffers), and
+    the CPU port (oracle/ec_oracle.c, 1 core) in the same run."""
+    import ctypes
+
+    import numpy as np
+    import torch
+
+    import ec_oracle
+    import hdfs_native_ec as H
+    from hdfs_native_ec.synth import bench_counter_shards
+    olib = ec_oracle.load_c_oracle()
+    k, m, slice_ = 6, 3, 16 << 20
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    coder = H.Coder(k, m, 0)
+    stream = torch.cuda.current_stream(dev)
+    out = {"metric": "rust/benches/ec.rs cases (Criterion throughput = 6 x slice bytes)", "unit": "GiB/s",
+           "n_gpus": 1, "slice_bytes": slice_, "cases": {}}
+
+    def timeit(fn, reps, sync=None):
+        fn()
+        if sync:
+            sync()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        if sync:
+            sync()
+        return (time.perf_counter() - t0) / reps
+
+    # matrix-inversion/invert
+    enc = H.gen_rs_matrix(k, m)
+    sub = [enc[r] for r in range(3, 9)]
+    flat = (ctypes.c_uint8 * 36)()
+    flat_o = (ctypes.c_uint8 * 36)()
+
+    def inv_engine():
+        ctypes.memmove(flat, bytes(v for row in sub for v in row), 36)
+        assert H.lib.hec_matrix_invert(flat, 6) == 0
+
+    def inv_port():
+        ctypes.memmove(flat_o, bytes(v for row in sub for v in row), 36)
+        assert olib.orc_invert(flat_o, 6) == 0
+
+    t_e, t_p = timeit(inv_engine, 20000), timeit(inv_port, 20000)
+    assert bytes(flat) == bytes(flat_o)
+    out["cases"]["matrix-inversion/invert"] = {"engine_host_us": round(t_e * 1e6, 3), "cpu_port_us": round(t_p * 1e6, 3),
+                                               "note": "6x6 Gauss-Jordan over GF(2^8), host code (incl. a 36-B copy)"}
+
+    # rs-encode/encode: one stripe, the bench's big-endian counter fill
+    data = bench_counter_shards(k, slice_)
+    d = torch.from_numpy(np.stack(data)).unsqueeze(0).to(dev)
+    p = torch.empty((1, m, slice_), dtype=torch.uint8, device=dev)
+    t_dev = timeit(lambda: H.encode_batch(coder, d, p), 50, torch.cuda.synchronize)
+    ins = (ctypes.c_void_p * k)(*[x.ctypes.data for x in data])
+    par = [np.empty(slice_, dtype=np.uint8) for _ in range(m)]
+    outs = (ctypes.c_void_p * m)(*[x.ctypes.data for x in par])
+    t_host = timeit(lambda: H.lib.hec_encode(coder.handle, ins, slice_, outs), 10)
+    par_o = [np.empty(slice_, dtype=np.uint8) for _ in range(m)]
+    outs_o = (ctypes.c_void_p * m)(*[x.ctypes.data for x in par_o])
+    t_port = timeit(lambda: olib.orc_encode(k, m, ins, slice_, outs_o), 2)
+    assert all(np.array_equal(a, b) for a, b in zip(par, par_o))
+    assert all(np.array_equal(p[0, j].cpu().numpy(), par_o[j]) for j in range(m))
+    gib = k * slice_ / GIB
+    out["cases"]["rs-encode/encode"] = {"device_GiBps": round(gib / t_dev, 2), "host_call_GiBps": round(gib / t_host, 3),
+                                        "cpu_port_GiBps": round(gib / t_port, 4),
+                                        "device_ms": round(t_dev * 1e3, 4)}
+
+    # rs-decode/decode-{1,2,3}-slice
+    full = data + par_o
+    dp_all = torch.cat([d[0], p[0]]).unsqueeze(0)  # [1, k+m, slice]
+    for e in (1, 2, 3):
+        miss = list(range(e))
+        shard_ptrs = [None if i in miss else dp_all.data_ptr() + i * slice_ for i in range(k + m)]
+        rec = torch.empty((1, k, slice_), dtype=torch.uint8, device=dev)
+        rp = [rec.data_ptr() + i * slice_ for i in range(k)]
+        strides = [(k + m) * slice_] * (k + m)
+
+        def dec_dev():
+            coder.decode_device(shard_ptrs, strides, rp, [k * slice_] * k, slice_, 1, stream.cuda_stream)
+
+        t_dev = timeit(dec_dev, 50, torch.cuda.synchronize)
+        assert all(torch.equal(rec[0, i], d[0, i]) for i in miss)
+        hs = (ctypes.c_void_p * (k + m))(*[0 if i in miss else full[i].ctypes.data for i in range(k + m)])
+        hrec = [np.empty(slice_, dtype=np.uint8) for _ in range(k)]
+        hout = (ctypes.c_void_p * (k + m))(*([x.ctypes.data for x in hrec] + [0] * m))
+        t_host = timeit(lambda: H.lib.hec_decode(coder.handle, hs, slice_, hout), 10)
+        orec = [np.empty(slice_, dtype=np.uint8) for _ in range(k)]
+        oout = (ctypes.c_void_p * (k + m))(*([x.ctypes.data for x in orec] + [0] * m))
+        t_port = timeit(lambda: olib.orc_decode(k, m, hs, slice_, oout), 2)
+        assert all(np.array_equal(hrec[i], data[i]) and np.array_equal(orec[i], data[i]) for i in miss)
+        out["cases"][f"rs-decode/decode-{e}-slice"] = {
+            "device_GiBps": round(gib / t_dev, 2), "host_call_GiBps": round(gib / t_host, 3),
+            "cpu_port_GiBps": round(gib / t_port, 4), "device_ms": round(t_dev * 1e3, 4)}
+    out["note"] = ("device = one stripe already in HBM (hec_encode_device / hec_decode_device + sync); host_call = "
+                   "the drop-in on pageable host buffers (what the Rust shim calls); cpu_port = the C restatement "
+                   "of the reference loop on 1 core (the reference Rust bench cannot be built here: no cargo)")
+    out["host"] = host_info()
+    coder.close()
+    print(json.dumps(out), flush=True)
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args))  # before anything touches the GPU
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if args.dry_run:
+        return dry_run(args, world, rank)
+    if args.ref_cases:
+        return ref_cases(args)
+
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -145,8 +395,6 @@ def main():
     import hdfs_native_ec as H
     from hdfs_native_ec.dist import max_over_ranks, shard_range, sum_over_ranks
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     ndev = torch.cuda.device_count()
     local = local % max(1, ndev)  # rehearsal: several ranks may share one GPU (gloo only)
@@ -274,12 +522,7 @@ def main():
         dec_avg = sum(dec_ms) / len(dec_ms) * 1e-3 if dec_ms else enc_avg
         achieved = (algo_bytes + dec_bytes) / (enc_avg + dec_avg) / 1e9
 
-    traffic = None
-    if os.path.exists(args.traffic):
-        with open(args.traffic) as f:
-            tr = json.load(f)
-        if tr.get("config") == {"k": k, "m": m, "cell": cell, "stripes": S} and not mixed:
-            traffic = tr.get("hbm_bytes_per_launch")
+    traffic, traffic_src = traffic_for(args.traffic, k, m, cell, S, args.decode_mode) if not args.tune else (None, None)
 
     result = {
         "metric": METRIC,
@@ -314,7 +557,9 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
-            "kernel": f"gf_matmul_v16<{k},{m}> (encode and decode launches)",
+            "traffic_source": traffic_src,
+            "kernel": f"gf_matmul_v16<{k},{m}> (encode and decode launches)" if cell > (256 << 10) else
+                      f"gf_matmul_dma<{k},{m}> (encode and decode launches)",
             "algorithmic_bytes_per_launch": algo_bytes,
             "avg_launch_ms": round(avg_launch_ms, 4),
             "frac_of_measured_copy": round(achieved / HBM_COPY_GBS, 4),
@@ -325,139 +570,13 @@ def main():
     }
 
     if args.crc:
-        bpc = 512
-        nch = (cell + bpc - 1) // bpc
-        sums = torch.empty((S, k + m, nch, 4), dtype=torch.uint8, device=dev)
-        cells_ptrs, cells_strides = dp + pp, ds + ps
-
-        def enc_crc():
-            coder.encode_crc_device(dp, ds, pp, ps, cell, S, bpc, sums.data_ptr(), sp)
-
-        def crc_only():
-            coder.crc32c_device(cells_ptrs, cells_strides, cell, S, bpc, sums.data_ptr(), sp)
-
-        def enc_crc_unfused():
-            H.tune_set(9, 1)
-            try:
-                enc_crc()
-            finally:
-                H.tune_set(9, 0)
-
-        for fn in (enc_crc, crc_only, enc_crc_unfused):
-            fn()
-        torch.cuda.synchronize(dev)
-        reps = max(3, args.steps // 2)
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
-        ev[0].record(stream)
-        for _ in range(reps):
-            crc_only()
-        ev[1].record(stream)
-        for _ in range(reps):
-            enc_crc_unfused()
-        ev[2].record(stream)
-        for _ in range(reps):
-            enc_crc()  # last: the spot-check below reads the fused kernel's sums
-        ev[3].record(stream)
-        torch.cuda.synchronize(dev)
-        t_c = ev[0].elapsed_time(ev[1]) / reps * 1e-3
-        t_u = ev[1].elapsed_time(ev[2]) / reps * 1e-3
-        t_ec = ev[2].elapsed_time(ev[3]) / reps * 1e-3
-        # spot-check one stripe's sums against the oracle
-        s0_cells = torch.cat([data[0], parity[0]]).cpu().numpy()
-        want = b"".join(ec_oracle.chunk_crc32c(s0_cells[i].tobytes(), bpc) for i in range(k + m))
-        assert sums[0].cpu().numpy().tobytes() == want, "crc32c != oracle"
-        result["crc32c"] = {
-            "bytes_per_checksum": bpc,
-            "encode_crc_GiBps": round(k * cell * S / t_ec / GIB, 2),
-            "encode_crc_ms": round(t_ec * 1e3, 3),
-            "encode_crc_hbm_TBps": round((k + m) * cell * S / t_ec / 1e12, 3),
-            "encode_then_crc_GiBps": round(k * cell * S / t_u / GIB, 2),
-            "encode_then_crc_ms": round(t_u * 1e3, 3),
-            "crc_only_GBps": round((k + m) * cell * S / t_c / 1e9, 1),
-            "crc_only_ms": round(t_c * 1e3, 3),
-            "note": "CRC32C of all k+m cells per 512-B chunk (WritePacket::calculate_checksum), big-endian",
-        }
-        if not args.encode_only and not mixed:
-            # read side: survivors' chunk sums verified while the missing data
-            # cells are rebuilt (hec_decode_verify_device: fused kernel, then a
-            # host look at the flags); vs. verify pass + decode pass
-            bad = torch.empty((S, k + m), dtype=torch.uint8, device=dev)
-            surv = [i for i in range(k + m) if shard_ptrs[i] is not None][:k]
-            sv_ptrs = [(dp + pp)[i] for i in surv]
-            sv_strides = [(ds + ps)[i] for i in surv]
-            sv_sums = sums[:, surv].contiguous()
-
-            # present data shards are repaired in place if they fail
-            vo_ptrs = [rp[i] if i in miss else dp[i] for i in range(k)]
-            vo_strides = [rs[0] if i in miss else ds[i] for i in range(k)]
-
-            def dec_verify():
-                coder.decode_verify_device(H.CHECKSUM_CRC32C, shard_ptrs, ds + ps, vo_ptrs, vo_strides, cell, S,
-                                           bpc, sums.data_ptr(), bad.data_ptr(), sp)
-
-            def verify_then_decode():
-                bad.zero_()
-                coder.checksum_verify_device(H.CHECKSUM_CRC32C, sv_ptrs, sv_strides, cell, S, bpc,
-                                             sv_sums.data_ptr(), bad.data_ptr(), sp)
-                decode()
-                torch.cuda.synchronize(dev)
-
-            for fn in (dec_verify, verify_then_decode):
-                fn()
-            torch.cuda.synchronize(dev)
-            tv = {}
-            for name, fn in (("unfused", verify_then_decode), ("fused", dec_verify)):
-                t_0 = time.perf_counter()
-                for _ in range(reps):
-                    fn()
-                torch.cuda.synchronize(dev)
-                tv[name] = (time.perf_counter() - t_0) / reps
-            assert not bad.any() and torch.equal(rec, data[:, :m]), "decode+verify mismatch"
-            e_ = len(miss)
-            result["crc32c"].update({
-                "decode_verify_GiBps": round(k * cell * S / tv["fused"] / GIB, 2),
-                "decode_verify_ms": round(tv["fused"] * 1e3, 3),
-                "decode_verify_hbm_TBps": round((k + e_) * cell * S / tv["fused"] / 1e12, 3),
-                "verify_then_decode_GiBps": round(k * cell * S / tv["unfused"] / GIB, 2),
-                "verify_then_decode_ms": round(tv["unfused"] * 1e3, 3),
-                "read_note": "CRC32C of the k survivors verified against their packet sums while data shards "
-                             f"{{{','.join(map(str, miss))}}} are rebuilt (ReadPacket::get_data + ec_decode); "
-                             "wall time of the synchronous call incl. the flag read-back",
-            })
+        result["crc32c"] = crc_leg(args, H, coder, data, parity, rec, dp, ds, pp, ps, rp, rs, shard_ptrs, miss,
+                                   decode, dev, stream, mixed)
 
     host_path = args.host_path if args.host_path >= 0 else int(world == 1)
     if host_path and rank == 0 and not mixed:
-        # The path starts and ends in host memory (DataNode sockets in, write
-        # pipeline out): pinned host buffers through the coder's 3-slot
-        # H2D / kernel / D2H pipelines.  Never `value`.
-        hs = min(S, 256)
-        h_in = data[:hs].cpu().pin_memory()
-        h_out = torch.empty((hs, m, cell), dtype=torch.uint8).pin_memory()
-        coder.encode_host_batch(h_in.data_ptr(), h_out.data_ptr(), cell, hs, 16)
-        reps = 3
-        th0 = time.perf_counter()
-        for _ in range(reps):
-            coder.encode_host_batch(h_in.data_ptr(), h_out.data_ptr(), cell, hs, 16)
-        th = (time.perf_counter() - th0) / reps
-        assert torch.equal(h_out, parity[:hs].cpu())
-        # read side: the reader's per-shard vertical buffers (data shards
-        # 0..m-1 lost) -> file-order rows with the lost cells rebuilt
-        vert = [None if i < m else h_in[:, i].contiguous().pin_memory() for i in range(k)] + \
-               [h_out[:, j].contiguous().pin_memory() for j in range(m)]
-        h_file = torch.empty((hs, k, cell), dtype=torch.uint8).pin_memory()
-        vaddr = [None if v is None else v.data_ptr() for v in vert]
-        coder.decode_host_batch(vaddr, cell, hs, h_file.data_ptr(), 16)
-        td0 = time.perf_counter()
-        for _ in range(reps):
-            coder.decode_host_batch(vaddr, cell, hs, h_file.data_ptr(), 16)
-        td = (time.perf_counter() - td0) / reps
-        assert torch.equal(h_file, h_in)
-        result["host_path"] = {"encode_GiBps_pcie_inclusive": round(k * cell * hs / th / GIB, 2),
-                               "decode_GiBps_pcie_inclusive": round(k * cell * hs / td / GIB, 2),
-                               "stripes": hs, "chunk_stripes": 16,
-                               "note": "pinned host -> H2D -> kernel -> D2H -> pinned host, 3-slot pipelines "
-                                       "(hec_encode_host_batch; hec_decode_host_batch with data shards "
-                                       f"0..{m - 1} lost, file-order rows out); data GiB/s, never `value`"}
+        result["host_path"] = pinned_leg(coder, data, parity, k, m, cell, S, torch)
+        result["host_path"]["per_call"] = per_call_leg(H, k, m, cell, 64, clib)
 
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         result["cpu_baseline"] = cpu_baseline(k, m, cell, args.cpu_seconds, 1)
@@ -471,6 +590,181 @@ def main():
     coder.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def pinned_leg(coder, data, parity, k, m, cell, S, torch):
+    """The path starts and ends in host memory (DataNode sockets in, write
+    pipeline out): pinned host buffers through the coder's 3-slot
+    H2D / kernel / D2H pipelines.  Never `value`."""
+    hs = min(S, 256)
+    h_in = data[:hs].cpu().pin_memory()
+    h_out = torch.empty((hs, m, cell), dtype=torch.uint8).pin_memory()
+    coder.encode_host_batch(h_in.data_ptr(), h_out.data_ptr(), cell, hs, 16)
+    reps = 3
+    th0 = time.perf_counter()
+    for _ in range(reps):
+        coder.encode_host_batch(h_in.data_ptr(), h_out.data_ptr(), cell, hs, 16)
+    th = (time.perf_counter() - th0) / reps
+    assert torch.equal(h_out, parity[:hs].cpu())
+    # read side: the reader's per-shard vertical buffers (data shards
+    # 0..m-1 lost) -> file-order rows with the lost cells rebuilt
+    vert = [None if i < m else h_in[:, i].contiguous().pin_memory() for i in range(k)] + \
+           [h_out[:, j].contiguous().pin_memory() for j in range(m)]
+    h_file = torch.empty((hs, k, cell), dtype=torch.uint8).pin_memory()
+    vaddr = [None if v is None else v.data_ptr() for v in vert]
+    coder.decode_host_batch(vaddr, cell, hs, h_file.data_ptr(), 16)
+    td0 = time.perf_counter()
+    for _ in range(reps):
+        coder.decode_host_batch(vaddr, cell, hs, h_file.data_ptr(), 16)
+    td = (time.perf_counter() - td0) / reps
+    assert torch.equal(h_file, h_in)
+    return {"encode_GiBps_pcie_inclusive": round(k * cell * hs / th / GIB, 2),
+            "decode_GiBps_pcie_inclusive": round(k * cell * hs / td / GIB, 2),
+            "stripes": hs, "chunk_stripes": 16,
+            "note": "pinned host -> H2D -> kernel -> D2H -> pinned host, 3-slot pipelines "
+                    "(hec_encode_host_batch; hec_decode_host_batch with data shards "
+                    f"0..{m - 1} lost, file-order rows out); data GiB/s, never `value`"}
+
+
+def crc_leg(args, H, coder, data, parity, rec, dp, ds, pp, ps, rp, rs, shard_ptrs, miss, decode, dev, stream, mixed):
+    import torch
+
+    import ec_oracle
+    k, m, cell = args.k, args.m, args.cell
+    S = data.shape[0]
+    sp = stream.cuda_stream
+    bpc = 512
+    nch = (cell + bpc - 1) // bpc
+    sums = torch.empty((S, k + m, nch, 4), dtype=torch.uint8, device=dev)
+    cells_ptrs, cells_strides = dp + pp, ds + ps
+
+    def enc_crc():
+        coder.encode_crc_device(dp, ds, pp, ps, cell, S, bpc, sums.data_ptr(), sp)
+
+    def crc_only():
+        coder.crc32c_device(cells_ptrs, cells_strides, cell, S, bpc, sums.data_ptr(), sp)
+
+    def enc_crc_unfused():  # the two passes a non-fused engine runs
+        coder.encode_device(dp, ds, pp, ps, cell, S, sp)
+        crc_only()
+
+    for fn in (enc_crc, crc_only, enc_crc_unfused):
+        fn()
+    torch.cuda.synchronize(dev)
+    reps = max(3, args.steps // 2)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    ev[0].record(stream)
+    for _ in range(reps):
+        crc_only()
+    ev[1].record(stream)
+    for _ in range(reps):
+        enc_crc_unfused()
+    ev[2].record(stream)
+    for _ in range(reps):
+        enc_crc()  # last: the spot-check below reads the fused kernel's sums
+    ev[3].record(stream)
+    torch.cuda.synchronize(dev)
+    t_c = ev[0].elapsed_time(ev[1]) / reps * 1e-3
+    t_u = ev[1].elapsed_time(ev[2]) / reps * 1e-3
+    t_ec = ev[2].elapsed_time(ev[3]) / reps * 1e-3
+    # spot-check one stripe's sums against the oracle
+    s0_cells = torch.cat([data[0], parity[0]]).cpu().numpy()
+    want = b"".join(ec_oracle.chunk_crc32c(s0_cells[i].tobytes(), bpc) for i in range(k + m))
+    assert sums[0].cpu().numpy().tobytes() == want, "crc32c != oracle"
+    res = {
+        "bytes_per_checksum": bpc,
+        "encode_crc_GiBps": round(k * cell * S / t_ec / GIB, 2),
+        "encode_crc_ms": round(t_ec * 1e3, 3),
+        "encode_crc_hbm_TBps": round((k + m) * cell * S / t_ec / 1e12, 3),
+        "encode_crc_frac": round((k + m) * cell * S / t_ec / 1e9 / HBM_PEAK_GBS, 4),
+        "encode_then_crc_GiBps": round(k * cell * S / t_u / GIB, 2),
+        "encode_then_crc_ms": round(t_u * 1e3, 3),
+        "crc_only_GBps": round((k + m) * cell * S / t_c / 1e9, 1),
+        "crc_only_ms": round(t_c * 1e3, 3),
+        "note": "CRC32C of all k+m cells per 512-B chunk (WritePacket::calculate_checksum), big-endian",
+    }
+    if args.encode_only or mixed:
+        return res
+    # read side: survivors' chunk sums verified while the missing data cells
+    # are rebuilt (hec_decode_verify_device: fused kernel, then a host look at
+    # the flags); vs. verify pass + decode pass; then with corrupt survivors
+    bad = torch.empty((S, k + m), dtype=torch.uint8, device=dev)
+    surv = [i for i in range(k + m) if shard_ptrs[i] is not None][:k]
+    sv_ptrs = [(dp + pp)[i] for i in surv]
+    sv_strides = [(ds + ps)[i] for i in surv]
+    sv_sums = sums[:, surv].contiguous()
+    # present data shards are repaired in place if they fail
+    vo_ptrs = [rp[i] if i in miss else dp[i] for i in range(k)]
+    vo_strides = [rs[0] if i in miss else ds[i] for i in range(k)]
+
+    def dec_verify():
+        coder.decode_verify_device(H.CHECKSUM_CRC32C, shard_ptrs, ds + ps, vo_ptrs, vo_strides, cell, S, bpc,
+                                   sums.data_ptr(), bad.data_ptr(), sp)
+
+    def verify_then_decode():
+        bad.zero_()
+        coder.checksum_verify_device(H.CHECKSUM_CRC32C, sv_ptrs, sv_strides, cell, S, bpc, sv_sums.data_ptr(),
+                                     bad.data_ptr(), sp)
+        decode()
+        torch.cuda.synchronize(dev)
+
+    for fn in (dec_verify, verify_then_decode):
+        fn()
+    torch.cuda.synchronize(dev)
+    reps = max(3, args.steps // 2)
+    tv = {}
+    for name, fn in (("unfused", verify_then_decode), ("fused", dec_verify)):
+        t_0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize(dev)
+        tv[name] = (time.perf_counter() - t_0) / reps
+    assert not bad.any() and torch.equal(rec, data[:, :m]), "decode+verify mismatch"
+    e_ = len(miss)
+    res.update({
+        "decode_verify_GiBps": round(k * cell * S / tv["fused"] / GIB, 2),
+        "decode_verify_ms": round(tv["fused"] * 1e3, 3),
+        "decode_verify_hbm_TBps": round((k + e_) * cell * S / tv["fused"] / 1e12, 3),
+        "verify_then_decode_GiBps": round(k * cell * S / tv["unfused"] / GIB, 2),
+        "verify_then_decode_ms": round(tv["unfused"] * 1e3, 3),
+        "read_note": "CRC32C of the k survivors verified against their packet sums while data shards "
+                     f"{{{','.join(map(str, miss))}}} are rebuilt (ReadPacket::get_data + ec_decode); "
+                     "wall time of the synchronous call incl. the flag read-back",
+    })
+    # corrupt survivors: a fraction of the stripes gets one flipped byte in
+    # the first survivor (shard m: a data shard, repaired in place from the
+    # remaining cells); the call re-plans those stripes (phase 2)
+    corrupt = {}
+    victim = surv[0]
+    vbase = data if victim < k else parity
+    vidx = victim if victim < k else victim - k
+    for frac in [float(x) for x in filter(None, args.corrupt.split(","))]:
+        n_bad = max(1, int(round(frac * S)))
+        idx = torch.linspace(0, S - 1, n_bad, device=dev).long().unique()
+        orig = vbase[idx, vidx, 7].clone()
+
+        def corrupt_and_run():
+            vbase[idx, vidx, 7] ^= 0x5A
+            t_0 = time.perf_counter()
+            dec_verify()
+            torch.cuda.synchronize(dev)
+            t = time.perf_counter() - t_0
+            return t
+
+        ts = []
+        for _ in range(3):
+            ts.append(corrupt_and_run())
+            assert torch.equal(vbase[idx, vidx, 7], orig), "in-place repair failed"
+            flagged = bad[:, victim].nonzero().flatten()
+            assert torch.equal(flagged, idx), "wrong cells flagged"
+        assert torch.equal(rec, data[:, :m]), "decode+verify with corrupt survivors mismatch"
+        t = min(ts)
+        corrupt[f"{frac:g}"] = {"stripes_corrupt": int(idx.numel()), "ms": round(t * 1e3, 3),
+                                "GiBps": round(k * cell * S / t / GIB, 2)}
+    res["decode_verify_corrupt"] = corrupt
+    dec_verify()  # leave clean flags behind
+    torch.cuda.synchronize(dev)
+    return res
 
 
 if __name__ == "__main__":

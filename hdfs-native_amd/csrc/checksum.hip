@@ -211,12 +211,6 @@ __global__ __launch_bounds__(kCrcBlock) void checksum_chunks_bytes(CrcArgs a) {
     }
 }
 
-int num_cus_for(int dev) {
-    int v = 0;
-    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
-    return v;
-}
-
 template <int KIND, int SCHEME>
 const void* crc_fn(int pf) {
     return pf == 2 ? reinterpret_cast<const void*>(&checksum_chunks512<KIND, SCHEME, 2>)
@@ -225,12 +219,16 @@ const void* crc_fn(int pf) {
 
 template <int KIND>
 const void* crc_pick(int scheme, int pf) {
-    return scheme == 1    ? crc_fn<KIND, 1>(pf)
-           : scheme == 16 ? reinterpret_cast<const void*>(&checksum_chunks512<KIND, 16, 1>)
-           : scheme == 11 ? crc_fn<KIND, 11>(pf)
-           : scheme == 4  ? crc_fn<KIND, 4>(pf)
-           : scheme == 8 ? crc_fn<KIND, 8>(pf)
-                         : crc_fn<KIND, 0>(pf);
+#ifdef HEC_EXPERIMENTAL
+    // rejected schemes (profiles/r01_probe_crc.log, r01d_probe_crc_1024.log):
+    // bank-replicated slicing-by-1 with 4 / 8 chains, slicing-by-8 at 4 waves
+    // per SIMD, and the memory side alone (scheme 0: WRONG sums)
+    if (scheme == 16) return reinterpret_cast<const void*>(&checksum_chunks512<KIND, 16, 1>);
+    if (scheme == 4) return crc_fn<KIND, 4>(pf);
+    if (scheme == 8) return crc_fn<KIND, 8>(pf);
+    if (scheme == 0) return crc_fn<KIND, 0>(pf);
+#endif
+    return scheme == 1 ? crc_fn<KIND, 1>(pf) : crc_fn<KIND, 11>(pf);
 }
 
 }  // namespace
@@ -240,6 +238,8 @@ int launch_checksum(const CrcArgs& in, int device, hipStream_t stream) {
     if (a.bytes_per_checksum == 0 || a.cell_len == 0 || a.n_shards == 0) return -1;
     if (a.kind != crc::kCrc32c && a.kind != crc::kCksum) return -1;
     if (a.expected && !a.bad) return -1;
+    // sums are read / written as u32 by every path (fast and byte kernels)
+    if ((reinterpret_cast<uintptr_t>(a.out) | reinterpret_cast<uintptr_t>(a.expected)) & 3u) return -1;
     if (a.n_shards > uint32_t(kCrcMaxShards) || a.n_total < a.n_shards) return -1;
     a.mapped = a.n_total != a.n_shards;
     for (uint32_t i = 0; i < a.n_shards; i++) {
@@ -248,10 +248,11 @@ int launch_checksum(const CrcArgs& in, int device, hipStream_t stream) {
     }
     a.chunks_per_cell = (a.cell_len + a.bytes_per_checksum - 1) / a.bytes_per_checksum;
     if (a.stripes == 0) return 0;
-    bool aligned = a.cell_len % 16 == 0 && (reinterpret_cast<uintptr_t>(a.out) & 3u) == 0;
+    bool aligned = a.cell_len % 16 == 0;
     for (uint32_t i = 0; i < a.n_shards; i++)
         aligned &= ((reinterpret_cast<uintptr_t>(a.base[i]) | a.stride[i]) & 15u) == 0;
-    const int cus = num_cus_for(device);
+    const int cus = num_cus(device);
+    const Tune tn = tune_snapshot();
     void* args[] = {&a};
     hipError_t e;
     if (aligned && a.bytes_per_checksum == 512) {
@@ -263,17 +264,17 @@ int launch_checksum(const CrcArgs& in, int device, hipStream_t stream) {
         // vs 4.80 replicated, 4 chains, and 4.64, 8 chains; 4.64 for
         // slicing-by-8 at 4 waves per SIMD, r01d_probe_crc_1024.log); the
         // memory side alone reaches 6.4.
-        const int scheme = g_tune_crc_variant == 1   ? 1
-                           : g_tune_crc_variant == 2 ? 4
-                           : g_tune_crc_variant == 3 ? 8
-                           : g_tune_crc_variant == 4 ? 16
-                           : g_tune_crc_variant == 9 ? 0
-                                                     : 11;
-        const int pf = g_tune_crc_prefetch == 1 ? 1 : 2;  // scheme 16: always 1 (128 VGPRs at 4 waves/SIMD)
+        const int scheme = tn.crc_variant == 1   ? 1
+                           : tn.crc_variant == 2 ? 4
+                           : tn.crc_variant == 3 ? 8
+                           : tn.crc_variant == 4 ? 16
+                           : tn.crc_variant == 9 ? 0
+                                                 : 11;
+        const int pf = tn.crc_prefetch == 1 ? 1 : 2;  // scheme 16: always 1 (128 VGPRs at 4 waves/SIMD)
         const int waves = scheme == 16 ? CrcShape<16>::kWaves : crcdev::sliced(scheme) ? CrcShape<1>::kWaves : CrcShape<4>::kWaves;
         const int per_cu = (crcdev::sliced(scheme) && scheme != 16) ? 2 : 1;  // LDS: 56 / 77.5 KiB; ~144 / ~154 KiB
         uint64_t grid = (tasks + waves - 1) / waves;
-        const uint64_t cap = g_tune_grid ? uint64_t(g_tune_grid) : uint64_t(cus) * per_cu;
+        const uint64_t cap = tn.grid ? uint64_t(tn.grid) : uint64_t(cus) * per_cu;
         if (grid > cap) grid = cap;
         const void* fn = a.kind == crc::kCrc32c ? crc_pick<crc::kCrc32c>(scheme, pf) : crc_pick<crc::kCksum>(scheme, pf);
         e = hipLaunchKernel(fn, dim3(uint32_t(grid)), dim3(uint32_t(waves * 64)), args, 0, stream);

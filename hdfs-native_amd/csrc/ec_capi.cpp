@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <map>
+#include <memory>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -75,8 +76,18 @@ struct hec_coder {
     bool xor_codec = false;
     std::vector<uint8_t> enc;  // (k+m) x k
 
+    // Decode plans keyed by presence bitmask (k+m <= 48), bounded: at most
+    // kPlanCacheMax entries; past that the least recently used eighth is
+    // dropped (mixed and verified reads can feed it any mask).  Entries are
+    // shared_ptrs, so a plan a caller still holds outlives its eviction.
+    static constexpr size_t kPlanCacheMax = 4096;
+    struct PlanSlot {
+        std::shared_ptr<const DecodePlan> plan;
+        uint64_t last_use;
+    };
     std::mutex plan_mu;
-    std::unordered_map<uint64_t, DecodePlan> plans;  // key: presence bitmask (k+m <= 48)
+    std::unordered_map<uint64_t, PlanSlot> plans;
+    uint64_t plan_clock = 0;
 
     std::mutex host_mu;  // serialises the host-buffer API (staging buffers)
     static constexpr int kSlots = 3;
@@ -123,14 +134,33 @@ DecodePlan compute_plan(size_t k, size_t m, const uint8_t* present, const std::v
     return p;
 }
 
-const DecodePlan& cached_plan(hec_coder* c, const uint8_t* present) {
+using PlanRef = std::shared_ptr<const DecodePlan>;
+
+PlanRef cached_plan(hec_coder* c, const uint8_t* present) {
     uint64_t key = 0;
     for (size_t i = 0; i < c->k + c->m; i++)
         if (present[i]) key |= uint64_t(1) << i;
     std::lock_guard<std::mutex> lk(c->plan_mu);
+    const uint64_t now = ++c->plan_clock;
     auto it = c->plans.find(key);
-    if (it != c->plans.end()) return it->second;
-    return c->plans.emplace(key, compute_plan(c->k, c->m, present, c->enc)).first->second;
+    if (it != c->plans.end()) {
+        it->second.last_use = now;
+        return it->second.plan;
+    }
+    if (c->plans.size() >= hec_coder::kPlanCacheMax) {
+        // evict the least recently used eighth (one pass to find the cut)
+        std::vector<uint64_t> uses;
+        uses.reserve(c->plans.size());
+        for (const auto& kv : c->plans) uses.push_back(kv.second.last_use);
+        const size_t n_evict = c->plans.size() / 8;
+        std::nth_element(uses.begin(), uses.begin() + n_evict, uses.end());
+        const uint64_t cut = uses[n_evict];
+        for (auto e = c->plans.begin(); e != c->plans.end();)
+            e = e->second.last_use < cut ? c->plans.erase(e) : std::next(e);
+    }
+    PlanRef p = std::make_shared<const DecodePlan>(compute_plan(c->k, c->m, present, c->enc));
+    c->plans.emplace(key, hec_coder::PlanSlot{p, now});
+    return p;
 }
 
 // Runs out[j] = sum_i mat[j*cols+i] * in[i] over a batch, <= 4 rows per launch.
@@ -167,6 +197,19 @@ int matmul_batch(int device, const uint8_t* mat, size_t rows, size_t cols, const
     }
     return HEC_OK;
 }
+
+// Drains the coder's three streams on scope exit, errors ignored: a pipeline
+// that fails half-way never returns while its DMA still reads or writes the
+// caller's host buffers (or the slot buffers the next call may reallocate).
+struct StreamDrain {
+    hec_coder* c;
+    ~StreamDrain() {
+        (void)hipStreamSynchronize(c->copy_stream[0]);
+        (void)hipStreamSynchronize(c->stream);
+        (void)hipStreamSynchronize(c->copy_stream[1]);
+        (void)hipGetLastError();
+    }
+};
 
 int ensure_dbuf(hec_coder* c, size_t bytes) {
     if (c->dbuf_bytes >= bytes) return HEC_OK;
@@ -336,7 +379,8 @@ int hec_decode_device(hec_coder_t* c, const uint8_t* const* d_shards, const size
     return guarded([&] {
         uint8_t present[HEC_MAX_DATA_UNITS + HEC_MAX_PARITY_UNITS];
         for (size_t i = 0; i < c->k + c->m; i++) present[i] = d_shards[i] != nullptr;
-        const DecodePlan& p = cached_plan(c, present);
+        const PlanRef p_ref = cached_plan(c, present);
+        const DecodePlan& p = *p_ref;
         if (p.status != HEC_OK) return p.status;
         if (p.missing.empty()) return HEC_OK;
         if (!d_out || !out_strides) return HEC_ERR_INVALID_ARG;
@@ -396,7 +440,8 @@ int hec_decode(hec_coder_t* c, const uint8_t* const* shards, size_t shard_len, u
     return guarded([&] {
         uint8_t present[HEC_MAX_DATA_UNITS + HEC_MAX_PARITY_UNITS];
         for (size_t i = 0; i < c->k + c->m; i++) present[i] = shards[i] != nullptr;
-        const DecodePlan& p = cached_plan(c, present);
+        const PlanRef p_ref = cached_plan(c, present);
+        const DecodePlan& p = *p_ref;
         if (p.status != HEC_OK) return p.status;
         if (p.missing.empty()) return HEC_OK;
         if (!out) return HEC_ERR_INVALID_ARG;
@@ -449,9 +494,10 @@ size_t plan_bytes(size_t k, size_t m) {
     return sizeof(hec::DevPlanHeader) + std::min(k, m) * k * sizeof(hec::PermTable);
 }
 
+// [per-stripe plan offset: u32 x stripes][plan blob] (hec::MixedArgs)
 size_t mixed_workspace(size_t k, size_t m, size_t stripes) {
     const size_t p = max_plans(k, m, stripes);
-    return align_up(stripes * sizeof(uint16_t)) + align_up(p * sizeof(uint32_t)) + p * plan_bytes(k, m);
+    return align_up(stripes * sizeof(uint32_t)) + p * plan_bytes(k, m);
 }
 
 void free_host_buffer(void* p) { delete[] static_cast<uint8_t*>(p); }
@@ -476,7 +522,7 @@ int hec_decode_device_mixed(hec_coder_t* c, const uint8_t* const* d_shards, cons
         const uint64_t all = n >= 64 ? ~uint64_t(0) : ((uint64_t(1) << n) - 1);
         // 1. plan per distinct mask (host), fail before launching anything
         std::map<uint64_t, uint16_t> ids;
-        std::vector<const DecodePlan*> plans;
+        std::vector<PlanRef> plans;
         std::vector<uint16_t> stripe_plan(stripes);
         size_t max_e = 0;
         for (size_t s = 0; s < stripes; s++) {
@@ -485,13 +531,14 @@ int hec_decode_device_mixed(hec_coder_t* c, const uint8_t* const* d_shards, cons
             if (it == ids.end()) {
                 uint8_t pres[HEC_MAX_DATA_UNITS + HEC_MAX_PARITY_UNITS];
                 for (size_t i = 0; i < n; i++) pres[i] = (mask >> i) & 1;
-                const DecodePlan& p = cached_plan(c, pres);
+                const PlanRef p_ref = cached_plan(c, pres);
+        const DecodePlan& p = *p_ref;
                 if (p.status != HEC_OK) return p.status;
                 uint16_t id = 0xFFFF;
                 if (!p.missing.empty()) {
                     if (plans.size() >= 0xFFFF) return HEC_ERR_INVALID_ARG;
                     id = uint16_t(plans.size());
-                    plans.push_back(&p);
+                    plans.push_back(p_ref);
                     max_e = std::max(max_e, p.missing.size());
                 }
                 it = ids.emplace(mask, id).first;
@@ -499,7 +546,7 @@ int hec_decode_device_mixed(hec_coder_t* c, const uint8_t* const* d_shards, cons
             stripe_plan[s] = it->second;
         }
         if (plans.empty()) return HEC_OK;
-        for (const DecodePlan* p : plans)
+        for (const PlanRef& p : plans)
             for (size_t i : p->missing)
                 if (!d_out[i]) return HEC_ERR_INVALID_ARG;
         for (size_t i = 0; i < n; i++)
@@ -546,30 +593,32 @@ int hec_decode_device_mixed(hec_coder_t* c, const uint8_t* const* d_shards, cons
             return HEC_OK;
         }
 
-        // 2. workspace image: stripe_plan | plan_off | plan blobs
-        const size_t need = align_up(stripes * sizeof(uint16_t)) + align_up(plans.size() * sizeof(uint32_t)) +
-                            plans.size() * plan_bytes(k, m);
-        if (!d_workspace || workspace_bytes < need) return HEC_ERR_INVALID_ARG;
+        // 2. workspace image: per-stripe plan offsets | plan blobs
+        const size_t blob_pos = align_up(stripes * sizeof(uint32_t));
+        size_t blob_bytes = 0;
+        std::vector<uint32_t> plan_off(plans.size());
+        for (size_t pi = 0; pi < plans.size(); pi++) {
+            plan_off[pi] = uint32_t(blob_bytes);
+            blob_bytes += sizeof(hec::DevPlanHeader) + plans[pi]->missing.size() * k * sizeof(hec::PermTable);
+        }
+        const size_t need = blob_pos + blob_bytes;
+        if (!d_workspace || workspace_bytes < need || blob_bytes > 0xFFFFFFF0ull) return HEC_ERR_INVALID_ARG;
         uint8_t* host = new uint8_t[need]();
-        std::memcpy(host, stripe_plan.data(), stripes * sizeof(uint16_t));
-        const size_t off_pos = align_up(stripes * sizeof(uint16_t));
-        const size_t blob_pos = off_pos + align_up(plans.size() * sizeof(uint32_t));
-        uint32_t* offs = reinterpret_cast<uint32_t*>(host + off_pos);
-        size_t cur = 0;
+        uint32_t* soff = reinterpret_cast<uint32_t*>(host);
+        for (size_t s_ = 0; s_ < stripes; s_++)
+            soff[s_] = stripe_plan[s_] == 0xFFFF ? hec::kNoPlan : plan_off[stripe_plan[s_]];
         for (size_t pi = 0; pi < plans.size(); pi++) {
             const DecodePlan& p = *plans[pi];
-            offs[pi] = uint32_t(cur);
-            auto* hdr = reinterpret_cast<hec::DevPlanHeader*>(host + blob_pos + cur);
+            auto* hdr = reinterpret_cast<hec::DevPlanHeader*>(host + blob_pos + plan_off[pi]);
             hdr->e = uint32_t(p.missing.size());
             for (size_t r = 0; r < k; r++) hdr->surv[r] = uint8_t(p.survivors[r]);
             for (size_t r = 0; r < p.missing.size(); r++) hdr->miss[r] = uint8_t(p.missing[r]);
-            auto* tab = reinterpret_cast<uint32_t*>(host + blob_pos + cur + sizeof(hec::DevPlanHeader));
+            auto* tab = reinterpret_cast<uint32_t*>(host + blob_pos + plan_off[pi] + sizeof(hec::DevPlanHeader));
             for (size_t r = 0; r < p.missing.size(); r++)
                 for (size_t i = 0; i < k; i++) {
                     const auto w = hec::perm_table_words(p.matrix[r * k + i]);
                     std::memcpy(tab + (r * k + i) * 8, w.data(), sizeof(uint32_t) * 8);
                 }
-            cur += sizeof(hec::DevPlanHeader) + p.missing.size() * k * sizeof(hec::PermTable);
         }
         const hipError_t ce = hipMemcpyAsync(d_workspace, host, need, hipMemcpyHostToDevice, stream);
         if (ce != hipSuccess) {
@@ -598,10 +647,9 @@ int hec_decode_device_mixed(hec_coder_t* c, const uint8_t* const* d_shards, cons
             a.out_stride[i] = out_strides[i];
         }
         uint8_t* ws = static_cast<uint8_t*>(d_workspace);
-        a.stripe_plan = reinterpret_cast<const uint16_t*>(ws);
-        a.plan_off = reinterpret_cast<const uint32_t*>(ws + off_pos);
+        a.stripe_off = reinterpret_cast<const uint32_t*>(ws);
         a.plans = ws + blob_pos;
-        a.blob_bytes = uint32_t(cur);
+        a.blob_bytes = uint32_t(blob_bytes);
         a.k = int32_t(k);
         a.cell_len = cell_len;
         a.stripes = stripes;
@@ -629,6 +677,7 @@ int hec_encode_host_batch(hec_coder_t* c, const uint8_t* h_data, uint8_t* h_pari
         std::lock_guard<std::mutex> lk(c->host_mu);
         DeviceGuard g(c->device);
         if (!g.ok) return fail(HEC_ERR_DEVICE, "hipSetDevice", hipErrorInvalidDevice);
+        StreamDrain drain{c};
         const size_t k = c->k, m = c->m;
         constexpr int kSlots = hec_coder::kSlots;
         chunk_stripes = std::min(chunk_stripes, stripes);
@@ -694,7 +743,8 @@ int hec_decode_host_batch(hec_coder_t* c, const uint8_t* const* h_vertical, size
         const size_t k = c->k, m = c->m;
         uint8_t present[HEC_MAX_DATA_UNITS + HEC_MAX_PARITY_UNITS];
         for (size_t i = 0; i < k + m; i++) present[i] = h_vertical[i] != nullptr;
-        const DecodePlan& p = cached_plan(c, present);
+        const PlanRef p_ref = cached_plan(c, present);
+        const DecodePlan& p = *p_ref;
         if (p.status != HEC_OK) return p.status;
 
         // host side: present data cells -> file slots, rows split over up to
@@ -706,7 +756,8 @@ int hec_decode_host_batch(hec_coder_t* c, const uint8_t* const* h_vertical, size
                         std::memcpy(h_file + (r * k + i) * cell_len, h_vertical[i] + r * cell_len, cell_len);
         };
         const size_t copy_bytes = rows * (k - p.missing.size()) * cell_len;
-        const size_t max_threads = hec::g_tune_host_copy_threads > 0 ? size_t(hec::g_tune_host_copy_threads) : 4;
+        const int tuned_threads = hec::tune_snapshot().host_copy_threads;
+        const size_t max_threads = tuned_threads > 0 ? size_t(tuned_threads) : 4;
         const size_t nthreads = std::min<size_t>(max_threads, std::max<size_t>(1, copy_bytes >> 24));  // >= 16 MiB each
         std::vector<std::thread> copiers;
         auto join_copiers = [&] {
@@ -736,6 +787,7 @@ int hec_decode_host_batch(hec_coder_t* c, const uint8_t* const* h_vertical, size
             std::lock_guard<std::mutex> lk(c->host_mu);
             DeviceGuard g(c->device);
             if (!g.ok) return fail(HEC_ERR_DEVICE, "hipSetDevice", hipErrorInvalidDevice);
+            StreamDrain drain{c};  // before join_copiers and before returning, also on errors
             constexpr int kSlots = hec_coder::kSlots;
             chunk_rows = std::min(chunk_rows, rows);
             // slot: the k survivors shard-major [k][chunk][cell] (one
@@ -891,7 +943,7 @@ int hec_encode_crc_device(hec_coder_t* c, const uint8_t* const* d_data, const si
     if (stripes == 0) return HEC_OK;
     // Fused single pass when the shape allows it (k in {2,3,6,10}, m <= 4,
     // 512-B chunks, 16-B aligned cells); otherwise encode, then checksum.
-    if (bytes_per_checksum == 512 && c->m <= size_t(hec::kMaxR) && !hec::g_tune_crc_unfused) {
+    if (bytes_per_checksum == 512 && c->m <= size_t(hec::kMaxR) && !hec::tune_snapshot().crc_unfused) {
         const int rc = guarded([&] {
             DeviceGuard g(c->device);
             if (!g.ok) return fail(HEC_ERR_DEVICE, "hipSetDevice", hipErrorInvalidDevice);
@@ -962,7 +1014,8 @@ int hec_decode_verify_device(hec_coder_t* c, int checksum_type, const uint8_t* c
         const hipStream_t stream = static_cast<hipStream_t>(hip_stream);
         uint8_t present[HEC_MAX_DATA_UNITS + HEC_MAX_PARITY_UNITS];
         for (size_t i = 0; i < n; i++) present[i] = d_shards[i] != nullptr;
-        const DecodePlan& p = cached_plan(c, present);
+        const PlanRef p_ref = cached_plan(c, present);
+        const DecodePlan& p = *p_ref;
         if (p.status != HEC_OK) return p.status;  // fewer than k available: nothing is read
         std::vector<size_t> surv = p.survivors;
         if (p.missing.empty())
@@ -1073,7 +1126,8 @@ int hec_decode_verify_device(hec_coder_t* c, int checksum_type, const uint8_t* c
                 status = HEC_ERR_NOT_ENOUGH_SHARDS;
                 continue;
             }
-            const DecodePlan& q = cached_plan(c, avail);
+            const PlanRef q_ref = cached_plan(c, avail);
+        const DecodePlan& q = *q_ref;
             if (q.status != HEC_OK) return q.status;
             if (q.missing.empty()) continue;
             const uint8_t* qin[HEC_MAX_DATA_UNITS];
@@ -1097,28 +1151,8 @@ int hec_decode_verify_device(hec_coder_t* c, int checksum_type, const uint8_t* c
     });
 }
 
-// Tuning knobs for the measurement harness (not part of the reference API).
-// A value of 0 (-1 for key 2) restores the per-shape default.
-// key 1 = 16-B column chunks per lane (1|2|4), 2 = non-temporal loads/stores
-// (0|1), 3 = resident blocks per CU, 4 = threads per block (256|512),
-// 5 = pipeline (1 = register kernel, 2 = LDS-DMA prefetch kernel, 3 = register
-//     double-buffered kernel, 4 = output-burst kernel),
-// 6 = chunk mapping (1 = block slabs, 2 = wave-contiguous runs), 7 = grid size,
-// 8 = tile-order group (stripes interleaved column-major; 1 = stripe-major),
-// 9 = 1: hec_encode_crc_device as two passes (encode, then CRC) instead of fused,
-// 10 = slabs per wave of the fused encode+CRC kernel (0 default, 4 or 8),
-// 11 = CRC lookup scheme (0 default: 11-bit slicing in the CRC kernels,
-//      slice-by-8 in the fused ones; 1 slice-by-8 tables, 2 / 3 bank-replicated
-//      slice-by-1 with 4 / 8 chains per lane, 4 = slice-by-8 in 1024-thread
-//      blocks (4 waves per SIMD, CRC kernel only), 5 = 11-bit slicing (6 lookups
-//      per 8 bytes; CRC kernel only); 9 = loads + staging only, WRONG
-//      sums: measures the kernel's memory side),
-// 12 = CRC kernel register prefetch depth in tasks (0 default = 2, 1 or 2),
-// 13 = store cache policy of the register double-buffered kernel (key 5 = 3)
-//      at RS(6,3) / RS(10,4): 0 nt, 1 sc1, 2 sc0 sc1, 3 nt sc1, 4 plain,
-// 14 = host threads copying present data cells in hec_decode_host_batch (0 = default 4),
-// 15 = column tiles per store burst of the output-burst kernel (key 5 = 4): 2 or 3,
-// 16 = 1: XCD-contiguous block -> tile mapping in the register kernel.
+// Tuning knobs for the measurement harness: see include/hdfs_ec_amd.h and
+// csrc/tuning.hpp (atomics, snapshotted per launch).
 // ---- multi-GPU coder group -----------------------------------
 
 }  // extern "C"
@@ -1248,69 +1282,34 @@ int hec_group_decode_host_batch(hec_group_t* g, const uint8_t* const* h_vertical
     });
 }
 
+int hec_device_alloc(int device, size_t bytes, unsigned flags, void** out) {
+    if (!out || bytes == 0 || (flags & ~unsigned(HEC_ALLOC_CONTIGUOUS))) return HEC_ERR_INVALID_ARG;
+    *out = nullptr;
+    return guarded([&] {
+        DeviceGuard g(device);
+        if (!g.ok) return fail(HEC_ERR_DEVICE, "hipSetDevice", hipErrorInvalidDevice);
+        const unsigned hf = (flags & HEC_ALLOC_CONTIGUOUS) ? hipDeviceMallocContiguous : hipDeviceMallocDefault;
+        HEC_HIP(hipExtMallocWithFlags(out, bytes, hf), HEC_ERR_NO_MEMORY);
+        return HEC_OK;
+    });
+}
+
+int hec_device_free(int device, void* ptr) {
+    if (!ptr) return HEC_OK;
+    return guarded([&] {
+        DeviceGuard g(device);
+        if (!g.ok) return fail(HEC_ERR_DEVICE, "hipSetDevice", hipErrorInvalidDevice);
+        HEC_HIP(hipFree(ptr), HEC_ERR_DEVICE);
+        return HEC_OK;
+    });
+}
+
 int hec_tune_set(int key, int value) {
-    switch (key) {
-        case 1:
-            if (value < 0 || value > 4) return HEC_ERR_INVALID_ARG;
-            hec::g_tune_unroll = value;
-            return HEC_OK;
-        case 2: hec::g_tune_nt = value < 0 ? -1 : (value ? 1 : 0); return HEC_OK;
-        case 3:
-            if (value < 0 || value > 16) return HEC_ERR_INVALID_ARG;
-            hec::g_tune_blocks_per_cu = value;
-            return HEC_OK;
-        case 4:
-            if (value != 0 && value != 256 && value != 512) return HEC_ERR_INVALID_ARG;
-            hec::g_tune_block = value;
-            return HEC_OK;
-        case 5:
-            if (value < 0 || value > 4) return HEC_ERR_INVALID_ARG;
-            hec::g_tune_pipeline = value;
-            return HEC_OK;
-        case 6:
-            if (value < 0 || value > 2) return HEC_ERR_INVALID_ARG;
-            hec::g_tune_map = value;
-            return HEC_OK;
-        case 7:
-            if (value < 0 || value > 65536) return HEC_ERR_INVALID_ARG;
-            hec::g_tune_grid = value;
-            return HEC_OK;
-        case 8:
-            if (value < 0 || value > 65536) return HEC_ERR_INVALID_ARG;
-            hec::g_tune_group = value;
-            return HEC_OK;
-        case 9:
-            hec::g_tune_crc_unfused = value ? 1 : 0;
-            return HEC_OK;
-        case 10:
-            if (value != 0 && value != 4 && value != 8) return HEC_ERR_INVALID_ARG;
-            hec::g_tune_fused_slabs = value;
-            return HEC_OK;
-        case 11:
-            if ((value < 0 || value > 5) && value != 9) return HEC_ERR_INVALID_ARG;
-            hec::g_tune_crc_variant = value;
-            return HEC_OK;
-        case 12:
-            if (value < 0 || value > 2) return HEC_ERR_INVALID_ARG;
-            hec::g_tune_crc_prefetch = value;
-            return HEC_OK;
-        case 13:
-            if (value < 0 || value > 4) return HEC_ERR_INVALID_ARG;
-            hec::g_tune_store_pol = value;
-            return HEC_OK;
-        case 14:
-            if (value < 0 || value > 64) return HEC_ERR_INVALID_ARG;
-            hec::g_tune_host_copy_threads = value;
-            return HEC_OK;
-        case 15:
-            if (value != 0 && value != 2 && value != 3) return HEC_ERR_INVALID_ARG;
-            hec::g_tune_burst_tiles = value;
-            return HEC_OK;
-        case 16:
-            hec::g_tune_xcd_remap = value ? 1 : 0;
-            return HEC_OK;
-        default: return HEC_ERR_INVALID_ARG;
-    }
+    const int rc = hec::tune_store(key, value);
+    if (rc != HEC_OK)
+        std::snprintf(g_last_error, sizeof(g_last_error),
+                      "hec_tune_set: key %d value %d unknown, out of range or experimental-build only", key, value);
+    return rc;
 }
 
 }  // extern "C"

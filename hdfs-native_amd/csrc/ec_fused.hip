@@ -230,28 +230,21 @@ __global__ __launch_bounds__(crcdev::sliced(SCHEME) ? 256 : 512) __attribute__((
 
 namespace {
 
-int g_cus[64] = {0};
-
-int cus_of(int dev) {
-    if (dev < 0 || dev >= 64) return 256;
-    if (!g_cus[dev]) {
-        int v = 0;
-        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
-        g_cus[dev] = v;
-    }
-    return g_cus[dev];
-}
-
 // 8 slabs per wave while the r x 8 accumulators fit (k <= 6, r <= 3), else 4
 constexpr int fused_slabs(int k, int r) { return (r <= 3 && k <= 6) ? 8 : 4; }
 
 template <int K, int R>
 const void* encode_fn(int slabs, int scheme) {
-    if (scheme == 1)
-        return slabs == 4 ? reinterpret_cast<const void*>(&gf_fused_crc<K, R, 4, 1, crc::kCrc32c, false>)
-                          : reinterpret_cast<const void*>(&gf_fused_crc<K, R, 8, 1, crc::kCrc32c, false>);
-    return slabs == 4 ? reinterpret_cast<const void*>(&gf_fused_crc<K, R, 4, 4, crc::kCrc32c, false>)
-                      : reinterpret_cast<const void*>(&gf_fused_crc<K, R, 8, 4, crc::kCrc32c, false>);
+#ifdef HEC_EXPERIMENTAL
+    // bank-replicated slicing-by-1, 4 chains (tune key 11 = 2): 7-10 % slower
+    // (profiles/r01_probe_fused_scheme.log)
+    if (scheme == 4)
+        return slabs == 4 ? reinterpret_cast<const void*>(&gf_fused_crc<K, R, 4, 4, crc::kCrc32c, false>)
+                          : reinterpret_cast<const void*>(&gf_fused_crc<K, R, 8, 4, crc::kCrc32c, false>);
+#endif
+    (void)scheme;
+    return slabs == 4 ? reinterpret_cast<const void*>(&gf_fused_crc<K, R, 4, 1, crc::kCrc32c, false>)
+                      : reinterpret_cast<const void*>(&gf_fused_crc<K, R, 8, 1, crc::kCrc32c, false>);
 }
 
 // verify: default slabs and lookup scheme only, both checksum kinds
@@ -276,6 +269,7 @@ const void* pick_r(bool verify, int r, int slabs, int scheme, int kind) {
 
 int launch_fused(const MatmulArgs& in, const FusedCrcArgs& cs, bool verify, int device, hipStream_t stream) {
     MatmulArgs a = in;
+    const Tune tn = tune_snapshot();
     const void* sums = verify ? static_cast<const void*>(cs.expected) : static_cast<const void*>(cs.sums);
     bool aligned = a.cell_len % 16 == 0 && sums && (reinterpret_cast<uintptr_t>(sums) & 3u) == 0 && a.r >= 1 &&
                    a.r <= kMaxR && (!verify || cs.bad);
@@ -285,13 +279,13 @@ int launch_fused(const MatmulArgs& in, const FusedCrcArgs& cs, bool verify, int 
         aligned &= ((reinterpret_cast<uintptr_t>(a.out[j]) | a.out_stride[j]) & 15u) == 0;
     if (cs.kind != crc::kCrc32c && (cs.kind != crc::kCksum || !verify)) return -1;
     const int slabs = verify                                               ? fused_slabs(a.k, a.r)
-                      : (g_tune_fused_slabs == 4 || g_tune_fused_slabs == 8) ? g_tune_fused_slabs
+                      : (tn.fused_slabs == 4 || tn.fused_slabs == 8) ? tn.fused_slabs
                                                                              : fused_slabs(a.k, a.r);
     // checksum lookups (checksum_device.hpp): slicing-by-8 in 256-thread
     // blocks, 2 per CU, beats the bank-replicated tables in 512-thread blocks
     // by 7-10 % here (profiles/r01_probe_fused_scheme.log); tune key 11 = 2
     // selects the latter for encode
-    const int scheme = (!verify && g_tune_crc_variant == 2) ? 4 : 1;
+    const int scheme = (!verify && tn.crc_variant == 2) ? 4 : 1;
     const int waves = crcdev::sliced(scheme) ? 4 : 8;
     const void* fn = nullptr;
     switch (a.k) {
@@ -311,12 +305,12 @@ int launch_fused(const MatmulArgs& in, const FusedCrcArgs& cs, bool verify, int 
     a.chunks = uint32_t(chunks);
     a.tiles_per_stripe = uint32_t(tps);
     a.total_tiles = uint32_t(total);
-    a.group = g_tune_group > 0 ? uint32_t(g_tune_group) : 4u;
+    a.group = group_for(a.stripes, tn.group > 0 ? uint32_t(tn.group) : 4u);
     // LDS: ~61 KiB per 256-thread block (two per CU) / ~131 KiB per 512-thread block (one)
     // a grid of 8 blocks per CU (2 or 1 resident): finer-grained dynamic
     // scheduling beats exactly the resident blocks by 3 % (RS(6,3)) to 5 %
     // (RS(10,4))
-    uint64_t grid = g_tune_grid ? uint64_t(g_tune_grid) : uint64_t(cus_of(device)) * 8;
+    uint64_t grid = tn.grid ? uint64_t(tn.grid) : uint64_t(num_cus(device)) * 8;
     if (grid > total) grid = total;
     FusedCrcArgs c = cs;
     void* args[] = {&a, &c};

@@ -17,10 +17,13 @@
 //    of the byte lets a 2-dword, 8-entry byte pool answer each lookup with
 //    one v_perm_b32 on four bytes at once).  Per input dword: 5 selector ops;
 //    per (input dword, coefficient): 3 v_perm_b32 + 2 XOR (v_bitop3).
-//  * Grid = resident blocks only, grid-stride over (stripe, column-tile)
-//    tiles so the table prologue is paid once per block.
+//  * Grid-stride over (stripe, column-tile) tiles so the table prologue is
+//    paid once per block.
 //  * Tails (cell_len % 16) and unaligned layouts use a byte-granular kernel
 //    with LDS log/antilog lookups -- same results, correctness path.
+// Variants measured and rejected (register double buffering, output bursts,
+// store cache policies) live in ec_experimental.hip, built only into the
+// HEC_EXPERIMENTAL library.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -32,22 +35,11 @@
 namespace hec {
 
 // ---------------------------------------------------------------------------
-// Vector kernel: 16 B per lane per shard, U column chunks per lane.
-// K = compile-time input count (0 = runtime a.k), R = outputs (1..4).
+// Vector kernel: 16 B per lane per shard, U column chunks per lane (chunk u
+// of a tile is a contiguous BS-lane slab: a wave's U pieces are BS*16 B
+// apart).  K = compile-time input count (0 = runtime a.k), R = outputs (1..4).
 // ---------------------------------------------------------------------------
-// Column of chunk u of this lane within a tile.  MAP 0: chunk u of the
-// block is a contiguous BS-lane slab (a wave's U pieces are BS*16 B apart);
-// MAP 1: each wave owns U*64 contiguous chunks (one 4 KiB run per stream at
-// U=4) and issues a stream's pieces back to back.
-template <int U, int BS, int MAP>
-__device__ __forceinline__ uint32_t chunk_col(uint32_t tile_base, int u, uint32_t tid) {
-    if constexpr (MAP == 0)
-        return tile_base + u * BS + tid;
-    else
-        return tile_base + (tid / 64) * (U * 64) + u * 64 + (tid & 63);
-}
-
-template <int K, int R, int U, bool NT, int BS, int MAP = 0>
+template <int K, int R, int U, bool NT, int BS>
 __global__ __launch_bounds__(BS) void gf_matmul_v16(MatmulArgs a) {
     __shared__ PermTable s_tab[R][kMaxK];
     __shared__ uint8_t s_exp[512];
@@ -60,11 +52,19 @@ __global__ __launch_bounds__(BS) void gf_matmul_v16(MatmulArgs a) {
     const uint32_t total = a.total_tiles;
     constexpr uint32_t TILE = BS * U;
 
-    // Blocks are dispatched round-robin over the 8 XCDs (block b -> XCD b % 8);
-    // xcd_remap gives XCD x's blocks the contiguous logical range
-    // [x * grid/8, (x+1) * grid/8) (launcher: grid % 8 == 0)
-    const uint32_t first = a.xcd_remap ? (blockIdx.x % 8u) * (gridDim.x / 8u) + blockIdx.x / 8u : blockIdx.x;
-    for (uint32_t tile = first; tile < total; tile += gridDim.x) {
+    // Previous tile's store data (compile-time K).  Held live until the next
+    // tile's loads are issued, and every accumulator is materialised before
+    // the first store: the compiler then never overwrites a VGPR that an
+    // in-flight store still reads, so its waitcnt pass has no reason to drain
+    // the stores (s_waitcnt vmcnt(0)) before the next loads or between the
+    // chunks' stores -- it used to do both, twice per tile (same-box A/B:
+    // RS(3,2) +8 %, RS(6,3) +2 %, RS(10,4) +3 %; profiles/r02_ab_drain/).
+    u32x4 acc[U][R];
+#pragma unroll
+    for (int u = 0; u < U; u++)
+#pragma unroll
+        for (int j = 0; j < R; j++) acc[u][j] = u32x4{0, 0, 0, 0};
+    for (uint32_t tile = blockIdx.x; tile < total; tile += gridDim.x) {
         uint32_t stripe, tcol;
         tile_coords(tile, a, stripe, tcol);
         // Keep the per-coefficient table reads inside the loop (LDS broadcast
@@ -81,29 +81,20 @@ __global__ __launch_bounds__(BS) void gf_matmul_v16(MatmulArgs a) {
             uint32_t offs[U];
 #pragma unroll
             for (int u = 0; u < U; u++) {
-                const uint32_t col = chunk_col<U, BS, MAP>(tcol * TILE, u, threadIdx.x);
+                const uint32_t col = tcol * TILE + u * BS + threadIdx.x;
                 live[u] = col < chunks;
                 offs[u] = (live[u] ? col : 0u) * 16u;
             }
-            if constexpr (MAP == 0) {
-#pragma unroll
-                for (int u = 0; u < U; u++)
-#pragma unroll
-                    for (int i = 0; i < K; i++)
-                        x[u][i] = load16<NT>((a.in[i] + uint64_t(stripe) * a.in_stride[i]) + offs[u]);
-            } else {
-#pragma unroll
-                for (int i = 0; i < K; i++)
-#pragma unroll
-                    for (int u = 0; u < U; u++)
-                        x[u][i] = load16<NT>((a.in[i] + uint64_t(stripe) * a.in_stride[i]) + offs[u]);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            u32x4 acc[U][R];
 #pragma unroll
             for (int u = 0; u < U; u++)
 #pragma unroll
-                for (int j = 0; j < R; j++) acc[u][j] = u32x4{0, 0, 0, 0};
+                for (int i = 0; i < K; i++)
+                    x[u][i] = load16<NT>((a.in[i] + uint64_t(stripe) * a.in_stride[i]) + offs[u]);
+#pragma unroll
+            for (int u = 0; u < U; u++)
+#pragma unroll
+                for (int j = 0; j < R; j++) asm volatile("" ::"v"(acc[u][j]));
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int i = 0; i < K; i++) {
                 // Opaque per-input table offset: input i's coefficient-table
@@ -111,10 +102,12 @@ __global__ __launch_bounds__(BS) void gf_matmul_v16(MatmulArgs a) {
                 // compiler front-loads all R*K tables = R*K*5 VGPRs).
                 uint32_t toff = uint32_t(i) * uint32_t(sizeof(PermTable));
                 asm volatile("" : "+v"(toff));
+                if (i > 0) {
 #pragma unroll
-                for (int u = 0; u < U; u++)
+                    for (int u = 0; u < U; u++)
 #pragma unroll
-                    for (int j = 0; j < R; j++) asm volatile("" : "+v"(acc[u][j]) : "v"(toff));
+                        for (int j = 0; j < R; j++) asm volatile("" : "+v"(acc[u][j]) : "v"(toff));
+                }
                 Sel s[U][4];
 #pragma unroll
                 for (int u = 0; u < U; u++)
@@ -128,14 +121,26 @@ __global__ __launch_bounds__(BS) void gf_matmul_v16(MatmulArgs a) {
 #pragma unroll
                     for (int u = 0; u < U; u++)
 #pragma unroll
-                        for (int d = 0; d < 4; d++)
-                            acc[u][j][d] ^= gf_mul4(t0lo, t0hi, t1lo, t1hi, t2, s[u][d].s0, s[u][d].s1, s[u][d].s2);
+                        for (int d = 0; d < 4; d++) {
+                            const uint32_t p = gf_mul4(t0lo, t0hi, t1lo, t1hi, t2, s[u][d].s0, s[u][d].s1, s[u][d].s2);
+                            acc[u][j][d] = i == 0 ? p : (acc[u][j][d] ^ p);
+                        }
                 }
                 // one input at a time: stops the scheduler from hoisting every
                 // coefficient's table read (R*K*5 VGPRs) to the top
                 __builtin_amdgcn_sched_barrier(0);
             }
-            if constexpr (MAP == 0) {
+#pragma unroll
+            for (int u = 0; u < U; u++)
+#pragma unroll
+                for (int j = 0; j < R; j++) asm volatile("" : "+v"(acc[u][j]));
+            if ((tcol + 1) * TILE <= chunks) {  // block-uniform: the whole tile lies inside the cell
+#pragma unroll
+                for (int u = 0; u < U; u++)
+#pragma unroll
+                    for (int j = 0; j < R; j++)
+                        store16<NT>((a.out[j] + uint64_t(stripe) * a.out_stride[j]) + offs[u], acc[u][j]);
+            } else {
 #pragma unroll
                 for (int u = 0; u < U; u++) {
                     if (!live[u]) continue;
@@ -143,25 +148,17 @@ __global__ __launch_bounds__(BS) void gf_matmul_v16(MatmulArgs a) {
                     for (int j = 0; j < R; j++)
                         store16<NT>((a.out[j] + uint64_t(stripe) * a.out_stride[j]) + offs[u], acc[u][j]);
                 }
-            } else {
-#pragma unroll
-                for (int j = 0; j < R; j++)
-#pragma unroll
-                    for (int u = 0; u < U; u++) {
-                        if (!live[u]) continue;
-                        store16<NT>((a.out[j] + uint64_t(stripe) * a.out_stride[j]) + offs[u], acc[u][j]);
-                    }
             }
         } else {
             // Runtime K: one shard at a time, U chunks per lane.
 #pragma unroll
             for (int u = 0; u < U; u++) {
-                const uint32_t col = chunk_col<U, BS, MAP>(tcol * TILE, u, threadIdx.x);
+                const uint32_t col = tcol * TILE + u * BS + threadIdx.x;
                 if (col >= chunks) continue;
                 const uint64_t off = uint64_t(col) * 16u;
-                u32x4 acc[R];
+                u32x4 racc[R];
 #pragma unroll
-                for (int j = 0; j < R; j++) acc[j] = u32x4{0, 0, 0, 0};
+                for (int j = 0; j < R; j++) racc[j] = u32x4{0, 0, 0, 0};
                 for (int i = 0; i < k; i++) {
                     u32x4 x = load16<NT>(a.in[i] + uint64_t(stripe) * a.in_stride[i] + off);
                     Sel s[4];
@@ -173,11 +170,11 @@ __global__ __launch_bounds__(BS) void gf_matmul_v16(MatmulArgs a) {
                         const uint32_t t0lo = t.t0lo, t0hi = t.t0hi, t1lo = t.t1lo, t1hi = t.t1hi, t2 = t.t2;
 #pragma unroll
                         for (int d = 0; d < 4; d++)
-                            acc[j][d] ^= gf_mul4(t0lo, t0hi, t1lo, t1hi, t2, s[d].s0, s[d].s1, s[d].s2);
+                            racc[j][d] ^= gf_mul4(t0lo, t0hi, t1lo, t1hi, t2, s[d].s0, s[d].s1, s[d].s2);
                     }
                 }
 #pragma unroll
-                for (int j = 0; j < R; j++) store16<NT>(a.out[j] + uint64_t(stripe) * a.out_stride[j] + off, acc[j]);
+                for (int j = 0; j < R; j++) store16<NT>(a.out[j] + uint64_t(stripe) * a.out_stride[j] + off, racc[j]);
             }
         }
     }
@@ -319,333 +316,138 @@ __global__ __launch_bounds__(BS) void gf_matmul_dma(MatmulArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Output-burst kernel (measurement variant, tune key 5 = 4): a block takes T
-// adjacent column tiles of one stripe, parks each tile's R x U accumulators
-// in LDS (every lane its own 16-B pieces: no barrier), and only after the T
-// tiles issues all the stores, stream by stream -- T x 16 KiB contiguous per
-// output stream per block instead of 16 KiB, and T tiles of pure reads
-// between write bursts.  tiles_per_stripe / total_tiles count super-tiles.
-// ---------------------------------------------------------------------------
-template <int K, int R, int T>
-__global__ __launch_bounds__(256) void gf_matmul_burst(MatmulArgs a) {
-    constexpr int U = 4, BS = 256;
-    constexpr uint32_t TILE = BS * U;
-    __shared__ PermTable s_tab[R][kMaxK];
-    __shared__ uint8_t s_exp[512];
-    __shared__ uint8_t s_log[256];
-    __shared__ uint8_t s_coef[R * kMaxK];
-    __shared__ u32x4 s_out[T][R][U][BS];
-    prologue<R, BS>(a, K, s_tab, s_exp, s_log, s_coef);
-    const uint32_t chunks = a.chunks;
-    const uint32_t tid = threadIdx.x;
-    for (uint32_t st = blockIdx.x; st < a.total_tiles; st += gridDim.x) {
-        uint32_t stripe, scol;
-        tile_coords(st, a, stripe, scol);
-        int nt = 0;
-#pragma unroll
-        for (int t = 0; t < T; t++) {
-            const uint32_t base = (scol * T + t) * TILE;
-            if (base >= chunks) break;  // block-uniform
-            nt = t + 1;
-            asm volatile("" ::: "memory");
-            u32x4 x[U][K];
-#pragma unroll
-            for (int u = 0; u < U; u++) {
-                const uint32_t col = base + u * BS + tid;
-                const uint64_t off = uint64_t(col < chunks ? col : 0) * 16u;
-#pragma unroll
-                for (int i = 0; i < K; i++) x[u][i] = load16<true>(a.in[i] + uint64_t(stripe) * a.in_stride[i] + off);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            u32x4 acc[U][R];
-#pragma unroll
-            for (int u = 0; u < U; u++)
-#pragma unroll
-                for (int j = 0; j < R; j++) acc[u][j] = u32x4{0, 0, 0, 0};
-#pragma unroll
-            for (int i = 0; i < K; i++) {
-                uint32_t toff = uint32_t(i) * uint32_t(sizeof(PermTable));
-                asm volatile("" : "+v"(toff));
-#pragma unroll
-                for (int u = 0; u < U; u++)
-#pragma unroll
-                    for (int j = 0; j < R; j++) asm volatile("" : "+v"(acc[u][j]) : "v"(toff));
-                Sel sl[U][4];
-#pragma unroll
-                for (int u = 0; u < U; u++)
-#pragma unroll
-                    for (int d = 0; d < 4; d++) sl[u][d] = make_sel(x[u][i][d]);
-#pragma unroll
-                for (int j = 0; j < R; j++) {
-                    const PermTable& tb =
-                        *reinterpret_cast<const PermTable*>(reinterpret_cast<const char*>(&s_tab[j][0]) + toff);
-                    const uint32_t t0lo = tb.t0lo, t0hi = tb.t0hi, t1lo = tb.t1lo, t1hi = tb.t1hi, t2 = tb.t2;
-#pragma unroll
-                    for (int u = 0; u < U; u++)
-#pragma unroll
-                        for (int d = 0; d < 4; d++)
-                            acc[u][j][d] ^= gf_mul4(t0lo, t0hi, t1lo, t1hi, t2, sl[u][d].s0, sl[u][d].s1, sl[u][d].s2);
-                }
-                __builtin_amdgcn_sched_barrier(0);
-            }
-#pragma unroll
-            for (int u = 0; u < U; u++)
-#pragma unroll
-                for (int j = 0; j < R; j++) s_out[t][j][u][tid] = acc[u][j];
-        }
-        // the burst: every parked tile, one output stream after the other
-#pragma unroll
-        for (int j = 0; j < R; j++) {
-            uint8_t* ob = a.out[j] + uint64_t(stripe) * a.out_stride[j];
-#pragma unroll
-            for (int t = 0; t < T; t++) {
-                if (t >= nt) break;
-#pragma unroll
-                for (int u = 0; u < U; u++) {
-                    const uint32_t col = (scol * T + t) * TILE + u * BS + tid;
-                    if (col < chunks) store16<true>(ob + uint64_t(col) * 16u, s_out[t][j][u][tid]);
-                }
-            }
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Register double-buffered kernel (compile-time K only).  Two register sets
-// of K x U chunks: the loads of tile t+1 are issued before tile t is
-// computed, so a wave always has one tile of loads in flight during its GF
-// math (the LDS-DMA kernel's overlap without the LDS round trip).
-//  * Loads and stores address as (uniform stripe base) + 32-bit lane offset
-//    (global_* saddr form), and the next tile's coordinates are computed
-//    while the accumulators are still live, before the stores: no VGPR
-//    temporary is written after a store is issued, so the waitcnt pass never
-//    has to drain the in-flight loads to protect store data registers.
-//  * Per input, the U chunks are walked u-outer with all R coefficient
-//    tables live, so only one chunk's selectors are live at a time.
-// ---------------------------------------------------------------------------
-template <int U>
-struct PipeCoords {
-    uint32_t stripe;
-    uint32_t off[U];  // byte offset of chunk u (clamped into the cell)
-    bool live[U];
-};
-
-template <int U, int BS>
-__device__ __forceinline__ PipeCoords<U> pipe_coords(const MatmulArgs& a, uint32_t tile) {
-    PipeCoords<U> c;
-    uint32_t tcol;
-    tile_coords(tile < a.total_tiles ? tile : a.total_tiles - 1, a, c.stripe, tcol);
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-        const uint32_t col = tcol * (BS * U) + u * BS + threadIdx.x;
-        c.live[u] = tile < a.total_tiles && col < a.chunks;
-        c.off[u] = (col < a.chunks ? col : a.chunks - 1) * 16u;  // dead lanes fetch a valid chunk
-    }
-    return c;
-}
-
-template <int K, int U>
-__device__ __forceinline__ void pipe_load(const MatmulArgs& a, const PipeCoords<U>& c, u32x4 (&x)[U][K]) {
-#pragma unroll
-    for (int i = 0; i < K; i++) {
-        const uint8_t* base = a.in[i] + uint64_t(c.stripe) * a.in_stride[i];
-#pragma unroll
-        for (int u = 0; u < U; u++) x[u][i] = load16<true>(base + c.off[u]);
-    }
-}
-
-template <int K, int R, int U>
-__device__ __forceinline__ void pipe_compute(const u32x4 (&x)[U][K], const PermTable (*s_tab)[kMaxK],
-                                             u32x4 (&acc)[U][R]) {
-#pragma unroll
-    for (int u = 0; u < U; u++)
-#pragma unroll
-        for (int j = 0; j < R; j++) acc[u][j] = u32x4{0, 0, 0, 0};
-#pragma unroll
-    for (int i = 0; i < K; i++) {
-        uint32_t toff = uint32_t(i) * uint32_t(sizeof(PermTable));
-        asm volatile("" : "+v"(toff));
-#pragma unroll
-        for (int u = 0; u < U; u++)
-#pragma unroll
-            for (int j = 0; j < R; j++) asm volatile("" : "+v"(acc[u][j]) : "v"(toff));
-        uint32_t tb[R][5];
-#pragma unroll
-        for (int j = 0; j < R; j++) {
-            const PermTable& t =
-                *reinterpret_cast<const PermTable*>(reinterpret_cast<const char*>(&s_tab[j][0]) + toff);
-            tb[j][0] = t.t0lo;
-            tb[j][1] = t.t0hi;
-            tb[j][2] = t.t1lo;
-            tb[j][3] = t.t1hi;
-            tb[j][4] = t.t2;
-        }
-#pragma unroll
-        for (int u = 0; u < U; u++)
-#pragma unroll
-            for (int d = 0; d < 4; d++) {
-                const Sel s = make_sel(x[u][i][d]);
-#pragma unroll
-                for (int j = 0; j < R; j++)
-                    acc[u][j][d] ^= gf_mul4(tb[j][0], tb[j][1], tb[j][2], tb[j][3], tb[j][4], s.s0, s.s1, s.s2);
-            }
-        __builtin_amdgcn_sched_barrier(0);
-    }
-}
-
-template <int R, int U, int POL>
-__device__ __forceinline__ void pipe_store(const MatmulArgs& a, const PipeCoords<U>& c, const u32x4 (&acc)[U][R]) {
-#pragma unroll
-    for (int j = 0; j < R; j++) {
-        uint8_t* base = a.out[j] + uint64_t(c.stripe) * a.out_stride[j];
-#pragma unroll
-        for (int u = 0; u < U; u++)
-            if (c.live[u]) store16p<POL>(base + c.off[u], acc[u][j]);
-    }
-}
-
-template <int K, int R, int U, int BS, int POL = 0>
-__global__ __launch_bounds__(BS) void gf_matmul_pipe(MatmulArgs a) {
-    static_assert(K > 0, "pipelined kernel needs a compile-time input count");
-    __shared__ PermTable s_tab[R][kMaxK];
-    __shared__ uint8_t s_exp[512];
-    __shared__ uint8_t s_log[256];
-    __shared__ uint8_t s_coef[R * kMaxK];
-    prologue<R, BS>(a, K, s_tab, s_exp, s_log, s_coef);
-    const uint32_t total = a.total_tiles;
-    const uint32_t step = gridDim.x;
-    u32x4 xa[U][K], xb[U][K], acc[U][R];
-    // Tiles past the end load a clamped (valid) tile and store nothing.
-    uint32_t tile = blockIdx.x;
-    PipeCoords<U> ca = pipe_coords<U, BS>(a, tile);
-    PipeCoords<U> cb = pipe_coords<U, BS>(a, tile + step);
-    pipe_load<K, U>(a, ca, xa);
-    for (; tile < total; tile += 2 * step) {
-        pipe_load<K, U>(a, cb, xb);  // tile + step
-        __builtin_amdgcn_sched_barrier(0);
-        pipe_compute<K, R, U>(xa, s_tab, acc);
-        PipeCoords<U> cur = ca;
-        ca = pipe_coords<U, BS>(a, tile + 2 * step);
-        __builtin_amdgcn_sched_barrier(0);
-        pipe_store<R, U, POL>(a, cur, acc);
-        __builtin_amdgcn_sched_barrier(0);
-        if (tile + step >= total) break;  // wave-uniform
-        pipe_load<K, U>(a, ca, xa);  // tile + 2 step
-        __builtin_amdgcn_sched_barrier(0);
-        pipe_compute<K, R, U>(xb, s_tab, acc);
-        cur = cb;
-        cb = pipe_coords<U, BS>(a, tile + 3 * step);
-        __builtin_amdgcn_sched_barrier(0);
-        pipe_store<R, U, POL>(a, cur, acc);
-        __builtin_amdgcn_sched_barrier(0);
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Mixed-pattern decode: every stripe carries its own erasure pattern (plan
-// index), as a striped read over many block groups does.  Same register
-// kernel shape as gf_matmul_v16; per tile the block looks up the stripe's
-// plan, re-stages its header + coefficient tables into LDS when the plan
-// changes (block-uniform), and gathers the survivors by shard index.
+// Mixed-pattern decode: every stripe carries its own erasure pattern, as a
+// striped read over many block groups does (ec/mod.rs:71 decodes row by
+// row).  Same register math as gf_matmul_v16; per tile the block finds the
+// stripe's plan (header: survivor and missing shard indices; e x K
+// coefficient tables) and gathers the survivors by shard index through the
+// block's LDS copy of the shard base / stride table.
+//  RESIDENT: the per-stripe plan offsets and every plan sit in LDS for the
+//    whole launch, so a tile's metadata costs a few broadcast LDS reads and
+//    no memory round trip (a per-tile global read of the plan index used to
+//    wait behind the previous tile's stores: vmcnt is in order).
+//  otherwise: blocks walk contiguous runs of whole stripes and restage the
+//    plan into LDS once per stripe.
 // ---------------------------------------------------------------------------
 template <int K, int R, int U, int BS, bool RESIDENT>
 __global__ __launch_bounds__(BS) void gf_decode_mixed(MixedArgs a) {
     static_assert(K > 0, "compile-time k");
-    __shared__ PermTable s_tab[R][K];
+    __shared__ PermTable s_tab[RESIDENT ? 1 : R][K];  // non-resident: the current plan's rows
     __shared__ DevPlanHeader s_hdr;
-    // RESIDENT: the whole plan blob (a.blob_bytes) is copied to dynamic LDS
-    // once per block, so per-tile plan switches need no barrier.
-    extern __shared__ __attribute__((aligned(16))) uint8_t s_blob[];
-    if constexpr (RESIDENT) {
-        const uint32_t words = a.blob_bytes / 4;
-        for (uint32_t t = threadIdx.x; t < words; t += BS)
-            reinterpret_cast<uint32_t*>(s_blob)[t] = reinterpret_cast<const uint32_t*>(a.plans)[t];
-        __syncthreads();
+    __shared__ uint64_t s_base[kMaxShards], s_stride[kMaxShards], s_obase[kMaxK], s_ostride[kMaxK];
+    // RESIDENT: [stripe plan offsets: u32 x stripes, 16-B padded][plan blob]
+    extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
+    const int tid = threadIdx.x;
+    if (tid < kMaxShards) {
+        s_base[tid] = reinterpret_cast<uint64_t>(a.base[tid]);
+        s_stride[tid] = a.stride[tid];
     }
+    if (tid < kMaxK) {
+        s_obase[tid] = reinterpret_cast<uint64_t>(a.out[tid]);
+        s_ostride[tid] = a.out_stride[tid];
+    }
+    const uint32_t off_bytes = (uint32_t(a.stripes) * 4u + 15u) & ~15u;
+    if constexpr (RESIDENT) {
+        const uint32_t off_words = uint32_t(a.stripes);
+        for (uint32_t t = tid; t < off_words; t += BS) reinterpret_cast<uint32_t*>(s_dyn)[t] = a.stripe_off[t];
+        const uint32_t words = a.blob_bytes / 4;
+        for (uint32_t t = tid; t < words; t += BS)
+            reinterpret_cast<uint32_t*>(s_dyn + off_bytes)[t] = reinterpret_cast<const uint32_t*>(a.plans)[t];
+    }
+    __syncthreads();
     const uint32_t chunks = a.chunks;
     const uint32_t total = a.total_tiles;
     constexpr uint32_t TILE = BS * U;
-    uint32_t cur_plan = 0xFFFFFFFFu;
-    MatmulArgs dummy;  // tile_coords only reads tiles_per_stripe/group/stripes
-    dummy.tiles_per_stripe = a.tiles_per_stripe;
-    dummy.group = a.group;
-    dummy.stripes = a.stripes;
+    MatmulArgs order;  // tile_coords reads tiles_per_stripe / group only
+    order.tiles_per_stripe = a.tiles_per_stripe;
+    order.group = a.group;
+    order.stripes = a.stripes;
 
     // RESIDENT: grouped interleaved order (best DRAM locality).  Otherwise
     // each block walks a contiguous range of whole stripes, so its plan
-    // changes (and LDS restaging with two barriers) once per stripe, not once
-    // per tile.
+    // changes (and LDS restaging with two barriers) once per stripe.
     uint32_t t_begin = blockIdx.x, t_end = total, t_step = gridDim.x;
     if constexpr (!RESIDENT) {
         const uint32_t per = (total + gridDim.x - 1) / gridDim.x;
         t_begin = blockIdx.x * per;
         t_end = min(total, t_begin + per);
         t_step = 1;
-        dummy.group = 1;
+        order.group = 1;
     }
+    uint32_t cur_stripe = 0xFFFFFFFFu;
+    bool cur_none = true;
+    u32x4 acc[U][R];  // previous tile's store data, held through the next loads (see gf_matmul_v16)
+#pragma unroll
+    for (int u = 0; u < U; u++)
+#pragma unroll
+        for (int j = 0; j < R; j++) acc[u][j] = u32x4{0, 0, 0, 0};
     for (uint32_t tile = t_begin; tile < t_end; tile += t_step) {
         uint32_t stripe, tcol;
-        tile_coords(tile, dummy, stripe, tcol);
-        const uint32_t p = a.stripe_plan[stripe];
-        if (p == 0xFFFFu) continue;
+        tile_coords(tile, order, stripe, tcol);
         const DevPlanHeader* hdr = &s_hdr;
-        const PermTable* tab_base = &s_tab[0][0];
-        int tab_row0 = 0;  // row of tab_base[0]
+        const PermTable* tabs = &s_tab[0][0];  // row r, input i at tabs[r * K + i]
         if constexpr (RESIDENT) {
-            hdr = reinterpret_cast<const DevPlanHeader*>(s_blob + a.plan_off[p]);
-            tab_base = reinterpret_cast<const PermTable*>(s_blob + a.plan_off[p] + sizeof(DevPlanHeader));
-            tab_row0 = a.row0;
-        } else if (p != cur_plan) {  // block-uniform: every thread sees the same tile
-            __syncthreads();
-            const uint8_t* blob = a.plans + a.plan_off[p];
-            const int tid = threadIdx.x;
-            if (tid < 16) reinterpret_cast<uint32_t*>(&s_hdr)[tid] = reinterpret_cast<const uint32_t*>(blob)[tid];
-            const uint32_t e_all = reinterpret_cast<const DevPlanHeader*>(blob)->e;
-            const PermTable* tabs = reinterpret_cast<const PermTable*>(blob + sizeof(DevPlanHeader));
-            for (int t = tid; t < R * K * 8; t += BS) {
-                const int j = t / (K * 8), rem = t - j * (K * 8), i = rem / 8, w = rem - i * 8;
-                const int row = a.row0 + j;
-                reinterpret_cast<uint32_t*>(&s_tab[j][i])[w] =
-                    row < int(e_all) ? reinterpret_cast<const uint32_t*>(&tabs[row * K + i])[w] : 0u;
+            const uint32_t off = __builtin_amdgcn_readfirstlane(reinterpret_cast<const uint32_t*>(s_dyn)[stripe]);
+            if (off == kNoPlan) continue;
+            hdr = reinterpret_cast<const DevPlanHeader*>(s_dyn + off_bytes + off);
+            tabs = reinterpret_cast<const PermTable*>(s_dyn + off_bytes + off + sizeof(DevPlanHeader)) + a.row0 * K;
+        } else {
+            if (stripe != cur_stripe) {  // block-uniform
+                __syncthreads();         // every wave is done with the previous plan
+                const uint32_t off = a.stripe_off[stripe];
+                cur_none = off == kNoPlan;
+                if (!cur_none) {
+                    const uint8_t* blob = a.plans + off;
+                    if (tid < 16) reinterpret_cast<uint32_t*>(&s_hdr)[tid] = reinterpret_cast<const uint32_t*>(blob)[tid];
+                    const uint32_t e_all = reinterpret_cast<const DevPlanHeader*>(blob)->e;
+                    const PermTable* src = reinterpret_cast<const PermTable*>(blob + sizeof(DevPlanHeader));
+                    for (int t = tid; t < R * K * 8; t += BS) {
+                        const int j = t / (K * 8), rem = t - j * (K * 8), i = rem / 8, w = rem - i * 8;
+                        const int row = a.row0 + j;
+                        reinterpret_cast<uint32_t*>(&s_tab[j][i])[w] =
+                            row < int(e_all) ? reinterpret_cast<const uint32_t*>(&src[row * K + i])[w] : 0u;
+                    }
+                }
+                __syncthreads();
+                cur_stripe = stripe;
             }
-            __syncthreads();
-            cur_plan = p;
+            if (cur_none) continue;
         }
-        const int e_all = int(hdr->e);
-        const int nrows = e_all - a.row0;  // rows of this launch that exist for this plan
+        const int nrows = int(__builtin_amdgcn_readfirstlane(hdr->e)) - a.row0;  // rows of this launch in the plan
         if (nrows <= 0) continue;
         asm volatile("" ::: "memory");
 
-        u32x4 x[U][K];
         bool live[U];
-        uint64_t offs[U];
+        uint32_t offs[U];
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const uint32_t col = tcol * TILE + u * BS + threadIdx.x;
             live[u] = col < chunks;
-            offs[u] = uint64_t(live[u] ? col : 0) * 16u;
+            offs[u] = (live[u] ? col : 0u) * 16u;
+        }
+        u32x4 x[U][K];
+#pragma unroll
+        for (int i = 0; i < K; i++) {
+            const int sh = __builtin_amdgcn_readfirstlane(hdr->surv[i]);
+            const uint8_t* ib = reinterpret_cast<const uint8_t*>(s_base[sh]) + uint64_t(stripe) * s_stride[sh];
+#pragma unroll
+            for (int u = 0; u < U; u++) x[u][i] = load16<true>(ib + offs[u]);
         }
 #pragma unroll
         for (int u = 0; u < U; u++)
 #pragma unroll
-            for (int i = 0; i < K; i++) {
-                const int sh = hdr->surv[i];
-                x[u][i] = load16<true>(a.base[sh] + uint64_t(stripe) * a.stride[sh] + offs[u]);
-            }
+            for (int j = 0; j < R; j++) asm volatile("" ::"v"(acc[u][j]));
         __builtin_amdgcn_sched_barrier(0);
-        u32x4 acc[U][R];
-#pragma unroll
-        for (int u = 0; u < U; u++)
-#pragma unroll
-            for (int j = 0; j < R; j++) acc[u][j] = u32x4{0, 0, 0, 0};
 #pragma unroll
         for (int i = 0; i < K; i++) {
             uint32_t toff = uint32_t(i) * uint32_t(sizeof(PermTable));
             asm volatile("" : "+v"(toff));
+            if (i > 0) {
 #pragma unroll
-            for (int u = 0; u < U; u++)
+                for (int u = 0; u < U; u++)
 #pragma unroll
-                for (int j = 0; j < R; j++) asm volatile("" : "+v"(acc[u][j]) : "v"(toff));
+                    for (int j = 0; j < R; j++) asm volatile("" : "+v"(acc[u][j]) : "v"(toff));
+            }
             Sel sl[U][4];
 #pragma unroll
             for (int u = 0; u < U; u++)
@@ -653,28 +455,33 @@ __global__ __launch_bounds__(BS) void gf_decode_mixed(MixedArgs a) {
                 for (int d = 0; d < 4; d++) sl[u][d] = make_sel(x[u][i][d]);
 #pragma unroll
             for (int j = 0; j < R; j++) {
-                if (j >= nrows) break;  // block-uniform
-                const PermTable& t = *reinterpret_cast<const PermTable*>(
-                    reinterpret_cast<const char*>(tab_base + (tab_row0 + j) * K) + toff);
+                // rows past the plan's e read zero tables / stale rows: computed, never stored
+                const PermTable& t =
+                    *reinterpret_cast<const PermTable*>(reinterpret_cast<const char*>(tabs + j * K) + toff);
                 const uint32_t t0lo = t.t0lo, t0hi = t.t0hi, t1lo = t.t1lo, t1hi = t.t1hi, t2 = t.t2;
 #pragma unroll
                 for (int u = 0; u < U; u++)
 #pragma unroll
-                    for (int d = 0; d < 4; d++)
-                        acc[u][j][d] ^= gf_mul4(t0lo, t0hi, t1lo, t1hi, t2, sl[u][d].s0, sl[u][d].s1, sl[u][d].s2);
+                    for (int d = 0; d < 4; d++) {
+                        const uint32_t p = gf_mul4(t0lo, t0hi, t1lo, t1hi, t2, sl[u][d].s0, sl[u][d].s1, sl[u][d].s2);
+                        acc[u][j][d] = i == 0 ? p : (acc[u][j][d] ^ p);
+                    }
             }
             __builtin_amdgcn_sched_barrier(0);
         }
 #pragma unroll
-        for (int j = 0; j < R; j++) {
-            if (j >= nrows) break;
-            const int mi = hdr->miss[a.row0 + j];
-            uint8_t* ob = a.out[mi] + uint64_t(stripe) * a.out_stride[mi];
+        for (int u = 0; u < U; u++)
 #pragma unroll
-            for (int u = 0; u < U; u++) {
-                if (!live[u]) continue;
-                store16<true>(ob + offs[u], acc[u][j]);
-            }
+            for (int j = 0; j < R; j++) asm volatile("" : "+v"(acc[u][j]));
+        const bool full = (tcol + 1) * TILE <= chunks;  // block-uniform
+#pragma unroll
+        for (int j = 0; j < R; j++) {
+            if (j >= nrows) break;  // block-uniform
+            const int mi = __builtin_amdgcn_readfirstlane(hdr->miss[a.row0 + j]);
+            uint8_t* ob = reinterpret_cast<uint8_t*>(s_obase[mi]) + uint64_t(stripe) * s_ostride[mi];
+#pragma unroll
+            for (int u = 0; u < U; u++)
+                if (full || live[u]) store16<true>(ob + offs[u], acc[u][j]);
         }
     }
 }
@@ -722,34 +529,29 @@ __global__ __launch_bounds__(kBlock) void gf_matmul_bytes(MatmulArgs a) {
 // ---------------------------------------------------------------------------
 namespace {
 
-struct KernelInfo {
-    const void* fn = nullptr;
-    int blocks_per_cu = 0;
-};
-
-template <int K, int R, int U, bool NT, int BS, int MAP>
+template <int K, int R, int U, bool NT, int BS>
 const void* vec_fn() {
-    return reinterpret_cast<const void*>(&gf_matmul_v16<K, R, U, NT, BS, MAP>);
+    return reinterpret_cast<const void*>(&gf_matmul_v16<K, R, U, NT, BS>);
 }
 
-template <int R, int U, bool NT, int BS, int MAP>
+template <int R, int U, bool NT, int BS>
 const void* pick_k(int k) {
     switch (k) {
-        case 2: return vec_fn<2, R, U, NT, BS, MAP>();
-        case 3: return vec_fn<3, R, U, NT, BS, MAP>();
-        case 6: return vec_fn<6, R, U, NT, BS, MAP>();
-        case 10: return vec_fn<10, R, U, NT, BS, MAP>();
-        default: return vec_fn<0, R, U, NT, BS, MAP>();
+        case 2: return vec_fn<2, R, U, NT, BS>();
+        case 3: return vec_fn<3, R, U, NT, BS>();
+        case 6: return vec_fn<6, R, U, NT, BS>();
+        case 10: return vec_fn<10, R, U, NT, BS>();
+        default: return vec_fn<0, R, U, NT, BS>();
     }
 }
 
-template <int U, bool NT, int BS, int MAP = 0>
+template <int U, bool NT, int BS>
 const void* pick_r(int k, int r) {
     switch (r) {
-        case 1: return pick_k<1, U, NT, BS, MAP>(k);
-        case 2: return pick_k<2, U, NT, BS, MAP>(k);
-        case 3: return pick_k<3, U, NT, BS, MAP>(k);
-        default: return pick_k<4, U, NT, BS, MAP>(k);
+        case 1: return pick_k<1, U, NT, BS>(k);
+        case 2: return pick_k<2, U, NT, BS>(k);
+        case 3: return pick_k<3, U, NT, BS>(k);
+        default: return pick_k<4, U, NT, BS>(k);
     }
 }
 
@@ -757,9 +559,9 @@ const void* pick_r(int k, int r) {
 // {(1,256),(2,256),(4,256),(1,512),(2,512)}, each with and without
 // non-temporal access.
 template <bool NT>
-const void* pick_shape(int k, int r, int unroll, int bs, int map) {
+const void* pick_shape(int k, int r, int unroll, int bs) {
     if (bs == 512) return unroll >= 2 ? pick_r<2, NT, 512>(k, r) : pick_r<1, NT, 512>(k, r);
-    if (unroll == 4) return map ? pick_r<4, NT, 256, 1>(k, r) : pick_r<4, NT, 256>(k, r);
+    if (unroll == 4) return pick_r<4, NT, 256>(k, r);
     if (unroll == 2) return pick_r<2, NT, 256>(k, r);
     return pick_r<1, NT, 256>(k, r);
 }
@@ -800,103 +602,6 @@ const void* pick_dma(int k, int r, int unroll, int bs) {
     return dma_pick<2, 256>(k, r);
 }
 
-// Register double-buffered kernel: K in {2,3,6} at U in {1,2,3} (256
-// threads) and K = 10 at U in {1,2}.
-template <int K, int U>
-const void* pipe_pick_r(int r) {
-    switch (r) {
-        case 1: return reinterpret_cast<const void*>(&gf_matmul_pipe<K, 1, U, 256>);
-        case 2: return reinterpret_cast<const void*>(&gf_matmul_pipe<K, 2, U, 256>);
-        case 3: return reinterpret_cast<const void*>(&gf_matmul_pipe<K, 3, U, 256>);
-        default: return reinterpret_cast<const void*>(&gf_matmul_pipe<K, 4, U, 256>);
-    }
-}
-
-template <int U>
-const void* pipe_pick_k(int k, int r) {
-    switch (k) {
-        case 2: return pipe_pick_r<2, U>(r);
-        case 3: return pipe_pick_r<3, U>(r);
-        case 6: return pipe_pick_r<6, U>(r);
-        default: return nullptr;
-    }
-}
-
-template <int K, int R, int U>
-const void* pipe_pol(int pol) {
-    switch (pol) {
-        case 1: return reinterpret_cast<const void*>(&gf_matmul_pipe<K, R, U, 256, 1>);
-        case 2: return reinterpret_cast<const void*>(&gf_matmul_pipe<K, R, U, 256, 2>);
-        case 3: return reinterpret_cast<const void*>(&gf_matmul_pipe<K, R, U, 256, 3>);
-        default: return reinterpret_cast<const void*>(&gf_matmul_pipe<K, R, U, 256, 4>);
-    }
-}
-
-// Output-burst kernel: K in {2,3,6}, R * T <= 9 (T x R x 16 KiB of LDS).
-template <int T>
-const void* burst_pick(int k, int r) {
-    auto f = [](auto kk, auto rr) { return reinterpret_cast<const void*>(&gf_matmul_burst<kk.value, rr.value, T>); };
-    using std::integral_constant;
-    if (r > 9 / T) return nullptr;
-    switch (k) {
-        case 2: return r == 1 ? f(integral_constant<int, 2>{}, integral_constant<int, 1>{})
-                     : r == 2 ? f(integral_constant<int, 2>{}, integral_constant<int, 2>{})
-                              : f(integral_constant<int, 2>{}, integral_constant<int, (9 / T >= 3 ? 3 : 2)>{});
-        case 3: return r == 1 ? f(integral_constant<int, 3>{}, integral_constant<int, 1>{})
-                     : r == 2 ? f(integral_constant<int, 3>{}, integral_constant<int, 2>{})
-                              : f(integral_constant<int, 3>{}, integral_constant<int, (9 / T >= 3 ? 3 : 2)>{});
-        case 6: return r == 1 ? f(integral_constant<int, 6>{}, integral_constant<int, 1>{})
-                     : r == 2 ? f(integral_constant<int, 6>{}, integral_constant<int, 2>{})
-                              : f(integral_constant<int, 6>{}, integral_constant<int, (9 / T >= 3 ? 3 : 2)>{});
-        default: return nullptr;
-    }
-}
-
-const void* pick_pipe(int k, int r, int unroll) {
-    // store-policy variants only at the bench shapes (RS(6,3), RS(10,4))
-    if (g_tune_store_pol > 0 && unroll <= 2 && ((k == 6 && r == 3) || (k == 10 && r == 4))) {
-        if (k == 6) return unroll == 2 ? pipe_pol<6, 3, 2>(g_tune_store_pol) : pipe_pol<6, 3, 1>(g_tune_store_pol);
-        return unroll == 2 ? pipe_pol<10, 4, 2>(g_tune_store_pol) : pipe_pol<10, 4, 1>(g_tune_store_pol);
-    }
-    if (k == 10) return unroll >= 2 ? pipe_pick_r<10, 2>(r) : pipe_pick_r<10, 1>(r);
-    if (unroll >= 3) return pipe_pick_k<3>(k, r);
-    if (unroll == 2) return pipe_pick_k<2>(k, r);
-    return pipe_pick_k<1>(k, r);
-}
-
-int g_num_cus[64] = {0};
-
-int num_cus(int dev) {
-    if (dev < 0 || dev >= 64) return 256;
-    if (!g_num_cus[dev]) {
-        int v = 0;
-        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
-        g_num_cus[dev] = v;
-    }
-    return g_num_cus[dev];
-}
-
-}  // namespace
-
-int g_tune_unroll = 0;         // 0 = per-shape default
-int g_tune_nt = -1;            // -1 = default (non-temporal on)
-int g_tune_blocks_per_cu = 0;  // 0 = per-shape default
-int g_tune_block = 0;          // 0 = per-shape default
-int g_tune_pipeline = 0;       // 0 = per-shape default, 1 = register kernel, 2 = LDS-DMA kernel
-int g_tune_map = 0;            // 0 = default, 1 = MAP 0, 2 = MAP 1
-int g_tune_grid = 0;           // 0 = blocks_per_cu * CUs, else absolute block count
-int g_tune_group = 0;          // 0 = default (1), else stripes per tile-order group
-int g_tune_crc_unfused = 0;    // 1 = hec_encode_crc_device as two passes
-int g_tune_crc_variant = 0;    // 0 = default, 1 = slice-by-8 CRC, 2/3 = bank-replicated slice-by-1, 4/8 chains
-int g_tune_xcd_remap = 0;           // 1 = XCD-contiguous block -> tile mapping
-int g_tune_burst_tiles = 0;         // output-burst kernel: column tiles per burst (2 or 3)
-int g_tune_host_copy_threads = 0;  // 0 = default (4)
-int g_tune_store_pol = 0;      // 0 = nt stores, else store16p policy (register double-buffered kernel)
-int g_tune_crc_prefetch = 0;   // 0 = default (2), else tasks of register prefetch per wave (1 or 2)
-int g_tune_fused_slabs = 0;    // 0 = default, 4 / 8 = slabs per wave of the fused encode+CRC
-
-namespace {
-
 // Launch shape chosen from the MI355X sweeps in DESIGN.md ("Tuning"): long
 // per-wave runs (4 x 1 KiB per stream) at one 256-thread block per CU keep
 // the fewest DRAM rows open for a given bytes-in-flight.
@@ -904,15 +609,13 @@ struct Shape {
     int unroll, block, blocks_per_cu;
     bool nt;
     bool dma;
-    int map;  // chunk_col mapping (U=4, 256 threads only)
-    bool rpipe = false;  // register double-buffered kernel
 };
 
 Shape default_shape(int k, uint64_t cell_len) {
     // RS(10,4): 20 x 1 KiB loads in flight per wave already.  One 512-thread
     // block is resident per CU; a grid of 8 per CU (8 rounds) beats 2 by 3 %
     // at 256-512 stripes and ties at 2048 (profiles/r01f_probe_bpc_k10_*.log)
-    if (k > 6) return {2, 512, 8, true, false, 0};
+    if (k > 6) return {2, 512, 8, true, false};
     // RS(3,2), RS(6,3): one wave per SIMD, 4 x 1 KiB per stream per wave.
     // Small cells (many short stripes) gain 2-3 % from the LDS-DMA prefetch;
     // 1 MiB cells lose ~5 % with it (profiles/r01_probe_dma_pipeline.log).
@@ -922,13 +625,14 @@ Shape default_shape(int k, uint64_t cell_len) {
     // the resident blocks (2 per CU: -9 % at 1 MiB).
     const bool small = cell_len <= (256u << 10);
     const bool dma = small && (k == 2 || k == 3 || k == 6);
-    return {4, 256, dma ? 2 : 1, true, dma, 0};
+    return {4, 256, dma ? 2 : 1, true, dma};
 }
 
 }  // namespace
 
 int launch_gf_matmul(const MatmulArgs& in, int device, hipStream_t stream) {
     MatmulArgs a = in;
+    const Tune tn = tune_snapshot();
     bool aligned = true;
     for (int i = 0; i < a.k; i++)
         aligned &= ((reinterpret_cast<uintptr_t>(a.in[i]) | a.in_stride[i]) & 15u) == 0;
@@ -941,33 +645,14 @@ int launch_gf_matmul(const MatmulArgs& in, int device, hipStream_t stream) {
 
     if (chunks > 0) {
         Shape sh = default_shape(a.k, a.cell_len);
-        if (g_tune_unroll) sh.unroll = g_tune_unroll;
-        if (g_tune_block) sh.block = g_tune_block;
-        if (g_tune_nt >= 0) sh.nt = g_tune_nt != 0;
-        if (g_tune_blocks_per_cu) sh.blocks_per_cu = g_tune_blocks_per_cu;
-        if (g_tune_pipeline) {
-            sh.dma = g_tune_pipeline == 2;
-            sh.rpipe = g_tune_pipeline == 3;
-        }
-        if (g_tune_map) sh.map = g_tune_map - 1;
-        if (g_tune_grid) sh.blocks_per_cu = 0;
+        if (tn.unroll) sh.unroll = tn.unroll == 3 ? 2 : tn.unroll;
+        if (tn.block) sh.block = tn.block;
+        if (tn.nt >= 0) sh.nt = tn.nt != 0;
+        if (tn.blocks_per_cu) sh.blocks_per_cu = tn.blocks_per_cu;
+        if (tn.pipeline == 1 || tn.pipeline == 2) sh.dma = tn.pipeline == 2;
         if (sh.block == 512 && sh.unroll > 2) sh.unroll = 2;
         const bool dma_ok = (a.k == 2 || a.k == 3 || a.k == 6 || a.k == 10);
         if (sh.dma && !dma_ok) sh.dma = false;
-        if (sh.rpipe && !dma_ok) sh.rpipe = false;
-        // output-burst kernel (tune key 5 = 4, key 15 = T in {2, 3}): U = 4, 256 threads
-        const int burst_t = g_tune_pipeline == 4 ? (g_tune_burst_tiles == 3 ? 3 : 2) : 0;
-        const void* burst_fn = burst_t == 3 ? burst_pick<3>(a.k, a.r) : burst_t == 2 ? burst_pick<2>(a.k, a.r) : nullptr;
-        if (burst_fn) {
-            sh.dma = sh.rpipe = false;
-            sh.unroll = 4;
-            sh.block = 256;
-        }
-        if (sh.rpipe) {
-            sh.dma = false;
-            sh.block = 256;
-            sh.unroll = std::min(sh.unroll, a.k == 10 ? 2 : 3);
-        }
         if (sh.dma) {
             if (a.k == 10) {
                 sh.unroll = 2;
@@ -978,25 +663,34 @@ int launch_gf_matmul(const MatmulArgs& in, int device, hipStream_t stream) {
                 sh.unroll = 2;
             }
         }
-        const uint64_t tile = uint64_t(sh.block) * sh.unroll * (burst_fn ? burst_t : 1);  // burst: super-tiles
+        const void* fn = nullptr;
+        int tile_mult = 1;  // column tiles per scheduling unit (output-burst kernel)
+#ifdef HEC_EXPERIMENTAL
+        ExpKernel ek;
+        if (tn.pipeline >= 3 && experimental_matmul(tn, a.k, a.r, &ek)) {
+            fn = ek.fn;
+            sh.unroll = ek.unroll;
+            sh.block = ek.block;
+            if (!tn.blocks_per_cu) sh.blocks_per_cu = ek.blocks_per_cu;
+            tile_mult = ek.tile_mult;
+        }
+#endif
+        if (!fn)
+            fn = sh.dma  ? pick_dma(a.k, a.r, sh.unroll, sh.block)
+                 : sh.nt ? pick_shape<true>(a.k, a.r, sh.unroll, sh.block)
+                         : pick_shape<false>(a.k, a.r, sh.unroll, sh.block);
+        const uint64_t tile = uint64_t(sh.block) * sh.unroll * tile_mult;
         const uint64_t tps = (chunks + tile - 1) / tile;
         const uint64_t total = tps * a.stripes;
-        if (chunks > 0xFFFFFFFFull || total > 0xFFFFFFFFull) return -1;
-        if (sh.rpipe && total > 0xFFF00000ull) return -1;  // tile + 3 * grid stays in 32 bits
+        if (chunks > 0xFFFFFFFFull || total > 0xFFF00000ull) return -1;  // tile indices (+ a prefetch stride) in 32 bits
         a.chunks = uint32_t(chunks);
         a.tiles_per_stripe = uint32_t(tps);
         a.total_tiles = uint32_t(total);
         // 4 stripes column-interleaved: +1-4 % over stripe-major at 1 MiB
         // cells (profiles/r01_probe_tile_order.log)
-        a.group = g_tune_group > 0 ? uint32_t(g_tune_group) : 4u;
-        const void* fn = burst_fn ? burst_fn
-                         : sh.rpipe ? pick_pipe(a.k, a.r, sh.unroll)
-                         : sh.dma ? pick_dma(a.k, a.r, sh.unroll, sh.block)
-                                  : (sh.nt ? pick_shape<true>(a.k, a.r, sh.unroll, sh.block, sh.map)
-                                           : pick_shape<false>(a.k, a.r, sh.unroll, sh.block, sh.map));
-        uint64_t grid = g_tune_grid ? uint64_t(g_tune_grid) : uint64_t(cus) * sh.blocks_per_cu;
+        a.group = group_for(a.stripes, tn.group > 0 ? uint32_t(tn.group) : 4u);
+        uint64_t grid = tn.grid ? uint64_t(tn.grid) : uint64_t(cus) * sh.blocks_per_cu;
         if (grid > total) grid = total;
-        a.xcd_remap = (g_tune_xcd_remap && grid % 8 == 0) ? 1u : 0u;
         void* args[] = {&a};
         const hipError_t e = hipLaunchKernel(fn, dim3(uint32_t(grid)), dim3(sh.block), args, 0, stream);
         if (e != hipSuccess) return int(e);
@@ -1037,14 +731,18 @@ const void* mixed_pick_r(int r, bool res) {
     }
 }
 
-constexpr uint32_t kResidentBlobMax = 64u << 10;  // LDS budget for resident plans
+// LDS budget for a resident launch: the stripes' plan offsets plus every
+// plan (dynamic LDS up to 64 KiB needs no launch attribute)
+constexpr uint64_t kResidentMax = 64u << 10;
 
 }  // namespace
 
 int launch_decode_mixed(const MixedArgs& in, int rows, int device, hipStream_t stream) {
     MixedArgs a = in;
+    const Tune tn = tune_snapshot();
     if (a.cell_len % 16 != 0 || a.cell_len / 16 > 0xFFFFFFFFull) return -1;
-    const bool res = a.blob_bytes <= kResidentBlobMax && a.blob_bytes % 4 == 0;
+    const uint64_t dyn = ((a.stripes * 4 + 15) & ~uint64_t(15)) + a.blob_bytes;
+    const bool res = dyn <= kResidentMax && a.blob_bytes % 4 == 0;
     const void* fn = nullptr;
     switch (a.k) {
         case 2: fn = mixed_pick_r<2>(rows, res); break;
@@ -1056,7 +754,7 @@ int launch_decode_mixed(const MixedArgs& in, int rows, int device, hipStream_t s
     const int U = a.k > 6 ? 2 : 4, BS = a.k > 6 ? 512 : 256;
     // K > 6: a grid of 8 per CU (one resident): RS(10,4) mixed decode 3216-3234
     // -> 3524-3621 GiB/s against 2 per CU
-    const int bpc = g_tune_blocks_per_cu ? g_tune_blocks_per_cu : (a.k > 6 ? 8 : 1);
+    const int bpc = tn.blocks_per_cu ? tn.blocks_per_cu : (a.k > 6 ? 8 : 1);
     const uint64_t chunks = a.cell_len / 16;
     const uint64_t tile = uint64_t(BS) * U;
     const uint64_t tps = (chunks + tile - 1) / tile;
@@ -1066,11 +764,11 @@ int launch_decode_mixed(const MixedArgs& in, int rows, int device, hipStream_t s
     a.chunks = uint32_t(chunks);
     a.tiles_per_stripe = uint32_t(tps);
     a.total_tiles = uint32_t(total);
-    a.group = g_tune_group > 0 ? uint32_t(g_tune_group) : 4u;
+    a.group = group_for(a.stripes, tn.group > 0 ? uint32_t(tn.group) : 4u);
     uint64_t grid = uint64_t(num_cus(device)) * bpc;
     if (grid > total) grid = total;
     void* args[] = {&a};
-    const hipError_t e = hipLaunchKernel(fn, dim3(uint32_t(grid)), dim3(BS), args, res ? a.blob_bytes : 0, stream);
+    const hipError_t e = hipLaunchKernel(fn, dim3(uint32_t(grid)), dim3(BS), args, res ? uint32_t(dyn) : 0u, stream);
     return e == hipSuccess ? 0 : int(e);
 }
 

@@ -6,6 +6,8 @@
 
 #include <cstdint>
 
+#include "tuning.hpp"
+
 namespace hec {
 
 constexpr int kBlock = 256;  // threads per block (4 waves)
@@ -27,8 +29,7 @@ struct MatmulArgs {
     uint32_t chunks;              // vec kernel: 16-B chunks per cell
     uint32_t tiles_per_stripe;
     uint32_t total_tiles;
-    uint32_t group;               // tile order: G stripes column-interleaved (1 = stripe-major)
-    uint32_t xcd_remap;           // register kernel: 1 = the 8 XCDs' blocks take contiguous tile runs
+    uint32_t group;               // tile order: G stripes column-interleaved (1 = stripe-major); divides stripes
 };
 
 // One coefficient's v_perm_b32 product tables (see ec_kernels.hip): c*x =
@@ -49,15 +50,18 @@ struct DevPlanHeader {
 };
 static_assert(sizeof(DevPlanHeader) == 64, "plan header is 64 B");
 
+constexpr uint32_t kNoPlan = 0xFFFFFFFFu;  // stripe with no missing data shard
+
+// Workspace (device): [per-stripe plan offset: u32 x stripes][plan blob];
+// plan = DevPlanHeader + e x k PermTables (row r, input i at r*k + i).
 struct MixedArgs {
     const uint8_t* base[kMaxShards];  // all k+m shard bases
     uint64_t stride[kMaxShards];
     uint8_t* out[kMaxK];              // reconstructed data shard i -> out[i]
     uint64_t out_stride[kMaxK];
-    const uint8_t* plans;             // blob: plan p at plans + plan_off[p]
-    uint32_t blob_bytes;              // size of the blob (LDS-resident when <= 64 KiB)
-    const uint32_t* plan_off;
-    const uint16_t* stripe_plan;      // per stripe; 0xFFFF = nothing missing
+    const uint8_t* plans;             // blob: plan of stripe s at plans + stripe_off[s]
+    const uint32_t* stripe_off;       // per stripe; kNoPlan = nothing missing
+    uint32_t blob_bytes;              // size of the blob
     int32_t k;
     int32_t row0;                     // first missing row handled by this launch
     uint64_t cell_len;
@@ -74,22 +78,15 @@ int launch_decode_mixed(const MixedArgs& a, int rows, int device, hipStream_t st
 // success, -1 invalid sizes, otherwise the (positive) hipError_t.
 int launch_gf_matmul(const MatmulArgs& a, int device, hipStream_t stream);
 
-// Tuning knobs (set through hec_tune_set).
-extern int g_tune_unroll;         // 0 = default, else 1|2|4
-extern int g_tune_nt;             // -1 = default, else 0|1
-extern int g_tune_blocks_per_cu;  // 0 = default
-extern int g_tune_block;          // 0 = default, else 256|512
-extern int g_tune_pipeline;       // 0 = default, 1 = register kernel, 2 = LDS-DMA kernel
-extern int g_tune_map;            // 0 = default, 1|2 = chunk mapping 0|1
-extern int g_tune_grid;           // 0 = default, else absolute grid size
-extern int g_tune_group;          // 0 = default, else stripes per tile-order group
-extern int g_tune_crc_unfused;    // 1 = encode + separate CRC pass
-extern int g_tune_crc_variant;    // 0 = default, 1 = slice-by-8, 2/3 = bank-replicated slice-by-1, 4/8 chains
-extern int g_tune_crc_prefetch;   // 0 = default, 1 / 2 tasks of register prefetch (CRC kernel)
-extern int g_tune_fused_slabs;    // 0 = default, else 4 / 8 slabs per wave (fused encode+CRC)
-extern int g_tune_xcd_remap;           // 1 = XCD-contiguous block -> tile mapping (register kernel)
-extern int g_tune_burst_tiles;          // output-burst kernel (key 5 = 4): tiles per burst, 2 or 3
-extern int g_tune_host_copy_threads;  // 0 = default (4): hec_decode_host_batch's host copy threads
-extern int g_tune_store_pol;      // 0 = nt stores, 1..4 = sc1 | sc0 sc1 | nt sc1 | plain (pipelined kernel)
+#ifdef HEC_EXPERIMENTAL
+// Rejected variants (ec_experimental.hip), selected by tune key 5 in {3, 4,
+// 5}: register pipe kernel, output bursts, register double buffering.
+struct ExpKernel {
+    const void* fn;
+    int unroll, block, blocks_per_cu;
+    int tile_mult;  // column tiles per scheduling unit (bursts)
+};
+bool experimental_matmul(const Tune& t, int k, int r, ExpKernel* out);
+#endif
 
 }  // namespace hec

@@ -84,14 +84,24 @@ __device__ __forceinline__ void tile_coords(uint32_t tile, const MatmulArgs& a, 
         tcol = tile - stripe * tps;
         return;
     }
+    // the launchers pick G dividing the stripe count (group_for), so there is
+    // no short last group and G is the only divisor: loop-invariant, its
+    // reciprocal is hoisted out of the tile loop (a per-tile divisor made hipcc
+    // rebuild one with VALU float ops in the loop, whose temporaries landed in
+    // in-flight store registers and forced store drains)
     const uint32_t per_group = G * tps;
     const uint32_t g = tile / per_group;
     const uint32_t r = tile - g * per_group;
-    const uint32_t first = g * G;
-    const uint32_t rem = uint32_t(a.stripes) - first;
-    const uint32_t gs = rem < G ? rem : G;  // last group may be short
-    tcol = r / gs;
-    stripe = first + (r - tcol * gs);
+    tcol = r / G;
+    stripe = g * G + (r - tcol * G);
+}
+
+// Tile-order group for a batch: the largest of want, .., 2, 1 that divides
+// the stripe count (tile_coords assumes whole groups).
+__host__ __device__ inline uint32_t group_for(uint64_t stripes, uint32_t want) {
+    for (uint32_t g = want; g > 1; g--)
+        if (stripes % g == 0) return g;
+    return 1;
 }
 
 __device__ __forceinline__ Sel make_sel(uint32_t x) {
@@ -116,26 +126,6 @@ __device__ __forceinline__ void store16(uint8_t* p, u32x4 v) {
         __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
     else
         *reinterpret_cast<u32x4*>(p) = v;
-}
-
-// Store cache policy (measurement knob, tune key 13): 0 = nt (default),
-// 1 = sc1, 2 = sc0 sc1, 3 = nt sc1, 4 = plain.  nt / plain keep the written
-// line in the XCD's L2 until it is evicted; sc1 drops it (MI355X_MICROARCH
-// "stores of each flavour").  The asm forms are invisible to the waitcnt
-// pass: later compiler waits on loads only over-wait (older stores retire
-// first), and the s_nop covers the >8-byte store-data VALU-write hazard.
-template <int POL>
-__device__ __forceinline__ void store16p(uint8_t* p, u32x4 v) {
-    if constexpr (POL == 0)
-        __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
-    else if constexpr (POL == 4)
-        *reinterpret_cast<u32x4*>(p) = v;
-    else if constexpr (POL == 1)
-        asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
-    else if constexpr (POL == 2)
-        asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
-    else
-        asm volatile("global_store_dwordx4 %0, %1, off sc1 nt\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
 }
 
 // Stage log/antilog + coefficient rows in LDS, build the perm tables.

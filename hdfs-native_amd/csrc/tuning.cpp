@@ -1,0 +1,89 @@
+// tuning.cpp -- hec_tune_set's knobs as atomics, and the CU-count cache
+// (see tuning.hpp).
+#include "tuning.hpp"
+
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+
+#include "../../include/hdfs_ec_amd.h"
+
+namespace hec {
+
+namespace {
+
+constexpr int kKeys = 16;
+std::atomic<int> g_knob[kKeys + 1];  // index = key; zero-initialised (static storage)
+std::atomic<int> g_nt{-1};           // key 2 defaults to -1 (non-temporal on)
+
+constexpr bool kExperimental =
+#ifdef HEC_EXPERIMENTAL
+    true;
+#else
+    false;
+#endif
+
+int load(int key) { return g_knob[key].load(std::memory_order_relaxed); }
+
+std::atomic<int> g_cus[64];
+
+}  // namespace
+
+Tune tune_snapshot() {
+    Tune t;
+    t.unroll = load(1);
+    t.nt = g_nt.load(std::memory_order_relaxed);
+    t.blocks_per_cu = load(3);
+    t.block = load(4);
+    t.pipeline = load(5);
+    t.grid = load(7);
+    t.group = load(8);
+    t.crc_unfused = load(9);
+    t.fused_slabs = load(10);
+    t.crc_variant = load(11);
+    t.crc_prefetch = load(12);
+    t.store_pol = load(13);
+    t.host_copy_threads = load(14);
+    t.burst_tiles = load(15);
+    return t;
+}
+
+int tune_store(int key, int value) {
+    bool ok = false;
+    switch (key) {
+        case 1: ok = value == 0 || value == 1 || value == 2 || value == 4 || (kExperimental && value == 3); break;
+        case 2:
+            g_nt.store(value < 0 ? -1 : (value ? 1 : 0), std::memory_order_relaxed);
+            return HEC_OK;
+        case 3: ok = value >= 0 && value <= 16; break;
+        case 4: ok = value == 0 || value == 256 || value == 512; break;
+        case 5: ok = (value >= 0 && value <= 2) || (kExperimental && value >= 3 && value <= 5); break;
+        case 7: ok = value >= 0 && value <= 65536; break;
+        case 8: ok = value >= 0 && value <= 65536; break;
+        case 9: value = value ? 1 : 0; ok = true; break;
+        case 10: ok = value == 0 || value == 4 || value == 8; break;
+        case 11:
+            ok = value == 0 || value == 1 || value == 5 ||
+                 (kExperimental && (value == 2 || value == 3 || value == 4 || value == 9));
+            break;
+        case 12: ok = value >= 0 && value <= 2; break;
+        case 13: ok = kExperimental && value >= 0 && value <= 4; break;
+        case 14: ok = value >= 0 && value <= 64; break;
+        case 15: ok = kExperimental && (value == 0 || value == 2 || value == 3); break;
+        default: ok = false;
+    }
+    if (!ok) return HEC_ERR_INVALID_ARG;
+    g_knob[key].store(value, std::memory_order_relaxed);
+    return HEC_OK;
+}
+
+int num_cus(int dev) {
+    if (dev < 0 || dev >= 64) return 256;
+    int v = g_cus[dev].load(std::memory_order_relaxed);
+    if (v > 0) return v;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+    g_cus[dev].store(v, std::memory_order_relaxed);  // every racing writer stores the same value
+    return v;
+}
+
+}  // namespace hec

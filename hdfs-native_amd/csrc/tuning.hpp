@@ -1,0 +1,41 @@
+// tuning.hpp -- launch-shape knobs for measurement (hec_tune_set) and the
+// per-device CU count cache.  Host code only.
+//
+// The knobs are process-wide std::atomic<int>s; every launcher reads one
+// consistent snapshot (relaxed loads) at its start, so a concurrent
+// hec_tune_set never races with a launch -- it affects launches that start
+// after it.  Variants that were measured and rejected (register double
+// buffering, output bursts, store cache policies, bank-replicated and
+// memory-only CRC schemes) exist only in the HEC_EXPERIMENTAL build
+// (lib/libhdfs_ec_amd_exp.so); the default library rejects their keys.
+#pragma once
+
+namespace hec {
+
+struct Tune {
+    int unroll;             // key 1: 16-B chunks per lane (0 = per-shape default)
+    int nt;                 // key 2: non-temporal loads/stores (-1 = default on)
+    int blocks_per_cu;      // key 3: grid = blocks_per_cu x CUs (0 = default)
+    int block;              // key 4: threads per block (0 = default)
+    int pipeline;           // key 5: 0 default, 1 register, 2 LDS-DMA (exp: 3 pipe, 4 burst, 5 double-buffered)
+    int grid;               // key 7: absolute grid size (0 = default)
+    int group;              // key 8: stripes per tile-order group (0 = default 4)
+    int crc_unfused;        // key 9: 1 = hec_encode_crc_device as encode + checksum passes
+    int fused_slabs;        // key 10: fused encode+CRC slabs per wave (0, 4, 8)
+    int crc_variant;        // key 11: 0 default, 1 slicing-by-8, 5 11-bit (exp: 2, 3, 4, 9)
+    int crc_prefetch;       // key 12: CRC kernel register prefetch depth (0 = 2, 1, 2)
+    int store_pol;          // key 13 (exp): store cache policy of the pipe kernel
+    int host_copy_threads;  // key 14: hec_decode_host_batch host copy threads (0 = 4)
+    int burst_tiles;        // key 15 (exp): tiles per output burst (2, 3)
+};
+
+// One consistent view of every knob (relaxed atomic loads).
+Tune tune_snapshot();
+
+// Validates and stores one knob; returns an HEC_* status.
+int tune_store(int key, int value);
+
+// Multiprocessor count of a device (cached per device, thread-safe).
+int num_cus(int device);
+
+}  // namespace hec

@@ -47,6 +47,7 @@ EXPORTS = [
     "hec_crc32c_device", "hec_encode_crc_device", "hec_checksum_device", "hec_checksum_verify_device",
     "hec_decode_verify_device", "hec_group_create", "hec_group_destroy", "hec_group_size", "hec_group_coder",
     "hec_group_range", "hec_group_encode_host_batch", "hec_group_decode_host_batch",
+    "hec_device_alloc", "hec_device_free",
 ]
 
 
@@ -87,13 +88,16 @@ def _share_torch_hip_runtime() -> None:
         import torch  # noqa: F401
 
 
-def _load() -> ctypes.CDLL:
+EXP_LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libhdfs_ec_amd_exp.so")
+
+
+def _load(path: str = LIB_PATH) -> ctypes.CDLL:
     _share_torch_hip_runtime()
-    if not os.path.exists(LIB_PATH):
+    if not os.path.exists(path):
         raise ImportError(
-            f"{LIB_PATH} not built: run `make -C hdfs-native_amd` (or __graft_entry__.build()). "
+            f"{path} not built: run `make -C hdfs-native_amd` (or __graft_entry__.build()). "
             "There is no CPU fallback.")
-    lib = ctypes.CDLL(LIB_PATH)
+    lib = ctypes.CDLL(path)
     P, S, I = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
     PP = ctypes.POINTER(ctypes.c_void_p)
     SP = ctypes.POINTER(ctypes.c_size_t)
@@ -132,6 +136,8 @@ def _load() -> ctypes.CDLL:
         "hec_group_range": ([P, S, S, SP, SP], I),
         "hec_group_encode_host_batch": ([P, P, P, S, S, S], I),
         "hec_group_decode_host_batch": ([P, PP, S, S, P, S], I),
+        "hec_device_alloc": ([I, S, ctypes.c_uint, ctypes.POINTER(P)], I),
+        "hec_device_free": ([I, P], I),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)
@@ -141,6 +147,18 @@ def _load() -> ctypes.CDLL:
 
 
 lib = _load()
+_exp_lib = None
+
+
+def experimental_lib() -> ctypes.CDLL:
+    """The HEC_EXPERIMENTAL build (lib/libhdfs_ec_amd_exp.so: the default
+    kernels plus the measured-and-rejected variants, selected by tune keys).
+    Pass it as Coder(..., lib=experimental_lib()); its knobs are its own
+    (set them with tune_set(..., lib=experimental_lib()))."""
+    global _exp_lib
+    if _exp_lib is None:
+        _exp_lib = _load(EXP_LIB_PATH)
+    return _exp_lib
 
 
 def strerror(rc: int) -> str:
@@ -198,8 +216,38 @@ def decode_plan(data_units: int, parity_units: int, present: Sequence[bool]):
     return list(surv) if e else [], list(miss[:e]), [list(mat[r * k:(r + 1) * k]) for r in range(e)]
 
 
-def tune_set(key: int, value: int) -> None:
-    _check(lib.hec_tune_set(key, value))
+ALLOC_DEFAULT = 0
+ALLOC_CONTIGUOUS = 1
+
+
+class DeviceBuffer:
+    """HBM from hec_device_alloc (optionally physically contiguous), exposed
+    to torch through __cuda_array_interface__: `torch.as_tensor(buf,
+    device=...)` views it without a copy.  Freed by close()."""
+
+    def __init__(self, nbytes: int, device: int = 0, flags: int = ALLOC_DEFAULT):
+        p = ctypes.c_void_p()
+        _check(lib.hec_device_alloc(device, nbytes, flags, ctypes.byref(p)))
+        self.ptr, self.nbytes, self.device = p.value, nbytes, device
+
+    @property
+    def __cuda_array_interface__(self):
+        return {"shape": (self.nbytes,), "typestr": "|u1", "data": (self.ptr, False), "version": 2}
+
+    def close(self) -> None:
+        if self.ptr:
+            _check(lib.hec_device_free(self.device, ctypes.c_void_p(self.ptr)))
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def tune_set(key: int, value: int, lib_=None) -> None:
+    _check((lib_ or lib).hec_tune_set(key, value))
 
 
 def _addr(buf) -> int:
@@ -216,9 +264,10 @@ def _addr(buf) -> int:
 class Coder:
     """Drop-in for hdfs_native::ec::gf256::Coder on one MI355X."""
 
-    def __init__(self, data_units: int, parity_units: int, device: int = 0, codec: str = "rs"):
+    def __init__(self, data_units: int, parity_units: int, device: int = 0, codec: str = "rs", lib=None):
+        self._lib = lib or globals()["lib"]
         h = ctypes.c_void_p()
-        _check(lib.hec_coder_create_codec(codec.encode(), data_units, parity_units, device, ctypes.byref(h)))
+        _check(self._lib.hec_coder_create_codec(codec.encode(), data_units, parity_units, device, ctypes.byref(h)))
         self.codec = codec
         self._h = h
         self.data_units = data_units
@@ -227,7 +276,7 @@ class Coder:
 
     def close(self) -> None:
         if getattr(self, "_h", None):
-            lib.hec_coder_destroy(self._h)
+            self._lib.hec_coder_destroy(self._h)
             self._h = None
 
     def __del__(self):
@@ -252,7 +301,7 @@ class Coder:
         ins = [np.ascontiguousarray(np.frombuffer(bytes(d) if not isinstance(d, np.ndarray) else d,
                                                   dtype=np.uint8)) for d in data]
         outs = [np.empty(n, dtype=np.uint8) for _ in range(self.parity_units)]
-        _check(lib.hec_encode(self._h, _pp([a.ctypes.data for a in ins]), n,
+        _check(self._lib.hec_encode(self._h, _pp([a.ctypes.data for a in ins]), n,
                               _pp([a.ctypes.data for a in outs])))
         return [o.tobytes() for o in outs]
 
@@ -269,7 +318,7 @@ class Coder:
         ins = [None if d is None else np.ascontiguousarray(np.frombuffer(bytes(d), dtype=np.uint8))
                for d in data]
         outs = [np.empty(n, dtype=np.uint8) if (i < k and data[i] is None) else None for i in range(k + m)]
-        _check(lib.hec_decode(self._h, _pp([0 if a is None else a.ctypes.data for a in ins]), n,
+        _check(self._lib.hec_decode(self._h, _pp([0 if a is None else a.ctypes.data for a in ins]), n,
                               _pp([0 if a is None else a.ctypes.data for a in outs])))
         for i in range(k):
             if data[i] is None:
@@ -278,27 +327,27 @@ class Coder:
     # -- device-resident batched API ----------------------------------------
     def encode_device(self, data_ptrs, data_strides, parity_ptrs, parity_strides, cell_len, stripes,
                       stream: int = 0) -> None:
-        _check(lib.hec_encode_device(self._h, _pp(data_ptrs), _sp(data_strides), _pp(parity_ptrs),
+        _check(self._lib.hec_encode_device(self._h, _pp(data_ptrs), _sp(data_strides), _pp(parity_ptrs),
                                      _sp(parity_strides), cell_len, stripes, ctypes.c_void_p(stream)))
 
     def decode_device(self, shard_ptrs, shard_strides, out_ptrs, out_strides, cell_len, stripes,
                       stream: int = 0) -> None:
-        _check(lib.hec_decode_device(self._h, _pp([p or 0 for p in shard_ptrs]), _sp(shard_strides),
+        _check(self._lib.hec_decode_device(self._h, _pp([p or 0 for p in shard_ptrs]), _sp(shard_strides),
                                      _pp([p or 0 for p in out_ptrs]), _sp(out_strides), cell_len, stripes,
                                      ctypes.c_void_p(stream)))
 
     def crc32c_device(self, ptrs, strides, cell_len, stripes, bytes_per_checksum, out_ptr, stream: int = 0):
-        _check(lib.hec_crc32c_device(self._h, _pp(ptrs), _sp(strides), len(ptrs), cell_len, stripes,
+        _check(self._lib.hec_crc32c_device(self._h, _pp(ptrs), _sp(strides), len(ptrs), cell_len, stripes,
                                      bytes_per_checksum, ctypes.c_void_p(out_ptr), ctypes.c_void_p(stream)))
 
     def checksum_device(self, checksum_type: int, ptrs, strides, cell_len, stripes, bytes_per_checksum, out_ptr,
                         stream: int = 0):
-        _check(lib.hec_checksum_device(self._h, checksum_type, _pp(ptrs), _sp(strides), len(ptrs), cell_len, stripes,
+        _check(self._lib.hec_checksum_device(self._h, checksum_type, _pp(ptrs), _sp(strides), len(ptrs), cell_len, stripes,
                                        bytes_per_checksum, ctypes.c_void_p(out_ptr), ctypes.c_void_p(stream)))
 
     def checksum_verify_device(self, checksum_type: int, ptrs, strides, cell_len, stripes, bytes_per_checksum,
                                expected_ptr, bad_ptr, stream: int = 0):
-        _check(lib.hec_checksum_verify_device(self._h, checksum_type, _pp(ptrs), _sp(strides), len(ptrs), cell_len,
+        _check(self._lib.hec_checksum_verify_device(self._h, checksum_type, _pp(ptrs), _sp(strides), len(ptrs), cell_len,
                                               stripes, bytes_per_checksum, ctypes.c_void_p(expected_ptr),
                                               ctypes.c_void_p(bad_ptr), ctypes.c_void_p(stream)))
 
@@ -307,24 +356,24 @@ class Coder:
         """Verified striped read (hec_decode_verify_device): raises
         ErasureCodingError when a stripe has fewer than k cells that verify
         (the bad flags are written either way)."""
-        _check(lib.hec_decode_verify_device(self._h, checksum_type, _pp(shard_ptrs), _sp(shard_strides),
+        _check(self._lib.hec_decode_verify_device(self._h, checksum_type, _pp(shard_ptrs), _sp(shard_strides),
                                             _pp(out_ptrs), _sp(out_strides), cell_len, stripes, bytes_per_checksum,
                                             ctypes.c_void_p(sums_ptr), ctypes.c_void_p(bad_ptr),
                                             ctypes.c_void_p(stream)))
 
     def encode_crc_device(self, data_ptrs, data_strides, parity_ptrs, parity_strides, cell_len, stripes,
                           bytes_per_checksum, sums_ptr, stream: int = 0):
-        _check(lib.hec_encode_crc_device(self._h, _pp(data_ptrs), _sp(data_strides), _pp(parity_ptrs),
+        _check(self._lib.hec_encode_crc_device(self._h, _pp(data_ptrs), _sp(data_strides), _pp(parity_ptrs),
                                          _sp(parity_strides), cell_len, stripes, bytes_per_checksum,
                                          ctypes.c_void_p(sums_ptr), ctypes.c_void_p(stream)))
 
     def decode_mixed_workspace_size(self, stripes: int) -> int:
-        return lib.hec_decode_mixed_workspace_size(self._h, stripes)
+        return self._lib.hec_decode_mixed_workspace_size(self._h, stripes)
 
     def decode_device_mixed(self, shard_ptrs, shard_strides, out_ptrs, out_strides, present_masks, cell_len,
                             stripes, workspace_ptr, workspace_bytes, stream: int = 0) -> None:
         masks = (ctypes.c_uint64 * stripes)(*present_masks)
-        _check(lib.hec_decode_device_mixed(self._h, _pp(shard_ptrs), _sp(shard_strides), _pp(out_ptrs),
+        _check(self._lib.hec_decode_device_mixed(self._h, _pp(shard_ptrs), _sp(shard_strides), _pp(out_ptrs),
                                            _sp(out_strides), masks, cell_len, stripes,
                                            ctypes.c_void_p(workspace_ptr), workspace_bytes,
                                            ctypes.c_void_p(stream)))
@@ -333,18 +382,18 @@ class Coder:
                          stripes, stream: int = 0) -> None:
         rows, cols = len(matrix), len(matrix[0])
         mat = (ctypes.c_uint8 * (rows * cols))(*[v for r in matrix for v in r])
-        _check(lib.hec_gf_matmul_device(self._h, mat, rows, cols, _pp(in_ptrs), _sp(in_strides), _pp(out_ptrs),
+        _check(self._lib.hec_gf_matmul_device(self._h, mat, rows, cols, _pp(in_ptrs), _sp(in_strides), _pp(out_ptrs),
                                         _sp(out_strides), cell_len, stripes, ctypes.c_void_p(stream)))
 
     def decode_host_batch(self, vertical_addrs, cell_len: int, rows: int, h_file_addr: int, chunk_rows: int) -> None:
         """vertical_addrs[k+m]: host addresses of the per-shard vertical
         buffers (0/None = missing) -> file-order bytes at h_file_addr."""
-        _check(lib.hec_decode_host_batch(self._h, _pp([a or 0 for a in vertical_addrs]), cell_len, rows,
+        _check(self._lib.hec_decode_host_batch(self._h, _pp([a or 0 for a in vertical_addrs]), cell_len, rows,
                                          ctypes.c_void_p(h_file_addr), chunk_rows))
 
     def encode_host_batch(self, h_data_addr: int, h_parity_addr: int, cell_len: int, stripes: int,
                           chunk_stripes: int) -> None:
-        _check(lib.hec_encode_host_batch(self._h, ctypes.c_void_p(h_data_addr), ctypes.c_void_p(h_parity_addr),
+        _check(self._lib.hec_encode_host_batch(self._h, ctypes.c_void_p(h_data_addr), ctypes.c_void_p(h_parity_addr),
                                          cell_len, stripes, chunk_stripes))
 
 
@@ -469,6 +518,7 @@ class _Borrowed(Coder):
     """A group slot's coder: the group owns (and destroys) the handle."""
 
     def __init__(self, handle, k, m, device, codec):  # noqa: D107 (no super().__init__: no new coder)
+        self._lib = lib
         self._h = handle
         self.codec, self.data_units, self.parity_units, self.device = codec, k, m, device
 

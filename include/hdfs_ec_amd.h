@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define HEC_ABI_VERSION 2
+#define HEC_ABI_VERSION 3
 
 /* Status codes */
 #define HEC_OK 0
@@ -291,6 +291,17 @@ int hec_group_encode_host_batch(hec_group_t *group, const uint8_t *h_data, uint8
  * part of every vertical buffer) into its rows of h_file. */
 int hec_group_decode_host_batch(hec_group_t *group, const uint8_t *const *h_vertical, size_t cell_len,
                                 size_t rows, uint8_t *h_file, size_t chunk_rows);
+
+/* ---- HBM buffers for the batched API ------------------------------------ *
+ * Device memory for stripe batches on `device` (hipExtMallocWithFlags).
+ * HEC_ALLOC_CONTIGUOUS asks for physically contiguous HBM, which the GPU
+ * maps with large page fragments: a batch of tens of GiB then needs far
+ * fewer translation entries.  hec_device_free releases it
+ * (synchronous, like hipFree). */
+#define HEC_ALLOC_DEFAULT 0
+#define HEC_ALLOC_CONTIGUOUS 1
+int hec_device_alloc(int device, size_t bytes, unsigned flags, void **out);
+int hec_device_free(int device, void *ptr);
 
 /* ---- Measurement knobs (not part of the reference interface) ---------- *
  * key 1: 16-B column chunks per lane per tile (1, 2, 3 or 4; 0 = default)

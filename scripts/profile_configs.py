@@ -1,0 +1,155 @@
+"""Per-config roofline evidence in ONE lease (GPU box), for every BASELINE
+config: the bench line, the rocprofv3 kernel trace of that same process, and
+FETCH_SIZE / WRITE_SIZE in two separate --pmc passes of the same command.
+
+For each config the summary records
+  * the bench JSON line printed by the profiled process itself (so its
+    ms_per_step and the trace come from the same run),
+  * the engine kernel's average duration over the timed region (the last
+    launches_per_step x steps dispatches of the trace) and over all launches,
+  * launches x average <= ms_per_step (the profile explains the line),
+  * frac recomputed from the trace = algorithmic bytes / avg / 8 TB/s,
+  * HBM traffic per launch from the PMC passes, corrected per
+    MI355X_MICROARCH.md §HBM (FETCH_SIZE KiB x1024 x2 on gfx950 16-B/lane
+    streaming reads; WRITE_SIZE KiB x1024).
+
+usage: python3 scripts/profile_configs.py OUTDIR [config ...]
+Every GPU step runs under its own `timeout -k 10`; the first failure ends
+the script (no GPU step after a failed one).
+"""
+import csv
+import glob
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PEAK = 8.0e12
+COMMON = ["--steps", "10", "--warmup", "3", "--spinup", "0.3", "--cpu-seconds", "0", "--host-path", "0"]
+# name -> (bench args, k, m, cell, stripes, launches per step)
+CONFIGS = {
+    "rs32": (["--k", "3", "--m", "2", "--stripes", "1024"], 3, 2, 1 << 20, 1024, 2),
+    "rs63": ([], 6, 3, 1 << 20, 1024, 2),
+    "rs63enc": (["--encode-only"], 6, 3, 1 << 20, 1024, 1),
+    "rs104": (["--k", "10", "--m", "4", "--global-stripes", "2048"], 10, 4, 1 << 20, 2048, 2),
+    "rs104x256": (["--k", "10", "--m", "4", "--stripes", "256"], 10, 4, 1 << 20, 256, 2),
+    "c64k": (["--cell", "65536", "--stripes", "65536"], 6, 3, 65536, 65536, 2),
+}
+KERNEL_RE = "gf_matmul"
+
+
+def run(cmd, log, limit):
+    with open(log, "w") as f:
+        rc = subprocess.call(["timeout", "-k", "10", str(limit)] + cmd, stdout=f, stderr=subprocess.STDOUT,
+                             cwd=ROOT)
+    if rc != 0:
+        sys.stdout.write(open(log).read()[-3000:])
+        raise SystemExit(f"step failed rc={rc}: {' '.join(cmd)}")
+
+
+def rows(d, pattern):
+    out = []
+    for path in sorted(glob.glob(os.path.join(d, "**", pattern), recursive=True)):
+        with open(path) as f:
+            out.extend(csv.DictReader(f))
+    return out
+
+
+def bench_line(log):
+    for line in reversed(open(log).read().splitlines()):
+        if line.startswith("{") and '"metric"' in line:
+            return json.loads(line)
+    raise SystemExit(f"no bench line in {log}")
+
+
+def counter(d, name):
+    vals = [float(r["Counter_Value"]) for r in rows(d, "*counter_collection.csv")
+            if KERNEL_RE in r.get("Kernel_Name", "") and r.get("Counter_Name") == name]
+    if not vals:
+        raise SystemExit(f"no {name} rows under {d}")
+    return vals
+
+
+def profile(out, name):
+    args, k, m, cell, stripes, lps = CONFIGS[name]
+    d = os.path.join(out, name)
+    os.makedirs(d, exist_ok=True)
+    bench = ["python3", "bench.py"] + args + COMMON
+    prof = ["rocprofv3", "--kernel-trace", "--stats", "-d", os.path.join(d, "trace"), "-o", "run",
+            "--output-format", "csv", "--"]
+    run(prof + bench, os.path.join(d, "bench_trace.log"), 400)
+    line = bench_line(os.path.join(d, "bench_trace.log"))
+    for cnt in ("FETCH_SIZE", "WRITE_SIZE"):
+        pmc = ["rocprofv3", "--pmc", cnt, "--kernel-include-regex", KERNEL_RE, "-d",
+               os.path.join(d, cnt.lower()), "-o", "run", "--output-format", "csv", "--"]
+        run(pmc + bench, os.path.join(d, f"bench_{cnt.lower()}.log"), 400)
+
+    trace = [r for r in rows(os.path.join(d, "trace"), "*kernel_trace.csv") if KERNEL_RE in r.get("Kernel_Name", "")]
+    trace.sort(key=lambda r: int(r["Start_Timestamp"]))
+    durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9 for r in trace]
+    steps = line["steps"]
+    timed = durs[-lps * steps:]
+    avg_timed = sum(timed) / len(timed)
+    avg_all = sum(durs) / len(durs)
+    stats = [r for r in rows(os.path.join(d, "trace"), "*kernel_stats.csv") if KERNEL_RE in r["Name"]]
+    algo = (k + m) * cell * stripes  # per launch: k cells read + r = m written (uniform decode: e = m)
+    fetch = counter(os.path.join(d, "fetch_size"), "FETCH_SIZE")
+    write = counter(os.path.join(d, "write_size"), "WRITE_SIZE")
+    fetch_b = 2.0 * 1024 * sum(fetch) / len(fetch)
+    write_b = 1024.0 * sum(write) / len(write)
+    res = {
+        "config": name, "args": " ".join(args + COMMON),
+        "k": k, "m": m, "cell": cell, "stripes": stripes, "launches_per_step": lps,
+        "kernel": sorted({r["Name"] for r in stats}),
+        "dispatches": len(durs),
+        "avg_launch_ms_timed_region": round(avg_timed * 1e3, 4),
+        "avg_launch_ms_all": round(avg_all * 1e3, 4),
+        "stats_avg_ms": [round(float(r["AverageNs"]) * 1e-6, 4) for r in stats],
+        "ms_per_step": line["ms_per_step"],
+        "kernel_ms_per_step": round(lps * avg_timed * 1e3, 4),
+        "kernel_within_step": lps * avg_timed * 1e3 <= line["ms_per_step"],
+        "algorithmic_bytes_per_launch": algo,
+        "frac_from_trace": round(algo / avg_timed / PEAK, 4),
+        "frac_bench_line": line["roofline"]["frac"],
+        "fetch_bytes_per_launch": fetch_b, "write_bytes_per_launch": write_b,
+        "hbm_bytes_per_launch": fetch_b + write_b,
+        "traffic_over_algorithmic": round((fetch_b + write_b) / algo, 5),
+        "pmc_dispatches": {"fetch": len(fetch), "write": len(write)},
+        "corrections": "FETCH_SIZE KiB x1024 x2 (gfx950 half-count on 16B/lane streaming reads); WRITE_SIZE KiB x1024",
+        "bench_line": line,
+    }
+    with open(os.path.join(out, "summary.jsonl"), "a") as f:
+        f.write(json.dumps(res) + "\n")
+    print(f"{name}: line {line['value']} GiB/s ms/step {line['ms_per_step']} | kernel {avg_timed * 1e3:.4f} ms x{lps} "
+          f"= {lps * avg_timed * 1e3:.4f} | frac trace {res['frac_from_trace']} line {res['frac_bench_line']} | "
+          f"traffic x{res['traffic_over_algorithmic']}", flush=True)
+
+
+def write_traffic(out, tag):
+    """pmc_traffic_configs.json: what bench.py reads for roofline.traffic
+    (matched on k, m, cell, stripes and decode mode)."""
+    rows = [json.loads(ln) for ln in open(os.path.join(out, "summary.jsonl"))]
+    cfgs = [{"config": r["config"], "k": r["k"], "m": r["m"], "cell": r["cell"], "stripes": r["stripes"],
+             "decode_mode": "uniform", "kernel": r["kernel"],
+             "fetch_bytes_per_launch": r["fetch_bytes_per_launch"], "write_bytes_per_launch": r["write_bytes_per_launch"],
+             "hbm_bytes_per_launch": r["hbm_bytes_per_launch"],
+             "algorithmic_bytes_per_launch": r["algorithmic_bytes_per_launch"],
+             "traffic_over_algorithmic": r["traffic_over_algorithmic"]} for r in rows]
+    with open(os.path.join(out, "pmc_traffic_configs.json"), "w") as f:
+        json.dump({"tag": tag, "corrections": rows[0]["corrections"] if rows else None, "configs": cfgs}, f, indent=1)
+
+
+def main():
+    out = sys.argv[1]
+    names = sys.argv[2:] or list(CONFIGS)
+    os.makedirs(out, exist_ok=True)
+    os.environ["TMPDIR"] = "/tmp"
+    for n in names:
+        profile(out, n)
+    write_traffic(out, os.path.basename(os.path.normpath(out)))
+    print("profile_configs ok", flush=True)
+
+
+if __name__ == "__main__":
+    main()

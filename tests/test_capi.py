@@ -32,7 +32,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version_and_strerror():
-    assert H.lib.hec_abi_version() == 2
+    assert H.lib.hec_abi_version() == 3
     assert "Not enough valid shards" in H.strerror(H.HEC_ERR_NOT_ENOUGH_SHARDS)
     assert H.strerror(H.HEC_ERR_CHECKSUM) == "checksum error"
     assert H.strerror(12345) == "unknown status"
@@ -145,3 +145,12 @@ def test_host_paths_under_address_sanitizer(tmp_path):
                        text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     assert "bad=0" in r.stdout
+
+
+def test_tune_set_validates_without_device():
+    # knobs are host-side atomics: no device needed; removed and
+    # experimental-only keys are rejected by the default library
+    assert H.lib.hec_tune_set(3, 2) == H.HEC_OK
+    assert H.lib.hec_tune_set(3, 0) == H.HEC_OK
+    for key, value in [(5, 3), (5, 4), (5, 5), (6, 1), (13, 1), (15, 2), (16, 1), (11, 2), (11, 9), (3, 99), (0, 0)]:
+        assert H.lib.hec_tune_set(key, value) == H.HEC_ERR_INVALID_ARG, (key, value)

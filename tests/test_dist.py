@@ -87,3 +87,28 @@ def test_gloo_sharded_encode_matches_single_process(tmp_path, world):
         assert first == len(got)
         got.extend(digests)
     assert got == want
+
+
+@pytest.mark.parametrize("args,want_S,want_global,scaling", [
+    (["--k", "10", "--m", "4", "--global-stripes", "2048"], 1024, 2048, "strong"),
+    (["--stripes", "1024"], 1024, 2048, "weak"),
+    (["--global-stripes", "7"], 4, 7, "strong"),
+])
+def test_bench_gpus_flag_spawns_ranks(args, want_S, want_global, scaling):
+    """`bench.py --gpus 2` run directly (no launcher WORLD_SIZE) starts two
+    ranks itself through torch.distributed.run, which rendezvous over
+    loopback, reduce, and print ONE JSON line with n_gpus = 2 (dry run: gloo,
+    no GPU, no engine -- the launcher/rank/reduction plumbing only)."""
+    import subprocess
+    from conftest import ROOT
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "gloo",
+                          "--dry-run"] + args, capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["dry_run"] and d["scaling"] == scaling
+    assert d["config"]["global_stripes"] == want_global
+    assert d["config"]["stripes_summed_over_ranks"] == want_global
+    assert d["config"]["stripes_per_gpu"] == want_S  # rank 0's share

@@ -138,9 +138,8 @@ def test_device_decode_batch_all_data_patterns(dev, c_oracle, k, m):
     par = oracle_batch_encode(c_oracle, k, m, data)
     d = torch.from_numpy(data).to(dev)
     p = torch.from_numpy(par).to(dev)
+    # every data-loss pattern (385 for RS(10,4))
     pats = [c for e in range(1, m + 1) for c in itertools.combinations(range(k), e)]
-    if len(pats) > 60:
-        pats = pats[:30] + pats[-30:]
     for miss in pats:
         out = torch.zeros_like(d)
         H.decode_batch(coder(k, m), d, p, miss, out)
@@ -219,9 +218,8 @@ def test_gf_matmul_device_arbitrary_matrix(dev):
 
 @pytest.mark.parametrize("knob", [((1, 1),), ((1, 2),), ((1, 4),), ((2, 0),), ((3, 2),), ((4, 512), (1, 1)),
                                   ((4, 512), (1, 2)), ((1, 4), (2, 0), (3, 3)), ((5, 2),), ((5, 2), (1, 2)),
-                                  ((5, 2), (4, 512)), ((5, 2), (3, 2)), ((5, 1),), ((6, 2),), ((6, 2), (7, 100)),
-                                  ((7, 3),), ((8, 2),), ((8, 3),), ((8, 4), (5, 2)), ((8, 64),), ((16, 1),),
-                                  ((16, 1), (7, 16)), ((16, 1), (7, 12))])
+                                  ((5, 2), (4, 512)), ((5, 2), (3, 2)), ((5, 1),), ((7, 100),), ((7, 3),), ((8, 2),),
+                                  ((8, 3),), ((8, 4), (5, 2)), ((8, 64),), ((7, 16),), ((7, 12),)])
 def test_tuning_variants_bit_identical(dev, c_oracle, knob):
     k, m, S, cell = 6, 3, 5, 8192 + 16
     data = batch_data(S, k, cell, first=21)
@@ -241,124 +239,89 @@ def test_tuning_variants_bit_identical(dev, c_oracle, knob):
         H.tune_set(3, 0)
         H.tune_set(4, 0)
         H.tune_set(5, 0)
-        H.tune_set(6, 0)
         H.tune_set(7, 0)
         H.tune_set(8, 0)
-        H.tune_set(16, 0)
     assert np.array_equal(p.cpu().numpy(), want)
     for i in (0, 2, 4):
         assert torch.equal(out[:, i], d[:, i])
 
 
-@pytest.mark.parametrize("pipeline", [1, 2, 3])
+@pytest.mark.parametrize("pipeline", [1, 2])
 @pytest.mark.parametrize("k,m", [(2, 1), (3, 2), (6, 3), (10, 4)])
 @pytest.mark.parametrize("cell", [4096, 4096 + 16, 3 * 65536 + 48])
-def test_pipelines_vs_oracle(dev, c_oracle, pipeline, k, m, cell):
-    # register kernel and LDS-DMA kernel, full and partial tiles
-    S = 3
+@pytest.mark.parametrize("S", [3, 6])
+def test_pipelines_vs_oracle(dev, c_oracle, pipeline, k, m, cell, S):
+    # register kernel and LDS-DMA kernel, full and partial tiles; S = 3 and 6
+    # stripes: tile-order groups of 3 and of 2 (groups divide the batch)
     data = batch_data(S, k, cell, first=cell + k)
     want = oracle_batch_encode(c_oracle, k, m, data)
     d = torch.from_numpy(data).to(dev)
     p = torch.zeros((S, m, cell), dtype=torch.uint8, device=dev)
     try:
-        if pipeline == 3:  # register kernel, wave-contiguous chunk mapping
-            H.tune_set(5, 1)
-            H.tune_set(6, 2)
-        else:
-            H.tune_set(5, pipeline)
+        H.tune_set(5, pipeline)
         H.encode_batch(coder(k, m), d, p)
         out = torch.zeros_like(d)
         H.decode_batch(coder(k, m), d, p, list(range(m)), out)
         torch.cuda.synchronize()
     finally:
         H.tune_set(5, 0)
-        H.tune_set(6, 0)
     assert np.array_equal(p.cpu().numpy(), want)
     assert torch.equal(out[:, :m], d[:, :m])
 
 
-@pytest.mark.parametrize("unroll", [1, 2, 3])
-@pytest.mark.parametrize("grid", [0, 1, 5, 6])
-@pytest.mark.parametrize("k,m", [(2, 1), (3, 2), (6, 3), (10, 4)])
-def test_register_double_buffer_vs_oracle(dev, c_oracle, unroll, grid, k, m):
-    # tune key 5 = 3: register double-buffered kernel.  Small grids walk many
-    # tiles per block (both register sets, odd and even tile counts, the
-    # clamped past-the-end prefetch); the cell leaves a partial last tile.
-    S, cell = 3, 3 * 65536 + 48
-    data = batch_data(S, k, cell, first=cell + 7 * k + unroll)
+def test_tune_set_concurrent_with_launches(dev, c_oracle):
+    # hec_tune_set while other threads launch: the knobs are atomics read once
+    # per launch, and every value toggled here is result-neutral
+    import threading
+    k, m, S, cell = 6, 3, 4, 65536 + 16
+    data = batch_data(S, k, cell, first=5)
     want = oracle_batch_encode(c_oracle, k, m, data)
-    d = torch.from_numpy(data).to(dev)
-    p = torch.zeros((S, m, cell), dtype=torch.uint8, device=dev)
-    try:
-        H.tune_set(5, 3)
-        H.tune_set(1, unroll)
-        H.tune_set(7, grid)
-        H.encode_batch(coder(k, m), d, p)
-        out = torch.zeros_like(d)
-        H.decode_batch(coder(k, m), d, p, list(range(m)), out)
-        torch.cuda.synchronize()
-    finally:
-        H.tune_set(5, 0)
-        H.tune_set(1, 0)
-        H.tune_set(7, 0)
-    assert np.array_equal(p.cpu().numpy(), want)
-    assert torch.equal(out[:, :m], d[:, :m])
+    stop = threading.Event()
+    errors = []
+
+    def toggler():
+        i = 0
+        while not stop.is_set():
+            H.tune_set(3, 1 + i % 2)
+            H.tune_set(8, 1 + 3 * (i % 2))
+            H.tune_set(7, (i % 3) * 64)
+            i += 1
+
+    def launcher(seed):
+        try:
+            cod = H.Coder(k, m, 0)
+            st = torch.cuda.Stream(dev)
+            d = torch.from_numpy(data).to(dev)
+            for _ in range(40):
+                p = torch.zeros((S, m, cell), dtype=torch.uint8, device=dev)
+                with torch.cuda.stream(st):
+                    H.encode_batch(cod, d, p, st)
+                st.synchronize()
+                if not np.array_equal(p.cpu().numpy(), want):
+                    errors.append(seed)
+            cod.close()
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(repr(e))
+
+    t = threading.Thread(target=toggler)
+    ls = [threading.Thread(target=launcher, args=(i,)) for i in range(4)]
+    t.start()
+    for th in ls:
+        th.start()
+    for th in ls:
+        th.join()
+    stop.set()
+    t.join()
+    for key in (3, 7, 8):
+        H.tune_set(key, 0)
+    assert not errors, errors
 
 
-@pytest.mark.parametrize("tiles", [2, 3])
-@pytest.mark.parametrize("grid", [0, 1, 5])
-@pytest.mark.parametrize("k,m", [(2, 1), (3, 2), (6, 3)])
-def test_output_burst_vs_oracle(dev, c_oracle, tiles, grid, k, m):
-    # tune key 5 = 4: outputs parked in LDS, stored in bursts of `tiles`
-    # column tiles; partial super-tiles at the cell end, many per block
-    S, cell = 3, 3 * 65536 + 48
-    data = batch_data(S, k, cell, first=cell + 11 * k + tiles)
-    want = oracle_batch_encode(c_oracle, k, m, data)
-    d = torch.from_numpy(data).to(dev)
-    p = torch.zeros((S, m, cell), dtype=torch.uint8, device=dev)
-    try:
-        H.tune_set(5, 4)
-        H.tune_set(15, tiles)
-        H.tune_set(7, grid)
-        H.encode_batch(coder(k, m), d, p)
-        out = torch.zeros_like(d)
-        H.decode_batch(coder(k, m), d, p, list(range(m)), out)
-        torch.cuda.synchronize()
-    finally:
-        H.tune_set(5, 0)
-        H.tune_set(15, 0)
-        H.tune_set(7, 0)
-    assert np.array_equal(p.cpu().numpy(), want)
-    assert torch.equal(out[:, :m], d[:, :m])
-
-
-@pytest.mark.parametrize("pol", [1, 2, 3, 4])
-@pytest.mark.parametrize("unroll", [1, 2])
-@pytest.mark.parametrize("k,m", [(6, 3), (10, 4)])
-def test_store_policies_vs_oracle(dev, c_oracle, pol, unroll, k, m):
-    # tune key 13: cache policy of the double-buffered kernel's stores
-    # (sc1 / sc0 sc1 / nt sc1 / plain, inline-asm stores) at the bench shapes
-    S, cell = 5, 65536 + 32
-    data = batch_data(S, k, cell, first=pol * 31 + unroll)
-    want = oracle_batch_encode(c_oracle, k, m, data)
-    d = torch.from_numpy(data).to(dev)
-    p = torch.zeros((S, m, cell), dtype=torch.uint8, device=dev)
-    try:
-        H.tune_set(5, 3)
-        H.tune_set(1, unroll)
-        H.tune_set(13, pol)
-        H.tune_set(7, 7)
-        H.encode_batch(coder(k, m), d, p)
-        out = torch.zeros_like(d)
-        H.decode_batch(coder(k, m), d, p, list(range(m)), out)
-        torch.cuda.synchronize()
-    finally:
-        H.tune_set(5, 0)
-        H.tune_set(1, 0)
-        H.tune_set(13, 0)
-        H.tune_set(7, 0)
-    assert np.array_equal(p.cpu().numpy(), want)
-    assert torch.equal(out[:, :m], d[:, :m])
+def test_experimental_keys_rejected_by_default_library():
+    # the rejected variants exist only in lib/libhdfs_ec_amd_exp.so
+    for key, value in [(5, 3), (5, 4), (5, 5), (13, 1), (15, 2), (11, 2), (11, 9), (6, 1), (16, 1)]:
+        with pytest.raises(ValueError):
+            H.tune_set(key, value)
 
 
 @pytest.mark.parametrize("S,chunk,cell", [(9, 4, 65536), (23, 2, 65536), (7, 7, 4096 + 16), (5, 1, 1000)])
@@ -600,10 +563,10 @@ def _oracle_sums(cells: np.ndarray, bpc: int) -> np.ndarray:
 
 @pytest.mark.parametrize("cell,bpc,n", [(512 * 64, 512, 3), (512 * 70 + 256, 512, 2), (1 << 16, 512, 9),
                                         (4096, 4096, 2), (1000, 512, 3), (3 * 512 + 16, 512, 1), (2048, 100, 2)])
-@pytest.mark.parametrize("variant,pf", [(0, 0), (1, 1), (2, 2), (3, 1), (3, 2), (4, 0), (5, 1), (5, 2)])
+@pytest.mark.parametrize("variant,pf", [(0, 0), (0, 1), (1, 1), (1, 2), (5, 1), (5, 2)])
 def test_crc32c_device_vs_oracle(dev, cell, bpc, n, variant, pf):
-    """All CRC lookup schemes (tune key 11) and prefetch depths (key 12)
-    against the oracle."""
+    """The default library's CRC lookup schemes (tune key 11: 11-bit slicing,
+    slicing-by-8) and prefetch depths (key 12) against the oracle."""
     S = 3
     cells = batch_data(S, n, cell, first=cell + bpc)
     H.tune_set(11, variant)
@@ -629,10 +592,8 @@ def test_crc32c_device_published_vector(dev):
     ("rs", 10, 4, 1 << 15, 3), ("rs", 10, 4, 70 * 512 + 256, 2), ("rs", 3, 2, 1 << 17, 3),
     ("rs", 2, 1, 8192 + 512, 4), ("rs", 12, 4, 1 << 14, 2), ("rs", 6, 3, 1000, 2), ("xor", 2, 1, 1 << 14, 3)])
 @pytest.mark.parametrize("fused", [0, 4, 8, None])
-@pytest.mark.parametrize("scheme", [0, 2])
-def test_encode_crc_device(dev, c_oracle, codec, k, m, cell, S, fused, scheme):
-    """Fused encode+CRC (k in {2,3,6,10}; slice-by-8 default or, tune key 11
-    = 2, bank-replicated CRC tables) and the two-pass fallback (other k,
+def test_encode_crc_device(dev, c_oracle, codec, k, m, cell, S, fused, scheme=0):
+    """Fused encode+CRC (k in {2,3,6,10}) and the two-pass fallback (other k,
     unaligned cell_len, or tune key 9) against oracle parity + oracle CRCs."""
     bpc = 512
     data = batch_data(S, k, cell, first=31 + cell)
@@ -705,7 +666,7 @@ def _oracle_checksums(cells: np.ndarray, bpc: int, ctype: int) -> np.ndarray:
 @pytest.mark.parametrize("ctype", CKSUM_TYPES)
 @pytest.mark.parametrize("cell,bpc,n", [(512 * 64, 512, 3), (512 * 70 + 256, 512, 2), (1000, 512, 3),
                                         (4096, 4096, 2), (2048, 100, 2)])
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("variant", [0, 1, 5])
 def test_checksum_device_vs_oracle(dev, ctype, cell, bpc, n, variant):
     S = 3
     cells = batch_data(S, n, cell, first=cell + bpc + ctype)
