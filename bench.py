@@ -325,7 +325,7 @@ def ref_cases(args):
                                                "note": "6x6 Gauss-Jordan over GF(2^8), host code (incl. a 36-B copy)"}
 
     # rs-encode/encode: one stripe, the bench's big-endian counter fill
-    data = bench_counter_shards(k, slice_)
+    data = list(bench_counter_shards(k, slice_))
     d = torch.from_numpy(np.stack(data)).unsqueeze(0).to(dev)
     p = torch.empty((1, m, slice_), dtype=torch.uint8, device=dev)
     t_dev = timeit(lambda: H.encode_batch(coder, d, p), 50, torch.cuda.synchronize)
@@ -731,37 +731,49 @@ def crc_leg(args, H, coder, data, parity, rec, dp, ds, pp, ps, rp, rs, shard_ptr
                      f"{{{','.join(map(str, miss))}}} are rebuilt (ReadPacket::get_data + ec_decode); "
                      "wall time of the synchronous call incl. the flag read-back",
     })
-    # corrupt survivors: a fraction of the stripes gets one flipped byte in
-    # the first survivor (shard m: a data shard, repaired in place from the
-    # remaining cells); the call re-plans those stripes (phase 2)
+    # corrupt survivors: data shard 0 unavailable (one spare shard beyond k),
+    # and a fraction of the stripes gets one flipped byte in its first
+    # survivor (data shard 1).  The call re-plans those stripes (phase 2):
+    # shard 1 is dropped, the next parity shard read and verified, shards 0
+    # and 1 rebuilt -- shard 1 in place over its corrupt cell.
     corrupt = {}
-    victim = surv[0]
-    vbase = data if victim < k else parity
-    vidx = victim if victim < k else victim - k
+    c_ptrs = [None] + [dp[i] for i in range(1, k)] + pp
+    c_out = [rp[0]] + [dp[i] for i in range(1, k)]
+    c_ost = [rs[0]] + [ds[i] for i in range(1, k)]
+
+    def dec_verify_c():
+        coder.decode_verify_device(H.CHECKSUM_CRC32C, c_ptrs, ds + ps, c_out, c_ost, cell, S, bpc, sums.data_ptr(),
+                                   bad.data_ptr(), sp)
+
+    dec_verify_c()
+    torch.cuda.synchronize(dev)
+    t_0 = time.perf_counter()
+    for _ in range(reps):
+        dec_verify_c()
+    torch.cuda.synchronize(dev)
+    corrupt["0"] = {"stripes_corrupt": 0, "ms": round((time.perf_counter() - t_0) / reps * 1e3, 3)}
+    corrupt["0"]["GiBps"] = round(k * cell * S / (corrupt["0"]["ms"] * 1e-3) / GIB, 2)
     for frac in [float(x) for x in filter(None, args.corrupt.split(","))]:
         n_bad = max(1, int(round(frac * S)))
         idx = torch.linspace(0, S - 1, n_bad, device=dev).long().unique()
-        orig = vbase[idx, vidx, 7].clone()
-
-        def corrupt_and_run():
-            vbase[idx, vidx, 7] ^= 0x5A
-            t_0 = time.perf_counter()
-            dec_verify()
-            torch.cuda.synchronize(dev)
-            t = time.perf_counter() - t_0
-            return t
-
+        orig = data[idx, 1, 7].clone()
         ts = []
         for _ in range(3):
-            ts.append(corrupt_and_run())
-            assert torch.equal(vbase[idx, vidx, 7], orig), "in-place repair failed"
-            flagged = bad[:, victim].nonzero().flatten()
-            assert torch.equal(flagged, idx), "wrong cells flagged"
-        assert torch.equal(rec, data[:, :m]), "decode+verify with corrupt survivors mismatch"
+            data[idx, 1, 7] ^= 0x5A
+            torch.cuda.synchronize(dev)
+            t_0 = time.perf_counter()
+            dec_verify_c()
+            torch.cuda.synchronize(dev)
+            ts.append(time.perf_counter() - t_0)
+            assert torch.equal(data[idx, 1, 7], orig), "in-place repair failed"
+            assert torch.equal(bad[:, 1].nonzero().flatten(), idx), "wrong cells flagged"
+        assert torch.equal(rec[:, 0], data[:, 0]), "decode+verify with corrupt survivors mismatch"
         t = min(ts)
         corrupt[f"{frac:g}"] = {"stripes_corrupt": int(idx.numel()), "ms": round(t * 1e3, 3),
                                 "GiBps": round(k * cell * S / t / GIB, 2)}
     res["decode_verify_corrupt"] = corrupt
+    res["corrupt_note"] = ("data shard 0 unavailable, a fraction of stripes with a corrupt data shard 1 "
+                           "(re-planned, repaired in place); key = fraction of stripes")
     dec_verify()  # leave clean flags behind
     torch.cuda.synchronize(dev)
     return res

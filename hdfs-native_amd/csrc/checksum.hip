@@ -70,8 +70,9 @@ __device__ __forceinline__ const crc::Tables<KIND>& tables() {
 __device__ __forceinline__ void emit_sum(const CrcArgs& a, uint64_t cell_idx, uint64_t chunk, uint32_t crc) {
     uint64_t cell = cell_idx;
     if (a.mapped) {  // launch cells are a subset of the sums layout
-        const uint64_t stripe = cell_idx / a.n_shards;
-        cell = stripe * a.n_total + a.sid[cell_idx - stripe * a.n_shards];
+        const uint64_t s = cell_idx / a.n_shards;
+        const uint64_t stripe = a.stripe_list ? a.stripe_list[s] : s;
+        cell = stripe * a.n_total + a.sid[cell_idx - s * a.n_shards];
     }
     const uint64_t at = cell * a.chunks_per_cell + chunk;
     if (a.expected) {
@@ -90,8 +91,9 @@ __device__ __forceinline__ void emit_sum(const CrcArgs& a, uint64_t cell_idx, ui
 __device__ __forceinline__ void load_task(const CrcArgs& a, uint64_t groups, uint64_t task, int lane, u32x4 (&v)[8]) {
     const uint64_t cell_idx = task / groups;
     const uint64_t g = task - cell_idx * groups;
-    const uint64_t stripe = cell_idx / a.n_shards;
-    const uint32_t shard = uint32_t(cell_idx - stripe * a.n_shards);
+    const uint64_t s = cell_idx / a.n_shards;
+    const uint32_t shard = uint32_t(cell_idx - s * a.n_shards);
+    const uint64_t stripe = a.stripe_list ? a.stripe_list[s] : s;
     const uint8_t* base = a.base[shard] + stripe * a.stride[shard] + g * 16u * 512u;
     const uint64_t left = a.cell_len - g * 16u * 512u;
 #pragma unroll
@@ -200,8 +202,9 @@ __global__ __launch_bounds__(kCrcBlock) void checksum_chunks_bytes(CrcArgs a) {
          gidx += uint64_t(gridDim.x) * kCrcBlock) {
         const uint64_t cell_idx = gidx / a.chunks_per_cell;
         const uint64_t chunk = gidx - cell_idx * a.chunks_per_cell;
-        const uint64_t stripe = cell_idx / a.n_shards;
-        const uint32_t shard = uint32_t(cell_idx - stripe * a.n_shards);
+        const uint64_t s = cell_idx / a.n_shards;
+        const uint32_t shard = uint32_t(cell_idx - s * a.n_shards);
+        const uint64_t stripe = a.stripe_list ? a.stripe_list[s] : s;
         const uint8_t* p = a.base[shard] + stripe * a.stride[shard] + chunk * a.bytes_per_checksum;
         const uint64_t cs = chunk * a.bytes_per_checksum;
         const uint64_t len = a.cell_len - cs < a.bytes_per_checksum ? a.cell_len - cs : a.bytes_per_checksum;
@@ -241,7 +244,7 @@ int launch_checksum(const CrcArgs& in, int device, hipStream_t stream) {
     // sums are read / written as u32 by every path (fast and byte kernels)
     if ((reinterpret_cast<uintptr_t>(a.out) | reinterpret_cast<uintptr_t>(a.expected)) & 3u) return -1;
     if (a.n_shards > uint32_t(kCrcMaxShards) || a.n_total < a.n_shards) return -1;
-    a.mapped = a.n_total != a.n_shards;
+    a.mapped = a.n_total != a.n_shards || a.stripe_list != nullptr;
     for (uint32_t i = 0; i < a.n_shards; i++) {
         if (a.sid[i] >= a.n_total) return -1;
         a.mapped |= a.sid[i] != i;

@@ -19,6 +19,9 @@ struct CrcArgs {
     // bad[cell] = 1 on any mismatch in that cell (ReadPacket::get_data,
     // connection.rs:477-504); out unused.
     uint8_t sid[kCrcMaxShards];
+    // optional: launch stripe s is batch stripe stripe_list[s] (addresses,
+    // sums and flags); null = identity.  `stripes` counts the list.
+    const uint32_t* stripe_list;
     uint32_t n_total;
     uint32_t mapped;  // filled by the launcher: sid is not the identity
     uint8_t* out;

@@ -96,6 +96,18 @@ struct hec_coder {
     hipEvent_t ev_in[kSlots] = {}, ev_k[kSlots] = {}, ev_out[kSlots] = {};
     uint8_t* dbuf = nullptr;
     size_t dbuf_bytes = 0;
+    // hec_encode / hec_decode (one row per call, pageable caller buffers):
+    // a persistent pinned bounce buffer and device slots of their own, grown
+    // geometrically and released only by hec_coder_destroy
+    static constexpr int kCallEvents = HEC_MAX_DATA_UNITS;
+    uint8_t* call_host = nullptr;  // hipHostMalloc'd
+    uint8_t* call_dev = nullptr;
+    size_t call_bytes = 0;
+    hipEvent_t ev_call[kCallEvents] = {};
+    // verified read, phase 2: stripe lists + mixed-decode workspace (device),
+    // grown geometrically, released by hec_coder_destroy
+    uint8_t* verify_ws = nullptr;
+    size_t verify_ws_bytes = 0;
 };
 
 namespace {
@@ -211,6 +223,70 @@ struct StreamDrain {
     }
 };
 
+// Grows the per-call staging (pinned host + device) to `bytes`, doubling so
+// that a stream of growing rows reallocates O(log) times; never shrinks.
+int ensure_call_staging(hec_coder* c, size_t bytes) {
+    if (c->call_bytes >= bytes) return HEC_OK;
+    const size_t want = std::max(bytes, c->call_bytes * 2);
+    if (c->call_host) (void)hipHostFree(c->call_host);
+    if (c->call_dev) (void)hipFree(c->call_dev);
+    c->call_host = c->call_dev = nullptr;
+    c->call_bytes = 0;
+    HEC_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->call_host), want, hipHostMallocDefault), HEC_ERR_NO_MEMORY);
+    HEC_HIP(hipMalloc(&c->call_dev, want), HEC_ERR_NO_MEMORY);
+    c->call_bytes = want;
+    return HEC_OK;
+}
+
+// One row through the device, pageable caller buffers in and out:
+//   out[j] = sum_i mat[j*nin + i] * in[i], n bytes each.
+// Inputs are copied into the pinned bounce buffer shard by shard, each
+// shard's H2D DMA issued as soon as it is there (the next memcpy overlaps
+// it); outputs come back D2H shard by shard and each is copied out while the
+// next one is still in flight.  No allocation on the hot path.
+int call_through_device(hec_coder* c, const uint8_t* const* in, size_t nin, uint8_t* const* out, size_t nout,
+                        const uint8_t* mat, size_t n) {
+    const size_t pitch = (n + 255) & ~size_t(255);
+    int rc = ensure_call_staging(c, pitch * (nin + nout));
+    if (rc != HEC_OK) return rc;
+    StreamDrain drain{c};  // never return with a DMA still touching the bounce buffer
+    const uint8_t* din[HEC_MAX_DATA_UNITS];
+    uint8_t* dout[HEC_MAX_DATA_UNITS];
+    size_t strides[HEC_MAX_DATA_UNITS];
+    const bool piecewise = n >= (size_t(64) << 10);  // below that one DMA each way beats per-shard calls
+    for (size_t i = 0; i < nin; i++) {
+        std::memcpy(c->call_host + i * pitch, in[i], n);
+        din[i] = c->call_dev + i * pitch;
+        strides[i] = pitch;
+        if (piecewise)
+            HEC_HIP(hipMemcpyAsync(c->call_dev + i * pitch, c->call_host + i * pitch, n, hipMemcpyHostToDevice,
+                                   c->stream),
+                    HEC_ERR_DEVICE);
+    }
+    if (!piecewise)
+        HEC_HIP(hipMemcpyAsync(c->call_dev, c->call_host, pitch * (nin - 1) + n, hipMemcpyHostToDevice, c->stream),
+                HEC_ERR_DEVICE);
+    for (size_t j = 0; j < nout; j++) dout[j] = c->call_dev + (nin + j) * pitch;
+    rc = matmul_batch(c->device, mat, nout, nin, din, strides, dout, strides, n, 1, c->stream);
+    if (rc != HEC_OK) return rc;
+    uint8_t* hout = c->call_host + nin * pitch;
+    if (!piecewise) {
+        HEC_HIP(hipMemcpyAsync(hout, dout[0], pitch * (nout - 1) + n, hipMemcpyDeviceToHost, c->stream), HEC_ERR_DEVICE);
+        HEC_HIP(hipStreamSynchronize(c->stream), HEC_ERR_DEVICE);
+        for (size_t j = 0; j < nout; j++) std::memcpy(out[j], hout + j * pitch, n);
+        return HEC_OK;
+    }
+    for (size_t j = 0; j < nout; j++) {
+        HEC_HIP(hipMemcpyAsync(hout + j * pitch, dout[j], n, hipMemcpyDeviceToHost, c->stream), HEC_ERR_DEVICE);
+        HEC_HIP(hipEventRecord(c->ev_call[j], c->stream), HEC_ERR_DEVICE);
+    }
+    for (size_t j = 0; j < nout; j++) {
+        HEC_HIP(hipEventSynchronize(c->ev_call[j]), HEC_ERR_DEVICE);
+        std::memcpy(out[j], hout + j * pitch, n);
+    }
+    return HEC_OK;
+}
+
 int ensure_dbuf(hec_coder* c, size_t bytes) {
     if (c->dbuf_bytes >= bytes) return HEC_OK;
     if (c->dbuf) (void)hipFree(c->dbuf);
@@ -309,6 +385,8 @@ int hec_coder_create_codec(const char* codec, size_t data_units, size_t parity_u
             HEC_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), HEC_ERR_DEVICE);
             for (int i = 0; i < 2; i++)
                 HEC_HIP(hipStreamCreateWithFlags(&c->copy_stream[i], hipStreamNonBlocking), HEC_ERR_DEVICE);
+            for (int i = 0; i < hec_coder::kCallEvents; i++)
+                HEC_HIP(hipEventCreateWithFlags(&c->ev_call[i], hipEventDisableTiming), HEC_ERR_DEVICE);
             for (int i = 0; i < hec_coder::kSlots; i++) {
                 HEC_HIP(hipEventCreateWithFlags(&c->ev_in[i], hipEventDisableTiming), HEC_ERR_DEVICE);
                 HEC_HIP(hipEventCreateWithFlags(&c->ev_k[i], hipEventDisableTiming), HEC_ERR_DEVICE);
@@ -337,6 +415,11 @@ void hec_coder_destroy(hec_coder_t* c) {
         for (auto s : c->copy_stream)
             if (s) (void)hipStreamSynchronize(s);
         if (c->dbuf) (void)hipFree(c->dbuf);
+        if (c->call_dev) (void)hipFree(c->call_dev);
+        if (c->call_host) (void)hipHostFree(c->call_host);
+        if (c->verify_ws) (void)hipFree(c->verify_ws);
+        for (hipEvent_t e : c->ev_call)
+            if (e) (void)hipEventDestroy(e);
         for (int i = 0; i < hec_coder::kSlots; i++)
             for (hipEvent_t e : {c->ev_in[i], c->ev_k[i], c->ev_out[i]})
                 if (e) (void)hipEventDestroy(e);
@@ -413,25 +496,7 @@ int hec_encode(hec_coder_t* c, const uint8_t* const* data, size_t shard_len, uin
         std::lock_guard<std::mutex> lk(c->host_mu);
         DeviceGuard g(c->device);
         if (!g.ok) return fail(HEC_ERR_DEVICE, "hipSetDevice", hipErrorInvalidDevice);
-        const size_t pitch = (shard_len + 255) & ~size_t(255);
-        int rc = ensure_dbuf(c, pitch * (c->k + c->m));
-        if (rc != HEC_OK) return rc;
-        const uint8_t* din[HEC_MAX_DATA_UNITS];
-        uint8_t* dout[HEC_MAX_PARITY_UNITS];
-        size_t strides[HEC_MAX_DATA_UNITS + HEC_MAX_PARITY_UNITS];
-        for (size_t i = 0; i < c->k + c->m; i++) strides[i] = pitch;
-        for (size_t i = 0; i < c->k; i++) {
-            din[i] = c->dbuf + i * pitch;
-            HEC_HIP(hipMemcpyAsync(c->dbuf + i * pitch, data[i], shard_len, hipMemcpyHostToDevice, c->stream), HEC_ERR_DEVICE);
-        }
-        for (size_t j = 0; j < c->m; j++) dout[j] = c->dbuf + (c->k + j) * pitch;
-        rc = matmul_batch(c->device, c->enc.data() + c->k * c->k, c->m, c->k, din, strides, dout, strides, shard_len,
-                          1, c->stream);
-        if (rc != HEC_OK) return rc;
-        for (size_t j = 0; j < c->m; j++)
-            HEC_HIP(hipMemcpyAsync(parity[j], dout[j], shard_len, hipMemcpyDeviceToHost, c->stream), HEC_ERR_DEVICE);
-        HEC_HIP(hipStreamSynchronize(c->stream), HEC_ERR_DEVICE);
-        return HEC_OK;
+        return call_through_device(c, data, c->k, parity, c->m, c->enc.data() + c->k * c->k, shard_len);
     });
 }
 
@@ -447,28 +512,14 @@ int hec_decode(hec_coder_t* c, const uint8_t* const* shards, size_t shard_len, u
         if (!out) return HEC_ERR_INVALID_ARG;
         for (size_t i : p.missing)
             if (!out[i]) return HEC_ERR_INVALID_ARG;
+        const uint8_t* in[HEC_MAX_DATA_UNITS];
+        uint8_t* dst[HEC_MAX_DATA_UNITS];
+        for (size_t r = 0; r < c->k; r++) in[r] = shards[p.survivors[r]];
+        for (size_t r = 0; r < p.missing.size(); r++) dst[r] = out[p.missing[r]];
         std::lock_guard<std::mutex> lk(c->host_mu);
         DeviceGuard g(c->device);
         if (!g.ok) return fail(HEC_ERR_DEVICE, "hipSetDevice", hipErrorInvalidDevice);
-        const size_t e = p.missing.size();
-        const size_t pitch = (shard_len + 255) & ~size_t(255);
-        int rc = ensure_dbuf(c, pitch * (c->k + e));
-        if (rc != HEC_OK) return rc;
-        const uint8_t* din[HEC_MAX_DATA_UNITS];
-        uint8_t* dout[HEC_MAX_DATA_UNITS];
-        size_t strides[2 * HEC_MAX_DATA_UNITS];
-        for (size_t i = 0; i < c->k + e; i++) strides[i] = pitch;
-        for (size_t r = 0; r < c->k; r++) {
-            din[r] = c->dbuf + r * pitch;
-            HEC_HIP(hipMemcpyAsync(c->dbuf + r * pitch, shards[p.survivors[r]], shard_len, hipMemcpyHostToDevice, c->stream), HEC_ERR_DEVICE);
-        }
-        for (size_t r = 0; r < e; r++) dout[r] = c->dbuf + (c->k + r) * pitch;
-        rc = matmul_batch(c->device, p.matrix.data(), e, c->k, din, strides, dout, strides, shard_len, 1, c->stream);
-        if (rc != HEC_OK) return rc;
-        for (size_t r = 0; r < e; r++)
-            HEC_HIP(hipMemcpyAsync(out[p.missing[r]], dout[r], shard_len, hipMemcpyDeviceToHost, c->stream), HEC_ERR_DEVICE);
-        HEC_HIP(hipStreamSynchronize(c->stream), HEC_ERR_DEVICE);
-        return HEC_OK;
+        return call_through_device(c, in, c->k, dst, p.missing.size(), p.matrix.data(), shard_len);
     });
 }
 
@@ -509,15 +560,15 @@ size_t hec_decode_mixed_workspace_size(const hec_coder_t* c, size_t stripes) {
     return mixed_workspace(c->k, c->m, stripes);
 }
 
-int hec_decode_device_mixed(hec_coder_t* c, const uint8_t* const* d_shards, const size_t* shard_strides,
-                            uint8_t* const* d_out, const size_t* out_strides, const uint64_t* present,
-                            size_t cell_len, size_t stripes, void* d_workspace, size_t workspace_bytes,
-                            void* hip_stream) {
-    if (!c || !d_shards || !shard_strides || !d_out || !out_strides || !present || cell_len == 0)
-        return HEC_ERR_INVALID_ARG;
-    if (stripes == 0) return HEC_OK;
-    if (stripes > 0xFFFFFFFFull) return HEC_ERR_INVALID_ARG;
-    return guarded([&] {
+namespace {
+
+// Body of hec_decode_device_mixed.  Shards that no stripe's plan reads may be
+// null here (the verified read's phase 2); the public call requires storage
+// for every shard index.
+int mixed_decode_impl(hec_coder* c, const uint8_t* const* d_shards, const size_t* shard_strides,
+                      uint8_t* const* d_out, const size_t* out_strides, const uint64_t* present, size_t cell_len,
+                      size_t stripes, void* d_workspace, size_t workspace_bytes, void* hip_stream) {
+    {
         const size_t k = c->k, m = c->m, n = k + m;
         const uint64_t all = n >= 64 ? ~uint64_t(0) : ((uint64_t(1) << n) - 1);
         // 1. plan per distinct mask (host), fail before launching anything
@@ -532,7 +583,7 @@ int hec_decode_device_mixed(hec_coder_t* c, const uint8_t* const* d_shards, cons
                 uint8_t pres[HEC_MAX_DATA_UNITS + HEC_MAX_PARITY_UNITS];
                 for (size_t i = 0; i < n; i++) pres[i] = (mask >> i) & 1;
                 const PlanRef p_ref = cached_plan(c, pres);
-        const DecodePlan& p = *p_ref;
+                const DecodePlan& p = *p_ref;
                 if (p.status != HEC_OK) return p.status;
                 uint16_t id = 0xFFFF;
                 if (!p.missing.empty()) {
@@ -549,9 +600,6 @@ int hec_decode_device_mixed(hec_coder_t* c, const uint8_t* const* d_shards, cons
         for (const PlanRef& p : plans)
             for (size_t i : p->missing)
                 if (!d_out[i]) return HEC_ERR_INVALID_ARG;
-        for (size_t i = 0; i < n; i++)
-            if (!d_shards[i]) return HEC_ERR_INVALID_ARG;  // every shard needs storage (present in some stripe)
-
         DeviceGuard g(c->device);
         if (!g.ok) return fail(HEC_ERR_DEVICE, "hipSetDevice", hipErrorInvalidDevice);
         hipStream_t stream = static_cast<hipStream_t>(hip_stream);
@@ -660,6 +708,24 @@ int hec_decode_device_mixed(hec_coder_t* c, const uint8_t* const* d_shards, cons
             if (rc != 0) return to_status(rc);
         }
         return HEC_OK;
+    }
+}
+
+}  // namespace
+
+int hec_decode_device_mixed(hec_coder_t* c, const uint8_t* const* d_shards, const size_t* shard_strides,
+                            uint8_t* const* d_out, const size_t* out_strides, const uint64_t* present,
+                            size_t cell_len, size_t stripes, void* d_workspace, size_t workspace_bytes,
+                            void* hip_stream) {
+    if (!c || !d_shards || !shard_strides || !d_out || !out_strides || !present || cell_len == 0)
+        return HEC_ERR_INVALID_ARG;
+    if (stripes == 0) return HEC_OK;
+    if (stripes > 0xFFFFFFFFull) return HEC_ERR_INVALID_ARG;
+    for (size_t i = 0; i < c->k + c->m; i++)
+        if (!d_shards[i]) return HEC_ERR_INVALID_ARG;  // every shard needs storage (present in some stripe)
+    return guarded([&] {
+        return mixed_decode_impl(c, d_shards, shard_strides, d_out, out_strides, present, cell_len, stripes,
+                                 d_workspace, workspace_bytes, hip_stream);
     });
 }
 
@@ -867,9 +933,11 @@ int crc_kind(int checksum_type) {
 // s * n_total + sid[i] in the sums/flags layouts (sid == nullptr: identity).
 int checksum_launch(hec_coder* c, int kind, const uint8_t* const* bases, const size_t* strides, const uint8_t* sid,
                     size_t n_shards, size_t n_total, size_t cell_len, size_t stripes, size_t bpc, uint8_t* out,
-                    const uint8_t* expected, uint8_t* bad, hipStream_t stream) {
+                    const uint8_t* expected, uint8_t* bad, hipStream_t stream,
+                    const uint32_t* stripe_list = nullptr) {
     hec::CrcArgs a;
     std::memset(&a, 0, sizeof(a));
+    a.stripe_list = stripe_list;
     for (size_t i = 0; i < n_shards; i++) {
         if (!bases[i]) return HEC_ERR_INVALID_ARG;
         a.base[i] = bases[i];
@@ -1081,69 +1149,110 @@ int hec_decode_verify_device(hec_coder_t* c, int checksum_type, const uint8_t* c
         HEC_HIP(hipMemcpyAsync(bad.data(), d_bad, bad.size(), hipMemcpyDeviceToHost, stream), HEC_ERR_DEVICE);
         HEC_HIP(hipStreamSynchronize(stream), HEC_ERR_DEVICE);
 
-        // ---- phase 2: stripes with a failed survivor, one at a time
-        int status = HEC_OK;
+        // ---- phase 2, batched over every stripe with a failed survivor.  A
+        // round re-plans each such stripe on the host (drop what failed, take
+        // the first k available shards), verifies every newly used cell of
+        // every stripe with at most one checksum launch per shard index (a
+        // stripe-list launch), and reads the flags back once.  At most m
+        // rounds; then one mixed-pattern decode rebuilds every missing or
+        // failed data cell of those stripes with its final plan.
+        std::vector<uint32_t> F;  // stripes still being repaired
         for (size_t s = 0; s < stripes; s++) {
-            uint8_t* row = &bad[s * n];
             bool any = false;
-            for (size_t r = 0; r < k; r++) any |= row[surv[r]] != 0;
-            if (!any) continue;
-            uint8_t ok[HEC_MAX_DATA_UNITS + HEC_MAX_PARITY_UNITS] = {};  // verified good
-            for (size_t r = 0; r < k; r++) ok[surv[r]] = row[surv[r]] == 0;
-            uint8_t avail[HEC_MAX_DATA_UNITS + HEC_MAX_PARITY_UNITS];
-            bool enough = true;
-            for (;;) {
-                // the first k available shards that have not failed
-                std::vector<size_t> pick, todo;
-                for (size_t i = 0; i < n; i++) {
-                    avail[i] = present[i] && !row[i];
-                    if (avail[i] && pick.size() < k) pick.push_back(i);
+            for (size_t r = 0; r < k; r++) any |= bad[s * n + surv[r]] != 0;
+            if (any) F.push_back(uint32_t(s));
+        }
+        if (F.empty()) return HEC_OK;
+        int status = HEC_OK;
+        std::vector<uint8_t> ok(F.size() * n, 0);  // cell verified good
+        for (size_t f = 0; f < F.size(); f++)
+            for (size_t r = 0; r < k; r++) ok[f * n + surv[r]] = bad[F[f] * n + surv[r]] == 0;
+        std::vector<uint8_t> active(F.size(), 1);
+        const size_t nck = (cell_len + bytes_per_checksum - 1) / bytes_per_checksum;
+        (void)nck;
+        for (size_t round = 0; round <= c->m + 1; round++) {
+            std::vector<std::vector<uint32_t>> lists(n);
+            size_t todo_cells = 0;
+            for (size_t f = 0; f < F.size(); f++) {
+                if (!active[f]) continue;
+                const uint8_t* row = &bad[F[f] * n];
+                size_t picked = 0;
+                for (size_t i = 0; i < n && picked < k; i++) {
+                    if (!present[i] || row[i]) continue;
+                    picked++;
+                    if (!ok[f * n + i]) {
+                        lists[i].push_back(F[f]);
+                        todo_cells++;
+                    }
                 }
-                if (pick.size() < k) {
-                    enough = false;
-                    break;
+                if (picked < k) {  // fewer than k cells left that can verify
+                    active[f] = 0;
+                    status = HEC_ERR_NOT_ENOUGH_SHARDS;
                 }
-                for (size_t i : pick)
-                    if (!ok[i]) todo.push_back(i);
-                if (todo.empty()) break;
-                const uint8_t* tb[HEC_MAX_DATA_UNITS + HEC_MAX_PARITY_UNITS];
-                size_t ts[HEC_MAX_DATA_UNITS + HEC_MAX_PARITY_UNITS];
-                uint8_t tid[HEC_MAX_DATA_UNITS + HEC_MAX_PARITY_UNITS];
-                for (size_t t = 0; t < todo.size(); t++) {
-                    tb[t] = d_shards[todo[t]] + s * shard_strides[todo[t]];
-                    ts[t] = 0;
-                    tid[t] = uint8_t(todo[t]);
-                }
-                const size_t nck = (cell_len + bytes_per_checksum - 1) / bytes_per_checksum;
-                const int rc = checksum_launch(c, kind, tb, ts, tid, todo.size(), n, cell_len, 1, bytes_per_checksum,
-                                               nullptr, d_sums + s * n * nck * 4, d_bad + s * n, stream);
+            }
+            if (todo_cells == 0) break;
+            // one upload of every list, one launch per shard index, one read-back
+            std::vector<uint32_t> flat;
+            std::vector<size_t> off(n, 0);
+            for (size_t i = 0; i < n; i++) {
+                off[i] = flat.size();
+                flat.insert(flat.end(), lists[i].begin(), lists[i].end());
+            }
+            const size_t need = flat.size() * sizeof(uint32_t);
+            if (c->verify_ws_bytes < need) {
+                if (c->verify_ws) (void)hipFree(c->verify_ws);
+                c->verify_ws = nullptr;
+                c->verify_ws_bytes = 0;
+                const size_t want = std::max(need, size_t(64) << 10);
+                HEC_HIP(hipMalloc(&c->verify_ws, want), HEC_ERR_NO_MEMORY);
+                c->verify_ws_bytes = want;
+            }
+            const uint32_t* d_lists = reinterpret_cast<const uint32_t*>(c->verify_ws);
+            HEC_HIP(hipMemcpyAsync(c->verify_ws, flat.data(), need, hipMemcpyHostToDevice, stream), HEC_ERR_DEVICE);
+            for (size_t i = 0; i < n; i++) {
+                if (lists[i].empty()) continue;
+                const uint8_t* tb[1] = {d_shards[i]};
+                const size_t ts[1] = {shard_strides[i]};
+                const uint8_t tid[1] = {uint8_t(i)};
+                const int rc = checksum_launch(c, kind, tb, ts, tid, 1, n, cell_len, lists[i].size(), bytes_per_checksum,
+                                               nullptr, d_sums, d_bad, stream, d_lists + off[i]);
                 if (rc != HEC_OK) return rc;
-                HEC_HIP(hipMemcpyAsync(row, d_bad + s * n, n, hipMemcpyDeviceToHost, stream), HEC_ERR_DEVICE);
-                HEC_HIP(hipStreamSynchronize(stream), HEC_ERR_DEVICE);
-                for (size_t i : todo) ok[i] = row[i] == 0;
             }
-            if (!enough) {
-                status = HEC_ERR_NOT_ENOUGH_SHARDS;
-                continue;
+            HEC_HIP(hipMemcpyAsync(bad.data(), d_bad, bad.size(), hipMemcpyDeviceToHost, stream), HEC_ERR_DEVICE);
+            HEC_HIP(hipStreamSynchronize(stream), HEC_ERR_DEVICE);  // also keeps `flat` alive through the upload
+            for (size_t i = 0; i < n; i++)
+                for (uint32_t s : lists[i]) {
+                    const size_t f = size_t(std::lower_bound(F.begin(), F.end(), s) - F.begin());
+                    ok[f * n + i] = bad[size_t(s) * n + i] == 0;
+                }
+        }
+        // rebuild: final presence mask per repaired stripe, every other stripe
+        // a no-op (nothing missing), one mixed-pattern decode launch
+        const uint64_t all = n >= 64 ? ~uint64_t(0) : ((uint64_t(1) << n) - 1);
+        std::vector<uint64_t> masks(stripes, all);
+        bool any_rebuild = false;
+        for (size_t f = 0; f < F.size(); f++) {
+            if (!active[f]) continue;
+            uint64_t mask = 0;
+            for (size_t i = 0; i < n; i++)
+                if (present[i] && !bad[size_t(F[f]) * n + i]) mask |= uint64_t(1) << i;
+            masks[F[f]] = mask;
+            any_rebuild = true;
+        }
+        if (any_rebuild) {
+            const size_t ws_need = mixed_workspace(k, c->m, stripes);
+            if (c->verify_ws_bytes < ws_need) {
+                if (c->verify_ws) (void)hipFree(c->verify_ws);
+                c->verify_ws = nullptr;
+                c->verify_ws_bytes = 0;
+                HEC_HIP(hipMalloc(&c->verify_ws, ws_need), HEC_ERR_NO_MEMORY);
+                c->verify_ws_bytes = ws_need;
             }
-            const PlanRef q_ref = cached_plan(c, avail);
-        const DecodePlan& q = *q_ref;
-            if (q.status != HEC_OK) return q.status;
-            if (q.missing.empty()) continue;
-            const uint8_t* qin[HEC_MAX_DATA_UNITS];
-            size_t qst[HEC_MAX_DATA_UNITS];
-            uint8_t* qout[HEC_MAX_DATA_UNITS];
-            size_t qost[HEC_MAX_DATA_UNITS];
-            for (size_t r = 0; r < k; r++) {
-                qin[r] = d_shards[q.survivors[r]] + s * shard_strides[q.survivors[r]];
-                qst[r] = 0;
-            }
-            for (size_t j = 0; j < q.missing.size(); j++) {
-                qout[j] = d_out[q.missing[j]] + s * out_strides[q.missing[j]];
-                qost[j] = 0;
-            }
-            const int rc = matmul_batch(c->device, q.matrix.data(), q.missing.size(), k, qin, qst, qout, qost, cell_len,
-                                        1, stream);
+            // storage for shard indices no plan reads (absent for the whole batch)
+            const uint8_t* shards_all[HEC_MAX_DATA_UNITS + HEC_MAX_PARITY_UNITS];
+            for (size_t i = 0; i < n; i++) shards_all[i] = d_shards[i] ? d_shards[i] : d_out[0];
+            const int rc = mixed_decode_impl(c, shards_all, shard_strides, d_out, out_strides, masks.data(), cell_len,
+                                             stripes, c->verify_ws, c->verify_ws_bytes, hip_stream);
             if (rc != HEC_OK) return rc;
         }
         HEC_HIP(hipStreamSynchronize(stream), HEC_ERR_DEVICE);

@@ -149,6 +149,10 @@ __global__ __launch_bounds__(BS) void gf_matmul_v16(MatmulArgs a) {
                         store16<NT>((a.out[j] + uint64_t(stripe) * a.out_stride[j]) + offs[u], acc[u][j]);
                 }
             }
+            // drain policy (tune key 6): the tile's stores complete before the
+            // next tile's loads are issued -- writes and reads then reach DRAM
+            // in per-wave bursts rather than interleaved
+            if (a.drain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         } else {
             // Runtime K: one shard at a time, U chunks per lane.
 #pragma unroll
@@ -483,6 +487,7 @@ __global__ __launch_bounds__(BS) void gf_decode_mixed(MixedArgs a) {
             for (int u = 0; u < U; u++)
                 if (full || live[u]) store16<true>(ob + offs[u], acc[u][j]);
         }
+        if (a.drain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // as gf_matmul_v16
     }
 }
 
@@ -689,6 +694,11 @@ int launch_gf_matmul(const MatmulArgs& in, int device, hipStream_t stream) {
         // 4 stripes column-interleaved: +1-4 % over stripe-major at 1 MiB
         // cells (profiles/r01_probe_tile_order.log)
         a.group = group_for(a.stripes, tn.group > 0 ? uint32_t(tn.group) : 4u);
+        // stores drained before the next tile's loads unless key 6 = 1: same-box
+        // bench A/B (profiles/r02_drain_ab.txt): RS(6,3) 1 MiB 3702 vs 3514
+        // GiB/s, RS(10,4) 3926 vs 3906, RS(3,2) 3089 vs 3075 -- DRAM prefers a
+        // wave's writes and its next reads in separate bursts
+        a.drain = tn.drain == 1 ? 0u : 1u;
         uint64_t grid = tn.grid ? uint64_t(tn.grid) : uint64_t(cus) * sh.blocks_per_cu;
         if (grid > total) grid = total;
         void* args[] = {&a};
@@ -765,6 +775,7 @@ int launch_decode_mixed(const MixedArgs& in, int rows, int device, hipStream_t s
     a.tiles_per_stripe = uint32_t(tps);
     a.total_tiles = uint32_t(total);
     a.group = group_for(a.stripes, tn.group > 0 ? uint32_t(tn.group) : 4u);
+    a.drain = tn.drain == 1 ? 0u : 1u;
     uint64_t grid = uint64_t(num_cus(device)) * bpc;
     if (grid > total) grid = total;
     void* args[] = {&a};

@@ -30,6 +30,7 @@ struct MatmulArgs {
     uint32_t tiles_per_stripe;
     uint32_t total_tiles;
     uint32_t group;               // tile order: G stripes column-interleaved (1 = stripe-major); divides stripes
+    uint32_t drain;               // register kernel: 1 = wait for the tile's stores before the next tile's loads
 };
 
 // One coefficient's v_perm_b32 product tables (see ec_kernels.hip): c*x =
@@ -67,6 +68,7 @@ struct MixedArgs {
     uint64_t cell_len;
     uint64_t stripes;
     uint32_t chunks, tiles_per_stripe, total_tiles, group;
+    uint32_t drain;                   // 1 = wait for a tile's stores before the next tile (tune key 6)
 };
 
 // Mixed-pattern decode of one group of missing rows row0 .. row0+rows-1

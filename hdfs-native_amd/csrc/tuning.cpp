@@ -36,6 +36,7 @@ Tune tune_snapshot() {
     t.blocks_per_cu = load(3);
     t.block = load(4);
     t.pipeline = load(5);
+    t.drain = load(6);
     t.grid = load(7);
     t.group = load(8);
     t.crc_unfused = load(9);
@@ -58,6 +59,7 @@ int tune_store(int key, int value) {
         case 3: ok = value >= 0 && value <= 16; break;
         case 4: ok = value == 0 || value == 256 || value == 512; break;
         case 5: ok = (value >= 0 && value <= 2) || (kExperimental && value >= 3 && value <= 5); break;
+        case 6: ok = value >= 0 && value <= 2; break;
         case 7: ok = value >= 0 && value <= 65536; break;
         case 8: ok = value >= 0 && value <= 65536; break;
         case 9: value = value ? 1 : 0; ok = true; break;

@@ -18,6 +18,7 @@ struct Tune {
     int blocks_per_cu;      // key 3: grid = blocks_per_cu x CUs (0 = default)
     int block;              // key 4: threads per block (0 = default)
     int pipeline;           // key 5: 0 default, 1 register, 2 LDS-DMA (exp: 3 pipe, 4 burst, 5 double-buffered)
+    int drain;              // key 6: store drain per tile in the register kernels (0 default = yes, 1 no, 2 yes)
     int grid;               // key 7: absolute grid size (0 = default)
     int group;              // key 8: stripes per tile-order group (0 = default 4)
     int crc_unfused;        // key 9: 1 = hec_encode_crc_device as encode + checksum passes

@@ -217,8 +217,11 @@ int hec_checksum_verify_device(hec_coder_t *coder, int checksum_type, const uint
  * verify are not copied.  d_bad[s*(k+m) + i] = 1 marks the
  * cells that failed (zeroed by the call; device memory).  When every stripe
  * verifies first time this is one fused pass over the survivors (k in
- * {2,3,6,10}, 512-B chunks, 16-B aligned); failing stripes are re-planned
- * on the host and redone one by one.  Synchronous (it must see the
+ * {2,3,6,10}, 512-B chunks, 16-B aligned).  Stripes with a failing cell
+ * are re-planned on the host together: each round verifies every newly
+ * used cell of all of them (one stripe-list checksum launch per shard
+ * index, one flag read-back), and one mixed-pattern decode then rebuilds
+ * them all (at most m rounds).  Synchronous (it must see the
  * verdicts).  Returns HEC_ERR_NOT_ENOUGH_SHARDS when some stripe has fewer
  * than k shards that verify (its d_bad flags say which; the other stripes
  * are still rebuilt).  HEC_CHECKSUM_NULL decodes without verifying. */
@@ -294,6 +297,8 @@ int hec_group_decode_host_batch(hec_group_t *group, const uint8_t *const *h_vert
 
 /* ---- HBM buffers for the batched API ------------------------------------ *
  * Device memory for stripe batches on `device` (hipExtMallocWithFlags).
+ * Checksum sum / flag buffers passed to the checksum calls must be 4-byte
+ * aligned (they are read and written as u32).
  * HEC_ALLOC_CONTIGUOUS asks for physically contiguous HBM, which the GPU
  * maps with large page fragments: a batch of tens of GiB then needs far
  * fewer translation entries.  hec_device_free releases it

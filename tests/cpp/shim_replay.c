@@ -1,0 +1,181 @@
+/* shim_replay.c -- replays, call for call, what rust/src/ec/mi355x.rs (the
+ * Rust shim a maintainer adds to hdfs-native; not compilable in this image)
+ * does through the C ABI, and checks the results against the CPU oracle
+ * (oracle/ec_oracle.c, test infrastructure):
+ *   GpuCoder::new     -> hec_abi_version, hec_coder_create_codec("rs")
+ *   GpuCoder::encode  -> hec_encode (the shim asserts n > 0 first; the C side
+ *                        rejects n == 0 with HEC_ERR_INVALID_ARG as well)
+ *   GpuCoder::decode  -> hec_decode with null out slots for present shards
+ *                        and parity (here: sentinel buffers, which must stay
+ *                        untouched); HEC_ERR_NOT_ENOUGH_SHARDS -> the shim's
+ *                        ErasureCodingError("Not enough valid shards")
+ *   encode_rows / decode_rows / GpuGroup -> the batched calls
+ * Built by __graft_entry__.build(); run by tests/test_shim_replay.py (GPU). */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../include/hdfs_ec_amd.h"
+
+/* oracle/ec_oracle.c */
+int orc_encode(size_t k, size_t m, const uint8_t *const *data, size_t n, uint8_t *const *parity);
+
+static int failures = 0;
+#define CHECK(cond, ...)                                  \
+    do {                                                  \
+        if (!(cond)) {                                    \
+            fprintf(stderr, "FAIL %s:%d: ", __FILE__, __LINE__); \
+            fprintf(stderr, __VA_ARGS__);                 \
+            fprintf(stderr, "\n");                        \
+            failures++;                                   \
+        }                                                 \
+    } while (0)
+
+static uint64_t rng = 0x5EEDEC00u;
+static uint8_t next_byte(void) {
+    rng ^= rng << 13;
+    rng ^= rng >> 7;
+    rng ^= rng << 17;
+    return (uint8_t)(rng >> 24);
+}
+
+enum { K = 6, M = 3 };
+
+int main(void) {
+    CHECK(hec_abi_version() == 3, "ABI %d", hec_abi_version());
+    hec_coder_t *c = NULL;
+    int rc = hec_coder_create_codec("rs", K, M, 0, &c);
+    if (rc != HEC_OK) {
+        fprintf(stderr, "coder create: %s (%s)\n", hec_strerror(rc), hec_last_error());
+        return 2;
+    }
+    hec_coder_t *bad = NULL;
+    CHECK(hec_coder_create_codec("rs-legacy", K, M, 0, &bad) == HEC_ERR_UNSUPPORTED_CODEC && bad == NULL,
+          "rs-legacy must be UnsupportedErasureCodingPolicy");
+
+    const size_t n = (1u << 20) + 5; /* a full cell plus a tail the 16-B kernels do not cover */
+    uint8_t *data[K], *par[M], *want[M];
+    for (int i = 0; i < K; i++) {
+        data[i] = malloc(n);
+        for (size_t b = 0; b < n; b++) data[i][b] = next_byte();
+    }
+    for (int j = 0; j < M; j++) {
+        par[j] = malloc(n);
+        want[j] = malloc(n);
+    }
+    CHECK(orc_encode(K, M, (const uint8_t *const *)data, n, want) == 0, "oracle encode");
+
+    /* GpuCoder::encode: zero length is the reference's panic, a status here */
+    CHECK(hec_encode(c, (const uint8_t *const *)data, 0, par) == HEC_ERR_INVALID_ARG, "n == 0");
+    rc = hec_encode(c, (const uint8_t *const *)data, n, par);
+    CHECK(rc == HEC_OK, "encode %s", hec_strerror(rc));
+    for (int j = 0; j < M; j++) CHECK(memcmp(par[j], want[j], n) == 0, "parity %d != oracle", j);
+
+    /* GpuCoder::decode: data 0..2 missing; out slots of present shards and of
+     * parity hold sentinels that must not change */
+    uint8_t *shards[K + M], *out[K + M];
+    uint8_t *sentinel = malloc(n);
+    memset(sentinel, 0xCC, n);
+    for (int i = 0; i < K + M; i++) {
+        shards[i] = i < 3 ? NULL : (i < K ? data[i] : par[i - K]);
+        out[i] = malloc(n);
+        memcpy(out[i], sentinel, n);
+    }
+    rc = hec_decode(c, (const uint8_t *const *)shards, n, out);
+    CHECK(rc == HEC_OK, "decode %s", hec_strerror(rc));
+    for (int i = 0; i < K + M; i++) {
+        if (i < 3)
+            CHECK(memcmp(out[i], data[i], n) == 0, "rebuilt data %d", i);
+        else
+            CHECK(memcmp(out[i], sentinel, n) == 0, "slot %d written (must be untouched)", i);
+    }
+
+    /* data 0,1 and parity 0 missing: parity is never regenerated
+     * (gf256.rs:96-97); survivors 2,3,4,5,7,8 */
+    shards[2] = data[2];
+    shards[K] = NULL;
+    for (int i = 0; i < K + M; i++) memcpy(out[i], sentinel, n);
+    rc = hec_decode(c, (const uint8_t *const *)shards, n, out);
+    CHECK(rc == HEC_OK, "decode with a parity missing %s", hec_strerror(rc));
+    CHECK(memcmp(out[K], sentinel, n) == 0, "missing parity slot written");
+    CHECK(memcmp(out[2], sentinel, n) == 0, "present data slot written");
+    for (int i = 0; i < 2; i++) CHECK(memcmp(out[i], data[i], n) == 0, "rebuilt data %d (parity missing)", i);
+
+    /* 4 missing of RS(6,3): the shim's ErasureCodingError("Not enough valid shards") */
+    shards[3] = NULL;
+    rc = hec_decode(c, (const uint8_t *const *)shards, n, out);
+    CHECK(rc == HEC_ERR_NOT_ENOUGH_SHARDS, "4 missing -> %d", rc);
+    CHECK(strstr(hec_strerror(rc), "Not enough valid shards") != NULL, "message");
+
+    /* nothing missing: Ok, no write (gf256.rs:102-105) */
+    for (int i = 0; i < K; i++) shards[i] = data[i];
+    for (int j = 0; j < M; j++) shards[K + j] = NULL;
+    memcpy(out[0], sentinel, n);
+    CHECK(hec_decode(c, (const uint8_t *const *)shards, n, out) == HEC_OK, "no-op decode");
+    CHECK(memcmp(out[0], sentinel, n) == 0, "no-op decode wrote");
+
+    /* encode_rows / decode_rows: R rows of 64 KiB cells in file order */
+    enum { R = 5 };
+    const size_t cell = 65536;
+    uint8_t *rows = malloc(R * K * cell), *rpar = malloc(R * M * cell), *file = malloc(R * K * cell);
+    for (size_t b = 0; b < R * K * cell; b++) rows[b] = next_byte();
+    rc = hec_encode_host_batch(c, rows, rpar, cell, R, 2);
+    CHECK(rc == HEC_OK, "encode_rows %s", hec_strerror(rc));
+    for (int r = 0; r < R; r++) {
+        const uint8_t *rin[K];
+        uint8_t *rout[M];
+        for (int i = 0; i < K; i++) rin[i] = rows + (r * K + i) * cell;
+        for (int j = 0; j < M; j++) rout[j] = want[j];
+        orc_encode(K, M, rin, cell, rout);
+        for (int j = 0; j < M; j++) CHECK(memcmp(rpar + (r * M + j) * cell, want[j], cell) == 0, "row %d parity %d", r, j);
+    }
+    uint8_t *vert[K + M];
+    for (int i = 0; i < K + M; i++) {
+        vert[i] = malloc(R * cell);
+        for (int r = 0; r < R; r++)
+            memcpy(vert[i] + r * cell, i < K ? rows + (r * K + i) * cell : rpar + (r * M + i - K) * cell, cell);
+    }
+    const uint8_t *vin[K + M];
+    for (int i = 0; i < K + M; i++) vin[i] = (i == 1 || i == 4) ? NULL : vert[i];
+    rc = hec_decode_host_batch(c, vin, cell, R, file, 2);
+    CHECK(rc == HEC_OK, "decode_rows %s", hec_strerror(rc));
+    CHECK(memcmp(file, rows, R * K * cell) == 0, "decode_rows file order");
+
+    /* GpuGroup over device 0 twice: same rows, same parity */
+    hec_group_t *g = NULL;
+    const int devs[2] = {0, 0};
+    rc = hec_group_create("rs", K, M, devs, 2, &g);
+    CHECK(rc == HEC_OK, "group %s", hec_strerror(rc));
+    if (rc == HEC_OK) {
+        uint8_t *gpar = malloc(R * M * cell);
+        CHECK(hec_group_encode_host_batch(g, rows, gpar, cell, R, 2) == HEC_OK, "group encode_rows");
+        CHECK(memcmp(gpar, rpar, R * M * cell) == 0, "group parity");
+        memset(file, 0, R * K * cell);
+        CHECK(hec_group_decode_host_batch(g, vin, cell, R, file, 2) == HEC_OK, "group decode_rows");
+        CHECK(memcmp(file, rows, R * K * cell) == 0, "group file order");
+        free(gpar);
+        hec_group_destroy(g);
+    }
+
+    hec_coder_destroy(c);
+    for (int i = 0; i < K; i++) free(data[i]);
+    for (int j = 0; j < M; j++) {
+        free(par[j]);
+        free(want[j]);
+    }
+    for (int i = 0; i < K + M; i++) {
+        free(out[i]);
+        free(vert[i]);
+    }
+    free(sentinel);
+    free(rows);
+    free(rpar);
+    free(file);
+    if (failures) {
+        fprintf(stderr, "%d failure(s)\n", failures);
+        return 1;
+    }
+    printf("shim replay ok\n");
+    return 0;
+}

@@ -218,7 +218,7 @@ def test_gf_matmul_device_arbitrary_matrix(dev):
 
 @pytest.mark.parametrize("knob", [((1, 1),), ((1, 2),), ((1, 4),), ((2, 0),), ((3, 2),), ((4, 512), (1, 1)),
                                   ((4, 512), (1, 2)), ((1, 4), (2, 0), (3, 3)), ((5, 2),), ((5, 2), (1, 2)),
-                                  ((5, 2), (4, 512)), ((5, 2), (3, 2)), ((5, 1),), ((7, 100),), ((7, 3),), ((8, 2),),
+                                  ((5, 2), (4, 512)), ((5, 2), (3, 2)), ((5, 1),), ((6, 1),), ((6, 2),), ((6, 2), (4, 512)), ((7, 100),), ((7, 3),), ((8, 2),),
                                   ((8, 3),), ((8, 4), (5, 2)), ((8, 64),), ((7, 16),), ((7, 12),)])
 def test_tuning_variants_bit_identical(dev, c_oracle, knob):
     k, m, S, cell = 6, 3, 5, 8192 + 16
@@ -239,6 +239,7 @@ def test_tuning_variants_bit_identical(dev, c_oracle, knob):
         H.tune_set(3, 0)
         H.tune_set(4, 0)
         H.tune_set(5, 0)
+        H.tune_set(6, 0)
         H.tune_set(7, 0)
         H.tune_set(8, 0)
     assert np.array_equal(p.cpu().numpy(), want)
@@ -319,7 +320,7 @@ def test_tune_set_concurrent_with_launches(dev, c_oracle):
 
 def test_experimental_keys_rejected_by_default_library():
     # the rejected variants exist only in lib/libhdfs_ec_amd_exp.so
-    for key, value in [(5, 3), (5, 4), (5, 5), (13, 1), (15, 2), (11, 2), (11, 9), (6, 1), (16, 1)]:
+    for key, value in [(5, 3), (5, 4), (5, 5), (13, 1), (15, 2), (11, 2), (11, 9), (6, 3), (16, 1)]:
         with pytest.raises(ValueError):
             H.tune_set(key, value)
 
