@@ -10,8 +10,12 @@
 //   * device calls only enqueue kernels on the caller's stream.
 // Nothing here throws or aborts across the ABI: every entry point catches.
 #include <hip/hip_runtime.h>
+#include <sys/mman.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include <algorithm>
+#include <fstream>
 #include <map>
 #include <memory>
 #include <cstdio>
@@ -1410,6 +1414,89 @@ int hec_device_free(int device, void* ptr) {
         if (!g.ok) return fail(HEC_ERR_DEVICE, "hipSetDevice", hipErrorInvalidDevice);
         HEC_HIP(hipFree(ptr), HEC_ERR_DEVICE);
         return HEC_OK;
+    });
+}
+
+// ---- NUMA-placed pinned host buffers -------------------------------------
+
+namespace {
+
+std::mutex g_host_mu;
+std::unordered_map<void*, size_t> g_host_allocs;  // ptr -> mapped bytes
+
+int numa_node_of(int device) {
+    char bus[64] = {0};
+    if (hipDeviceGetPCIBusId(bus, sizeof(bus), device) != hipSuccess) return -1;
+    std::string id(bus);
+    for (auto& ch : id) ch = char(std::tolower(static_cast<unsigned char>(ch)));
+    std::ifstream f("/sys/bus/pci/devices/" + id + "/numa_node");
+    int node = -1;
+    if (!(f >> node)) return -1;
+    return node;
+}
+
+}  // namespace
+
+int hec_device_numa_node(int device) {
+    try {
+        return numa_node_of(device);
+    } catch (...) {
+        return -1;
+    }
+}
+
+int hec_host_alloc(int device, size_t bytes, int numa_node, void** out) {
+    if (!out || bytes == 0 || numa_node < -1 || numa_node >= 1024) return HEC_ERR_INVALID_ARG;
+    *out = nullptr;
+    return guarded([&] {
+        DeviceGuard g(device);
+        if (!g.ok) return fail(HEC_ERR_DEVICE, "hipSetDevice", hipErrorInvalidDevice);
+        const int node = numa_node >= 0 ? numa_node : numa_node_of(device);
+        const size_t page = size_t(sysconf(_SC_PAGESIZE));
+        const size_t len = (bytes + page - 1) / page * page;
+        void* p = mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+        if (p == MAP_FAILED) return int(HEC_ERR_NO_MEMORY);
+        if (node >= 0) {
+            // MPOL_BIND to the node before the pages exist: every page is
+            // faulted in there by the touch below
+            unsigned long mask[1024 / (8 * sizeof(unsigned long))] = {0};
+            mask[node / (8 * sizeof(unsigned long))] |= 1ul << (node % (8 * sizeof(unsigned long)));
+            const long MPOL_BIND_ = 2;
+            if (syscall(SYS_mbind, p, len, MPOL_BIND_, mask, 1024ul, 0ul) != 0) {
+                munmap(p, len);
+                std::snprintf(g_last_error, sizeof(g_last_error), "mbind to NUMA node %d failed", node);
+                return int(HEC_ERR_INVALID_ARG);
+            }
+        }
+        std::memset(p, 0, len);
+        const hipError_t e = hipHostRegister(p, len, hipHostRegisterDefault);
+        if (e != hipSuccess) {
+            munmap(p, len);
+            (void)hipGetLastError();
+            return fail(HEC_ERR_NO_MEMORY, "hipHostRegister", e);
+        }
+        std::lock_guard<std::mutex> lk(g_host_mu);
+        g_host_allocs[p] = len;
+        *out = p;
+        return int(HEC_OK);
+    });
+}
+
+int hec_host_free(void* ptr) {
+    if (!ptr) return HEC_OK;
+    return guarded([&] {
+        size_t len = 0;
+        {
+            std::lock_guard<std::mutex> lk(g_host_mu);
+            auto it = g_host_allocs.find(ptr);
+            if (it == g_host_allocs.end()) return int(HEC_ERR_INVALID_ARG);
+            len = it->second;
+            g_host_allocs.erase(it);
+        }
+        (void)hipHostUnregister(ptr);
+        (void)hipGetLastError();
+        munmap(ptr, len);
+        return int(HEC_OK);
     });
 }
 

@@ -174,13 +174,20 @@ struct EcSchema {
                 c.decode(vertical);
             }
         }
+        // mod.rs:82-86: Bytes::split_to(cell_size) panics when fewer bytes are
+        // left (the reader pads every cell to cell_size, block_reader.rs:
+        // 370-371, so that is a programming error): throw std::out_of_range,
+        // never clamp
         std::vector<Bytes> cells;
         std::vector<size_t> off(data_units, 0);
         while (vertical[0] && off[0] < vertical[0]->size()) {
             for (size_t i = 0; i < data_units; i++) {
                 const Bytes& v = *vertical[i];
-                const size_t a = std::min(off[i], v.size()), b = std::min(off[i] + cell_size, v.size());
-                cells.emplace_back(v.begin() + a, v.begin() + b);
+                if (off[i] + cell_size > v.size())
+                    throw std::out_of_range("split_to out of bounds: shard " + std::to_string(i) + " has " +
+                                            std::to_string(v.size() - std::min(off[i], v.size())) +
+                                            " bytes left, cell_size " + std::to_string(cell_size));
+                cells.emplace_back(v.begin() + off[i], v.begin() + off[i] + cell_size);
                 off[i] += cell_size;
             }
         }

@@ -47,7 +47,7 @@ EXPORTS = [
     "hec_crc32c_device", "hec_encode_crc_device", "hec_checksum_device", "hec_checksum_verify_device",
     "hec_decode_verify_device", "hec_group_create", "hec_group_destroy", "hec_group_size", "hec_group_coder",
     "hec_group_range", "hec_group_encode_host_batch", "hec_group_decode_host_batch",
-    "hec_device_alloc", "hec_device_free",
+    "hec_device_alloc", "hec_device_free", "hec_device_numa_node", "hec_host_alloc", "hec_host_free",
 ]
 
 
@@ -138,6 +138,9 @@ def _load(path: str = LIB_PATH) -> ctypes.CDLL:
         "hec_group_decode_host_batch": ([P, PP, S, S, P, S], I),
         "hec_device_alloc": ([I, S, ctypes.c_uint, ctypes.POINTER(P)], I),
         "hec_device_free": ([I, P], I),
+        "hec_device_numa_node": ([I], I),
+        "hec_host_alloc": ([I, S, I, ctypes.POINTER(P)], I),
+        "hec_host_free": ([P], I),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)
@@ -244,6 +247,35 @@ class DeviceBuffer:
             self.close()
         except Exception:
             pass
+
+
+class HostBuffer:
+    """Page-locked host memory on a NUMA node (hec_host_alloc; numa_node -1
+    = the node of `device`).  .array() views it as a numpy uint8 array."""
+
+    def __init__(self, nbytes: int, device: int = 0, numa_node: int = -1):
+        p = ctypes.c_void_p()
+        _check(lib.hec_host_alloc(device, nbytes, numa_node, ctypes.byref(p)))
+        self.ptr, self.nbytes = p.value, nbytes
+
+    def array(self):
+        import numpy as np
+        return np.ctypeslib.as_array((ctypes.c_uint8 * self.nbytes).from_address(self.ptr))
+
+    def close(self) -> None:
+        if self.ptr:
+            _check(lib.hec_host_free(ctypes.c_void_p(self.ptr)))
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def device_numa_node(device: int = 0) -> int:
+    return lib.hec_device_numa_node(device)
 
 
 def tune_set(key: int, value: int, lib_=None) -> None:

@@ -308,6 +308,16 @@ int hec_group_decode_host_batch(hec_group_t *group, const uint8_t *const *h_vert
 int hec_device_alloc(int device, size_t bytes, unsigned flags, void **out);
 int hec_device_free(int device, void *ptr);
 
+/* ---- NUMA-placed pinned host buffers (host-batch / group calls) -------- *
+ * hec_host_alloc: `bytes` of page-locked host memory whose pages live on
+ * NUMA node `numa_node` (-1 = the node of `device`'s PCIe root, read from
+ * sysfs), registered with HIP for full-rate DMA: the buffers one group slot
+ * streams to its GPU should sit next to that GPU's root complex.  Free with
+ * hec_host_free.  hec_device_numa_node: that node, -1 if unknown. */
+int hec_device_numa_node(int device);
+int hec_host_alloc(int device, size_t bytes, int numa_node, void **out);
+int hec_host_free(void *ptr);
+
 /* ---- Measurement knobs (not part of the reference interface) ---------- *
  * key 1: 16-B column chunks per lane per tile (1, 2, 3 or 4; 0 = default)
  * key 2: non-temporal global loads/stores (0 or 1; -1 = default on)

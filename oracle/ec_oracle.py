@@ -250,6 +250,8 @@ def ec_decode(k: int, m: int, cell_size: int, codec: str,
     offs = [0] * k
     while vs[0] is not None and offs[0] < len(vs[0]):
         for i in range(k):
+            if offs[i] + cell_size > len(vs[i]):  # Bytes::split_to panics (mod.rs:84)
+                raise ValueError("split_to out of bounds")
             cells.append(vs[i][offs[i]:offs[i] + cell_size])
             offs[i] += cell_size
     return cells

@@ -44,6 +44,21 @@ static int cpu_mode() {
             std::printf("{\"max_offset\": [%zu, %zu, %zu]}\n", index, bs, s.max_offset(index, bs));
     auto m = Coder::gen_rs_matrix(6, 3);
     std::printf("{\"rs63_row6\": [%d, %d, %d, %d, %d, %d]}\n", m[6][0], m[6][1], m[6][2], m[6][3], m[6][4], m[6][5]);
+    // ec_decode's cell split (mod.rs:82-86) with every data shard present (no
+    // decode, no device): whole cells split row by row; a shard shorter than
+    // the next cell is Bytes::split_to's panic -> std::out_of_range
+    EcSchema sp{"rs", 3, 2, 16};
+    std::vector<std::optional<Bytes>> v = {Bytes(32, 1), Bytes(32, 2), Bytes(32, 3), std::nullopt, std::nullopt};
+    const std::vector<Bytes> cells = sp.ec_decode(v);
+    std::printf("{\"split_cells\": [%zu, %d, %d]}\n", cells.size(), cells.empty() ? -1 : int(cells[1][0]),
+                cells.size() < 4 ? -1 : int(cells[3][0]));
+    v[2] = Bytes(20, 3);
+    try {
+        sp.ec_decode(v);
+        std::printf("{\"split_short\": \"no error\"}\n");
+    } catch (const std::out_of_range&) {
+        std::printf("{\"split_short\": \"out_of_range\"}\n");
+    }
     return 0;
 }
 
@@ -110,6 +125,22 @@ static Bytes read_block_group(const EcSchema& s, const std::vector<Bytes>& shard
     return out;
 }
 
+// Writes the shards of one striped write to $HEC_MIRROR_DUMP/<k>_<m>_<size>_<i>.bin
+// so the Python test can pin their bytes against the oracle.
+static void dump_shards(const EcSchema& s, size_t size, const std::vector<Bytes>& shards) {
+    const char* dir = std::getenv("HEC_MIRROR_DUMP");
+    if (!dir) return;
+    for (size_t i = 0; i < shards.size(); i++) {
+        const std::string path = std::string(dir) + "/" + std::to_string(s.data_units) + "_" +
+                                 std::to_string(s.parity_units) + "_" + std::to_string(size) + "_" +
+                                 std::to_string(i) + ".bin";
+        FILE* f = std::fopen(path.c_str(), "wb");
+        if (!f) continue;
+        if (!shards[i].empty()) std::fwrite(shards[i].data(), 1, shards[i].size(), f);
+        std::fclose(f);
+    }
+}
+
 static int gpu_mode() {
     int failures = 0;
     const size_t cell = 65536;
@@ -121,6 +152,7 @@ static int gpu_mode() {
         for (size_t size : sizes) {
             const Bytes file = counter_file(size);
             const std::vector<Bytes> shards = write_block_group(s, file);
+            if (size == cell * k * 5 + 4 || size == cell - 4) dump_shards(s, size, shards);
             for (size_t faults = 0; faults < m; faults++) {
                 const Bytes back = read_block_group(s, shards, size, faults, coder);
                 if (back != file) {

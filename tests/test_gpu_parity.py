@@ -958,3 +958,22 @@ def test_group_errors_and_slot_coders(dev, c_oracle):
     with pytest.raises(H.ErasureCodingError):
         g.decode_host_batch(ptrs, cell, rows, out.data_ptr(), 1)
     g.close()
+
+
+def test_numa_host_buffers_feed_the_host_batch(c_oracle):
+    # hec_host_alloc (pinned, NUMA-placed) buffers through hec_encode_host_batch
+    k, m, cell, S = 6, 3, 65536, 9
+    node = H.device_numa_node(0)
+    hin, hout = H.HostBuffer(S * k * cell, 0, -1), H.HostBuffer(S * m * cell, 0, -1)
+    try:
+        data = batch_data(S, k, cell, first=123)
+        hin.array()[:] = data.ravel()
+        coder(k, m).encode_host_batch(hin.ptr, hout.ptr, cell, S, 4)
+        want = oracle_batch_encode(c_oracle, k, m, data)
+        assert np.array_equal(hout.array().reshape(S, m, cell), want)
+    finally:
+        hin.close()
+        hout.close()
+    assert node >= -1
+    import ctypes
+    assert H.lib.hec_host_free(ctypes.c_void_p(12345)) == H.HEC_ERR_INVALID_ARG  # not ours: refused, not freed
