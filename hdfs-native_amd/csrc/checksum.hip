@@ -161,7 +161,8 @@ __global__ __launch_bounds__(CrcShape<SCHEME>::kBlock) void checksum_chunks512(C
             const uint32_t len = uint32_t(a.cell_len - cstart);
             uint32_t r = Spec::kInit;
             for (uint32_t p = 0; p < len; p++)
-                r = crcdev::byte_step<REFL, crcdev::ByteTable<SCHEME>::stride>(s_main + crcdev::ByteTable<SCHEME>::off, r,
+                r = crcdev::byte_step<REFL, crcdev::ByteTable<SCHEME>::stride, crcdev::ByteTable<SCHEME>::bswap>(
+                    s_main + crcdev::ByteTable<SCHEME>::off, r,
                                                                               stage[(4 * c + p / Q) * PITCH + (p % Q)]);
             val = r ^ Spec::kXorout;
         }
@@ -230,6 +231,9 @@ const void* crc_pick(int scheme, int pf) {
     if (scheme == 4) return crc_fn<KIND, 4>(pf);
     if (scheme == 8) return crc_fn<KIND, 8>(pf);
     if (scheme == 0) return crc_fn<KIND, 0>(pf);
+    // bank-replicated slicing-by-2, 4 chains: 5.14 vs 5.37 TB/s
+    // (profiles/r02_probe_crc_rep2.log)
+    if (scheme == 22) return crc_fn<KIND, 22>(pf);
 #endif
     return scheme == 1 ? crc_fn<KIND, 1>(pf) : crc_fn<KIND, 11>(pf);
 }
@@ -272,6 +276,7 @@ int launch_checksum(const CrcArgs& in, int device, hipStream_t stream) {
                            : tn.crc_variant == 3 ? 8
                            : tn.crc_variant == 4 ? 16
                            : tn.crc_variant == 9 ? 0
+                           : tn.crc_variant == 6 ? 22
                                                  : 11;
         const int pf = tn.crc_prefetch == 1 ? 1 : 2;  // scheme 16: always 1 (128 VGPRs at 4 waves/SIMD)
         const int waves = scheme == 16 ? CrcShape<16>::kWaves : crcdev::sliced(scheme) ? CrcShape<1>::kWaves : CrcShape<4>::kWaves;

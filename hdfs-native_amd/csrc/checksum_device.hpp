@@ -47,13 +47,22 @@ __device__ __forceinline__ uint32_t apply_shift(const uint32_t (*t)[256], uint32
 }
 
 // 8 message bytes through the 11-bit field tables (checksum_tables.hpp w11),
-// packed in LDS at word offsets 0, 2048, 4096, 5120, 7168, 9216.
+// packed in LDS at word offsets 0, 2048, 4096, 5120, 7168, 9216.  Each
+// field's byte offset into its table is one VALU op on its word.
+__device__ __forceinline__ uint32_t w11_off0(uint32_t w) { return w & 0x1FFCu; }
+__device__ __forceinline__ uint32_t w11_off1(uint32_t w) { return (w >> 11) & 0x1FFCu; }
+__device__ __forceinline__ uint32_t w11_off2(uint32_t w) { return __builtin_rotateright32(w, 22) & 0xFFCu; }
+
 template <bool REFL>
 __device__ __forceinline__ uint32_t step8_w11(const uint32_t* t, uint32_t crc, uint32_t lo, uint32_t hi) {
     lo ^= REFL ? crc : __builtin_bswap32(crc);
-    return x3(x3(t[lo & 0x7FF], t[2048 + ((lo >> 11) & 0x7FF)], t[4096 + (lo >> 22)]), t[5120 + (hi & 0x7FF)],
-              t[7168 + ((hi >> 11) & 0x7FF)]) ^
-           t[9216 + (hi >> 22)];
+    const char* tb = reinterpret_cast<const char*>(t);
+    auto at = [&](int word_off, uint32_t byte_off) {
+        return *reinterpret_cast<const uint32_t*>(tb + word_off * 4 + byte_off);
+    };
+    return x3(x3(at(0, w11_off0(lo)), at(2048, w11_off1(lo)), at(4096, w11_off2(lo))), at(5120, w11_off0(hi)),
+              at(7168, w11_off1(hi))) ^
+           at(9216, w11_off2(hi));
 }
 
 template <bool REFL>
@@ -112,11 +121,52 @@ __device__ __forceinline__ uint32_t quarter_rep(const uint32_t (*rep)[32], const
     return q;
 }
 
+// Bank-replicated slicing-by-2 (scheme 22): rep[k][e][b] at k*8192 + e*32 +
+// b, b = lane % 32, so a half-wave's lookups are conflict free; rep[0] =
+// slice[1] (the step's first byte), rep[1] = slice[0].  Four chains over the
+// quarter's 32-B segments (latency), combined by Horner with the "append
+// 32 zero bytes" table seg32.  An MSB-first register runs byte-swapped
+// (tables stored byte-swapped) so that both kinds share the reflected step
+// c' = T1[c & 0xFF] ^ T0[(c >> 8) & 0xFF] ^ (c >> 16).
+template <bool REFL>
+__device__ __forceinline__ uint32_t quarter_rep2(const uint32_t* s, const uint32_t (*seg32)[256], const uint8_t* row,
+                                                 int bank) {
+    const uint32_t* t0 = s + bank;
+    const uint32_t* t1 = s + 8192 + bank;
+    uint32_t c[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int ph = 0; ph < 2; ph++) {
+        v4u w[4];
+#pragma unroll
+        for (int g = 0; g < 4; g++) w[g] = *reinterpret_cast<const v4u*>(row + g * 32 + ph * 16);
+#pragma unroll
+        for (int d = 0; d < 4; d++) {
+#pragma unroll
+            for (int g = 0; g < 4; g++) c[g] ^= w[g][d];
+#pragma unroll
+            for (int h = 0; h < 2; h++)
+#pragma unroll
+                for (int g = 0; g < 4; g++)
+                    c[g] = x3(t0[(c[g] & 0xFF) * 32], t1[((c[g] >> 8) & 0xFF) * 32], c[g] >> 16);
+        }
+    }
+    if constexpr (!REFL) {
+#pragma unroll
+        for (int g = 0; g < 4; g++) c[g] = __builtin_bswap32(c[g]);
+    }
+    uint32_t q = c[0];
+#pragma unroll
+    for (int g = 1; g < 4; g++) q = apply_shift(seg32, q) ^ c[g];
+    return q;
+}
+
 // One byte through the register (tails): t0 = the classic table, read at
 // idx * STRIDE words (1 for slice tables, 32 for the replicated table).
-template <bool REFL, int STRIDE>
+template <bool REFL, int STRIDE, bool BSWAP = false>
 __device__ __forceinline__ uint32_t byte_step(const uint32_t* t0, uint32_t r, uint32_t b) {
-    return REFL ? t0[((r ^ b) & 0xFF) * STRIDE] ^ (r >> 8) : t0[(((r >> 24) ^ b) & 0xFF) * STRIDE] ^ (r << 8);
+    if constexpr (REFL) return t0[((r ^ b) & 0xFF) * STRIDE] ^ (r >> 8);
+    const uint32_t t = t0[(((r >> 24) ^ b) & 0xFF) * STRIDE];
+    return (BSWAP ? __builtin_bswap32(t) : t) ^ (r << 8);
 }
 
 // r -> shifted state from nibble tables t[8][16] (8 lookups instead of 4)
@@ -138,23 +188,28 @@ constexpr bool nib_shift(int scheme) { return scheme == 16 || scheme == 11; }
 
 // slice[8][256] (schemes 1, 16) | rep[256][32] (schemes 4, 8) ; shift[3][4][256]
 // (shift_nib[3][8][16] for scheme 16) ; seg[7][4][256] (schemes 4, 8)
+// scheme 22: rep[2][256][32] ; seg32[4][256] ; shift[3][4][256] (80 KiB)
 template <int SCHEME>
 struct TableLayout {
-    static constexpr int kMainWords = SCHEME == 11 ? 4 * 2048 + 2 * 1024 : sliced(SCHEME) ? 8 * 256 : 256 * 32;
+    static constexpr int kMainWords = SCHEME == 22   ? 2 * 256 * 32 + 4 * 256
+                                      : SCHEME == 11 ? 4 * 2048 + 2 * 1024
+                                      : sliced(SCHEME) ? 8 * 256
+                                                       : 256 * 32;
     static constexpr int kShiftOff = kMainWords;
     static constexpr int kShiftWords = nib_shift(SCHEME) ? 3 * 8 * 16 : 3 * 4 * 256;
     static constexpr int kSegOff = kShiftOff + kShiftWords;
-    static constexpr int kWords = kSegOff + (sliced(SCHEME) ? 0 : 7 * 4 * 256);
+    static constexpr int kWords = kSegOff + ((sliced(SCHEME) || SCHEME == 22) ? 0 : 7 * 4 * 256);
 };
 
 // Where the classic byte table (slice[0]) sits in a scheme's LDS image, for
 // byte-serial tails: slice[0][x] = t[off + x * stride].  Scheme 11 has no
-// byte table, but its field 5 (hi bits 22..31) holds it: byte 7 of the
-// step is field bits 2..9, so slice[0][x] = w11[5][x << 2].
+// byte table, but its field 5 (hi bits 24..31 + 0..1) holds it: byte 7 of
+// the step is field bits 0..7, so slice[0][x] = w11[5][x].
 template <int SCHEME>
 struct ByteTable {
-    static constexpr int off = SCHEME == 11 ? 9216 : 0;
-    static constexpr int stride = SCHEME == 11 ? 4 : sliced(SCHEME) ? 1 : 32;
+    static constexpr int off = SCHEME == 11 ? 9216 : SCHEME == 22 ? 8192 : 0;
+    static constexpr int stride = sliced(SCHEME) ? 1 : 32;
+    static constexpr bool bswap = SCHEME == 22;  // MSB-first kind: stored byte-swapped
 };
 
 // Moves quarter qi's linear CRC (qi < 3) to its place in the 512-B chunk.
@@ -168,9 +223,16 @@ __device__ __forceinline__ uint32_t shift_quarter(const uint32_t* s, int qi, uin
 
 // Fills a block's LDS table image (TableLayout<SCHEME>) from the constant
 // tables; caller synchronises.
-template <int SCHEME, int BS, typename T>
-__device__ __forceinline__ void stage_tables(uint32_t* s, const T& tab) {
-    if constexpr (SCHEME == 11) {
+template <int SCHEME, int BS, int KIND>
+__device__ __forceinline__ void stage_tables(uint32_t* s, const crc::Tables<KIND>& tab) {
+    if constexpr (SCHEME == 22) {
+        constexpr bool REFL = crc::Spec<KIND>::kReflected;
+        for (int t = threadIdx.x; t < 2 * 256 * 32; t += BS) {
+            const uint32_t v = tab.slice[1 - t / 8192][(t / 32) % 256];
+            s[t] = REFL ? v : __builtin_bswap32(v);
+        }
+        for (int t = threadIdx.x; t < 4 * 256; t += BS) s[2 * 256 * 32 + t] = (&tab.seg[5][0][0])[t];
+    } else if constexpr (SCHEME == 11) {
         constexpr int off[6] = {0, 2048, 4096, 5120, 7168, 9216}, len[6] = {2048, 2048, 1024, 2048, 2048, 1024};
 #pragma unroll
         for (int f = 0; f < 6; f++)
@@ -190,7 +252,9 @@ __device__ __forceinline__ void stage_tables(uint32_t* s, const T& tab) {
 // Linear part of the quarter at `row` under the block's LDS tables.
 template <int SCHEME, bool REFL>
 __device__ __forceinline__ uint32_t quarter(const uint32_t* s, const uint8_t* row, int lane) {
-    if constexpr (SCHEME == 11)
+    if constexpr (SCHEME == 22)
+        return quarter_rep2<REFL>(s, reinterpret_cast<const uint32_t(*)[256]>(s + 2 * 256 * 32), row, lane & 31);
+    else if constexpr (SCHEME == 11)
         return quarter_w11<REFL>(s, row);
     else if constexpr (sliced(SCHEME))
         return quarter_s8<REFL>(reinterpret_cast<const uint32_t(*)[256]>(s), row);

@@ -58,10 +58,12 @@ struct Tables {
     uint32_t seg[7][4][256]{};    // [i] = 16*(7-i) B: 112, 96, ..., 16
     uint32_t shift_nib[3][8][16]{};  // shift[] as nibble tables (1.5 KiB: the 1024-thread CRC kernel)
     // 11-bit slicing: the 8-byte step's 64 message bits (lo = bytes 0-3, hi =
-    // 4-7, little-endian) in six fields lo[0:11] lo[11:22] lo[22:32] hi[0:11]
-    // hi[11:22] hi[22:32]; w11[f][x] = XOR of the single-bit columns of the
-    // byte tables, slice[7 - j/8][1 << j%8] for message bit j.  6 lookups per
-    // 8 bytes instead of 8 (fields 2 and 5 use 1024 entries).
+    // 4-7, little-endian) in six fields, three per word w: w[2:13],
+    // w[13:24] and w[24:32] + w[0:2] (10 bits).  The fields sit where one
+    // VALU op turns a word into a table byte offset (index * 4): w & 0x1FFC,
+    // (w >> 11) & 0x1FFC, rotr(w, 22) & 0xFFC.  w11[f][x] = XOR of the
+    // single-bit columns of the byte tables, slice[7 - j/8][1 << j%8] for
+    // message bit j.  6 lookups per 8 bytes instead of 8.
     uint32_t w11[6][2048]{};
     uint32_t final512 = 0;
 
@@ -112,11 +114,13 @@ struct Tables {
                 }
         for (int i = 0; i < 7; i++) zero_shift_table(slice[0], 16 * (7 - i), seg[i]);
         for (int f = 0; f < 6; f++) {
-            const int j0 = (f / 3) * 32 + (f % 3) * 11, bits = (f % 3) == 2 ? 10 : 11;
+            const int word = f / 3, bits = (f % 3) == 2 ? 10 : 11;
             for (int x = 0; x < (1 << bits); x++) {
                 uint32_t v = 0;
-                for (int b = 0; b < bits; b++)
-                    if (x & (1 << b)) v ^= slice[7 - (j0 + b) / 8][1 << ((j0 + b) % 8)];
+                for (int b = 0; b < bits; b++) {
+                    const int j = 32 * word + (f % 3 == 0 ? 2 + b : f % 3 == 1 ? 13 + b : (24 + b) % 32);
+                    if (x & (1 << b)) v ^= slice[7 - j / 8][1 << (j % 8)];
+                }
                 w11[f][x] = v;
             }
         }

@@ -55,13 +55,16 @@ __device__ __forceinline__ const crc::Tables<KIND>& fused_tables() {
 //   VERIFY: checksummed shards 0..K-1 = the survivors; their expected sums
 //     sit at the same index (shard_id = survivor shard numbers), a mismatch
 //     sets bad[stripe * n_total + shard_id[s]].
-template <int K, int R, int SLABS, int SCHEME, int KIND, bool VERIFY>
-__global__ __launch_bounds__(crcdev::sliced(SCHEME) ? 256 : 512) __attribute__((amdgpu_waves_per_eu(2, 2))) void gf_fused_crc(
+template <int K, int R, int SLABS, int SCHEME, int KIND, bool VERIFY, int WPE = 2>
+__global__ __launch_bounds__(crcdev::sliced(SCHEME) ? 128 * WPE * (WPE - 1) : 512)
+    __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void gf_fused_crc(
     MatmulArgs a, FusedCrcArgs cs) {
     using TL = crcdev::TableLayout<SCHEME>;
     using Spec = crc::Spec<KIND>;
     constexpr bool REFL = Spec::kReflected;
-    constexpr int BS = crcdev::sliced(SCHEME) ? 256 : 512, WAVES = BS / 64;
+    // sliced schemes: WPE = 2 -> 256-thread blocks, two per CU; WPE = 3 ->
+    // one 768-thread block per CU (12 waves, 3 per SIMD)
+    constexpr int BS = crcdev::sliced(SCHEME) ? 128 * WPE * (WPE - 1) : 512, WAVES = BS / 64;
     constexpr int PITCH = 144, STAGE = 64 * PITCH, SPR = 8 / SLABS;
     constexpr int NSUM = VERIFY ? K : K + R;  // checksummed shards
     constexpr uint32_t WAVE_BYTES = SLABS * 1024u, TILE_BYTES = WAVES * WAVE_BYTES;
@@ -131,7 +134,7 @@ __global__ __launch_bounds__(crcdev::sliced(SCHEME) ? 256 : 512) __attribute__((
                 const uint32_t len = uint32_t(cell_len - cbyte);
                 uint32_t r = Spec::kInit;
                 for (uint32_t b = 0; b < len; b++)
-                    r = crcdev::byte_step<REFL, crcdev::ByteTable<SCHEME>::stride>(
+                    r = crcdev::byte_step<REFL, crcdev::ByteTable<SCHEME>::stride, crcdev::ByteTable<SCHEME>::bswap>(
                         s_ctabs + crcdev::ByteTable<SCHEME>::off, r, stage[(lane + b / 128) * PITCH + (b % 128)]);
                 val = r ^ Spec::kXorout;
             }
@@ -233,37 +236,53 @@ namespace {
 // 8 slabs per wave while the r x 8 accumulators fit (k <= 6, r <= 3), else 4
 constexpr int fused_slabs(int k, int r) { return (r <= 3 && k <= 6) ? 8 : 4; }
 
-template <int K, int R>
-const void* encode_fn(int slabs, int scheme) {
-#ifdef HEC_EXPERIMENTAL
-    // bank-replicated slicing-by-1, 4 chains (tune key 11 = 2): 7-10 % slower
-    // (profiles/r01_probe_fused_scheme.log)
-    if (scheme == 4)
-        return slabs == 4 ? reinterpret_cast<const void*>(&gf_fused_crc<K, R, 4, 4, crc::kCrc32c, false>)
-                          : reinterpret_cast<const void*>(&gf_fused_crc<K, R, 8, 4, crc::kCrc32c, false>);
-#endif
-    (void)scheme;
-    return slabs == 4 ? reinterpret_cast<const void*>(&gf_fused_crc<K, R, 4, 1, crc::kCrc32c, false>)
-                      : reinterpret_cast<const void*>(&gf_fused_crc<K, R, 8, 1, crc::kCrc32c, false>);
+template <int K, int R, int SCHEME, int WPE = 2>
+const void* encode_sl(int slabs) {
+    if constexpr (WPE == 3) return reinterpret_cast<const void*>(&gf_fused_crc<K, R, 4, SCHEME, crc::kCrc32c, false, 3>);
+    return slabs == 4 ? reinterpret_cast<const void*>(&gf_fused_crc<K, R, 4, SCHEME, crc::kCrc32c, false>)
+                      : reinterpret_cast<const void*>(&gf_fused_crc<K, R, 8, SCHEME, crc::kCrc32c, false>);
 }
 
-// verify: default slabs and lookup scheme only, both checksum kinds
-// (the 11-bit slicing of the CRC kernel, scheme 11, was measured here too and
-// lost: profiles/r01d_probe_fused_w11_*.log)
+template <int K, int R, int SCHEME, int WPE = 2>
+const void* verify_kind(int kind) {
+    constexpr int SL = WPE == 3 ? 4 : fused_slabs(K, R);
+    return kind == crc::kCrc32c ? reinterpret_cast<const void*>(&gf_fused_crc<K, R, SL, SCHEME, crc::kCrc32c, true, WPE>)
+                                : reinterpret_cast<const void*>(&gf_fused_crc<K, R, SL, SCHEME, crc::kCksum, true, WPE>);
+}
+
+// scheme 11 (default) = 11-bit slicing, 1 = slicing-by-8 (tune key 11 = 1)
 template <int K, int R>
-const void* verify_fn(int kind, int) {
-    constexpr int SL = fused_slabs(K, R);
-    return kind == crc::kCrc32c ? reinterpret_cast<const void*>(&gf_fused_crc<K, R, SL, 1, crc::kCrc32c, true>)
-                                : reinterpret_cast<const void*>(&gf_fused_crc<K, R, SL, 1, crc::kCksum, true>);
+const void* encode_fn(int slabs, int scheme, int wpe) {
+#ifdef HEC_EXPERIMENTAL
+    // rejected (same-box A/B, profiles/r01_probe_fused_scheme.log,
+    // r02_probe_fused_rep2.log, r02_probe_fused_wpe3_*.log):
+    // bank-replicated slicing-by-1 (4 chains) and slicing-by-2 (tune key 11
+    // = 2 / 6), one 768-thread block per CU at 3 waves per SIMD (key 16 = 3)
+    if (scheme == 4) return encode_sl<K, R, 4>(slabs);
+    if (scheme == 22) return encode_sl<K, R, 22>(slabs);
+    if (wpe == 3) return scheme == 11 ? encode_sl<K, R, 11, 3>(slabs) : encode_sl<K, R, 1, 3>(slabs);
+#endif
+    (void)wpe;
+    return scheme == 11 ? encode_sl<K, R, 11>(slabs) : encode_sl<K, R, 1>(slabs);
+}
+
+template <int K, int R>
+const void* verify_fn(int kind, int scheme, int wpe) {
+#ifdef HEC_EXPERIMENTAL
+    if (scheme == 22) return verify_kind<K, R, 22>(kind);
+    if (wpe == 3) return scheme == 11 ? verify_kind<K, R, 11, 3>(kind) : verify_kind<K, R, 1, 3>(kind);
+#endif
+    (void)wpe;
+    return scheme == 11 ? verify_kind<K, R, 11>(kind) : verify_kind<K, R, 1>(kind);
 }
 
 template <int K>
-const void* pick_r(bool verify, int r, int slabs, int scheme, int kind) {
+const void* pick_r(bool verify, int r, int slabs, int scheme, int kind, int wpe) {
     switch (r) {
-        case 1: return verify ? verify_fn<K, 1>(kind, scheme) : encode_fn<K, 1>(slabs, scheme);
-        case 2: return verify ? verify_fn<K, 2>(kind, scheme) : encode_fn<K, 2>(slabs, scheme);
-        case 3: return verify ? verify_fn<K, 3>(kind, scheme) : encode_fn<K, 3>(slabs, scheme);
-        default: return verify ? verify_fn<K, 4>(kind, scheme) : encode_fn<K, 4>(slabs, scheme);
+        case 1: return verify ? verify_fn<K, 1>(kind, scheme, wpe) : encode_fn<K, 1>(slabs, scheme, wpe);
+        case 2: return verify ? verify_fn<K, 2>(kind, scheme, wpe) : encode_fn<K, 2>(slabs, scheme, wpe);
+        case 3: return verify ? verify_fn<K, 3>(kind, scheme, wpe) : encode_fn<K, 3>(slabs, scheme, wpe);
+        default: return verify ? verify_fn<K, 4>(kind, scheme, wpe) : encode_fn<K, 4>(slabs, scheme, wpe);
     }
 }
 
@@ -278,21 +297,29 @@ int launch_fused(const MatmulArgs& in, const FusedCrcArgs& cs, bool verify, int 
     for (int j = 0; j < a.r; j++)
         aligned &= ((reinterpret_cast<uintptr_t>(a.out[j]) | a.out_stride[j]) & 15u) == 0;
     if (cs.kind != crc::kCrc32c && (cs.kind != crc::kCksum || !verify)) return -1;
-    const int slabs = verify                                               ? fused_slabs(a.k, a.r)
+    const int slabs = tn.fused_wpe == 3                                    ? 4
+                      : verify                                               ? fused_slabs(a.k, a.r)
                       : (tn.fused_slabs == 4 || tn.fused_slabs == 8) ? tn.fused_slabs
                                                                              : fused_slabs(a.k, a.r);
-    // checksum lookups (checksum_device.hpp): slicing-by-8 in 256-thread
-    // blocks, 2 per CU, beats the bank-replicated tables in 512-thread blocks
-    // by 7-10 % here (profiles/r01_probe_fused_scheme.log); tune key 11 = 2
-    // selects the latter for encode
-    const int scheme = (!verify && tn.crc_variant == 2) ? 4 : 1;
-    const int waves = crcdev::sliced(scheme) ? 4 : 8;
+    // checksum lookups (checksum_device.hpp): 11-bit slicing (6 lookups per
+    // 8 bytes) by default, slicing-by-8 on tune key 11 = 1; both in 256-thread
+    // blocks, 2 per CU.  Same-box A/B (profiles/r02_probe_fused_w11_*.log):
+    // encode + CRC 5-7 % faster with 11-bit slicing, decode + verify within
+    // +-1 %.  The kernel is bound by its VALU/issue stream more than by the
+    // LDS: the bank-replicated tables (conflict-free, half the LDS cycles,
+    // 1.5x the VALU) lose 10-20 % (r02_probe_fused_rep2.log).
+    const int scheme = (!verify && tn.crc_variant == 2) ? 4
+                       : tn.crc_variant == 6            ? 22
+                       : tn.crc_variant == 1            ? 1
+                                                        : 11;
+    const int wpe = (tn.fused_wpe == 3 && crcdev::sliced(scheme)) ? 3 : 2;
+    const int waves = !crcdev::sliced(scheme) ? 8 : wpe == 3 ? 12 : 4;
     const void* fn = nullptr;
     switch (a.k) {
-        case 2: fn = pick_r<2>(verify, a.r, slabs, scheme, cs.kind); break;
-        case 3: fn = pick_r<3>(verify, a.r, slabs, scheme, cs.kind); break;
-        case 6: fn = pick_r<6>(verify, a.r, slabs, scheme, cs.kind); break;
-        case 10: fn = pick_r<10>(verify, a.r, slabs, scheme, cs.kind); break;
+        case 2: fn = pick_r<2>(verify, a.r, slabs, scheme, cs.kind, wpe); break;
+        case 3: fn = pick_r<3>(verify, a.r, slabs, scheme, cs.kind, wpe); break;
+        case 6: fn = pick_r<6>(verify, a.r, slabs, scheme, cs.kind, wpe); break;
+        case 10: fn = pick_r<10>(verify, a.r, slabs, scheme, cs.kind, wpe); break;
         default: return -1;
     }
     if (!aligned) return -1;
@@ -310,7 +337,7 @@ int launch_fused(const MatmulArgs& in, const FusedCrcArgs& cs, bool verify, int 
     // a grid of 8 blocks per CU (2 or 1 resident): finer-grained dynamic
     // scheduling beats exactly the resident blocks by 3 % (RS(6,3)) to 5 %
     // (RS(10,4))
-    uint64_t grid = tn.grid ? uint64_t(tn.grid) : uint64_t(num_cus(device)) * 8;
+    uint64_t grid = tn.grid ? uint64_t(tn.grid) : uint64_t(num_cus(device)) * (wpe == 3 ? 4 : 8);
     if (grid > total) grid = total;
     FusedCrcArgs c = cs;
     void* args[] = {&a, &c};

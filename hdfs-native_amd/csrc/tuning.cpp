@@ -46,6 +46,7 @@ Tune tune_snapshot() {
     t.store_pol = load(13);
     t.host_copy_threads = load(14);
     t.burst_tiles = load(15);
+    t.fused_wpe = load(16);
     return t;
 }
 
@@ -66,12 +67,13 @@ int tune_store(int key, int value) {
         case 10: ok = value == 0 || value == 4 || value == 8; break;
         case 11:
             ok = value == 0 || value == 1 || value == 5 ||
-                 (kExperimental && (value == 2 || value == 3 || value == 4 || value == 9));
+                 (kExperimental && (value == 2 || value == 3 || value == 4 || value == 6 || value == 9));
             break;
         case 12: ok = value >= 0 && value <= 2; break;
         case 13: ok = kExperimental && value >= 0 && value <= 4; break;
         case 14: ok = value >= 0 && value <= 64; break;
         case 15: ok = kExperimental && (value == 0 || value == 2 || value == 3); break;
+        case 16: ok = value == 0 || value == 2 || (kExperimental && value == 3); break;
         default: ok = false;
     }
     if (!ok) return HEC_ERR_INVALID_ARG;

@@ -1,7 +1,8 @@
 """Measurement tool (GPU box): fused encode + CRC32C (hec_encode_crc_device)
 and fused decode + verify (hec_decode_verify_device) across CRC lookup
-schemes (tune key 11: 0/1 = slicing-by-8, 2 = bank-replicated (encode only),
-5 = 11-bit slicing), interleaved rounds, median per variant.  Every variant's
+schemes (tune key 11: 0/1 = slicing-by-8, 2 = bank-replicated (encode only, exp
+library), 5 = 11-bit slicing; suffix w = tune key 16 = 3, one 768-thread
+block per CU), interleaved rounds, median per variant.  Every variant's
 sums are checked against the default's.
 
   PROBE_K=6 PROBE_M=3 PROBE_S=1024 python scripts/probe_fused.py
@@ -21,8 +22,8 @@ S = int(os.environ.get("PROBE_S", "1024"))
 CELL = 1 << 20
 REPS = int(os.environ.get("PROBE_REPS", "10"))
 ROUNDS = int(os.environ.get("PROBE_ROUNDS", "5"))
-ENC = [int(v) for v in os.environ.get("PROBE_ENC", "1,2,5").split(",")]
-VER = [int(v) for v in os.environ.get("PROBE_VER", "1,5").split(",")]
+ENC = os.environ.get("PROBE_ENC", "1,5,5w").split(",")  # "<key 11 value>[w]": w = key 16 = 3 (768-thread blocks, 3 waves per SIMD)
+VER = os.environ.get("PROBE_VER", "1,5,5w").split(",")
 BPC = 512
 dev = torch.device("cuda:0")
 g = torch.Generator(device=dev).manual_seed(3)
@@ -62,7 +63,8 @@ variants = [("encode+crc", v, enc) for v in ENC] + [("decode+verify", v, ver) fo
 times = {(n, v): [] for n, v, _ in variants}
 for _ in range(ROUNDS):
     for name, v, fn in variants:
-        H.tune_set(11, v)
+        H.tune_set(11, int(v.rstrip("w")))
+        H.tune_set(16, 3 if v.endswith("w") else 0)
         fn()
         torch.cuda.synchronize()
         if name == "encode+crc":
@@ -77,6 +79,7 @@ for _ in range(ROUNDS):
         torch.cuda.synchronize()
         times[(name, v)].append(ev[0].elapsed_time(ev[1]) / REPS)
 H.tune_set(11, 0)
+H.tune_set(16, 0)
 print(f"RS({K},{M}) S={S} cell={CELL}")
 for (name, v), t in times.items():
     ms = statistics.median(t)

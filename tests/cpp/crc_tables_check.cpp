@@ -6,7 +6,7 @@
 //         "append 384/256/128 zero bytes" byte tables, + final512;
 //   w11 : the same quarters by 11-bit slicing, placed with the nibble tables;
 //   byte: the classic byte-serial loop, from the table slot the 11-bit
-//         scheme's tail reads (w11[5][x << 2]);
+//         scheme's tail reads (w11[5][x]);
 // and printed as hex, one line per chunk, for tests/test_oracle.py to compare
 // with the oracle.  Input: splitmix64 bytes (seed argv[1], chunks argv[2]).
 #include <cstdint>
@@ -44,12 +44,16 @@ struct Check {
         }
         return r;
     }
+    // the 11-bit fields of a word: w[2:13], w[13:24], w[24:32] + w[0:2]
+    static uint32_t f0(uint32_t w) { return (w >> 2) & 0x7FF; }
+    static uint32_t f1(uint32_t w) { return (w >> 13) & 0x7FF; }
+    static uint32_t f2(uint32_t w) { return (w >> 24) | ((w & 3u) << 8); }
     uint32_t q_w11(const uint8_t* q) const {
         uint32_t r = 0;
         for (int i = 0; i < 128; i += 8) {
             const uint32_t lo = le32(q + i) ^ pre(r), hi = le32(q + i + 4);
-            r = t.w11[0][lo & 0x7FF] ^ t.w11[1][(lo >> 11) & 0x7FF] ^ t.w11[2][lo >> 22] ^ t.w11[3][hi & 0x7FF] ^
-                t.w11[4][(hi >> 11) & 0x7FF] ^ t.w11[5][hi >> 22];
+            r = t.w11[0][f0(lo)] ^ t.w11[1][f1(lo)] ^ t.w11[2][f2(lo)] ^ t.w11[3][f0(hi)] ^ t.w11[4][f1(hi)] ^
+                t.w11[5][f2(hi)];
         }
         return r;
     }
@@ -74,7 +78,7 @@ struct Check {
         uint32_t r = Spec<KIND>::kInit;
         for (int i = 0; i < 512; i++) {
             const uint32_t idx = REFL ? ((r ^ c[i]) & 0xFF) : (((r >> 24) ^ c[i]) & 0xFF);
-            r = REFL ? (t.w11[5][idx << 2] ^ (r >> 8)) : (t.w11[5][idx << 2] ^ (r << 8));
+            r = REFL ? (t.w11[5][idx] ^ (r >> 8)) : (t.w11[5][idx] ^ (r << 8));
         }
         return r ^ Spec<KIND>::kXorout;
     }

@@ -117,10 +117,10 @@ def _oracle_sums(cells, bpc, ctype=H.CHECKSUM_CRC32C):
 
 @pytest.mark.parametrize("ctype", [H.CHECKSUM_CRC32C, H.CHECKSUM_CRC32])
 @pytest.mark.parametrize("cell,bpc,n", [(512 * 64, 512, 3), (512 * 70 + 256, 512, 2), (1000, 512, 3)])
-@pytest.mark.parametrize("variant,pf", [(2, 2), (3, 1), (3, 2), (4, 0)])
+@pytest.mark.parametrize("variant,pf", [(2, 2), (3, 1), (3, 2), (4, 0), (6, 1), (6, 2)])
 def test_crc_schemes_vs_oracle(xlib, dev, ctype, cell, bpc, n, variant, pf):
-    """Bank-replicated slicing-by-1 (4 / 8 chains) and slicing-by-8 at 4
-    waves per SIMD (tune key 11 = 2, 3, 4)."""
+    """Bank-replicated slicing-by-1 (4 / 8 chains), slicing-by-8 at 4 waves
+    per SIMD and bank-replicated slicing-by-2 (tune key 11 = 2, 3, 4, 6)."""
     cells = batch_data(3, n, cell, first=cell + bpc + ctype + variant)
     H.tune_set(11, variant, xlib)
     H.tune_set(12, pf, xlib)
@@ -133,9 +133,15 @@ def test_crc_schemes_vs_oracle(xlib, dev, ctype, cell, bpc, n, variant, pf):
     assert np.array_equal(got.cpu().numpy(), _oracle_sums(cells, bpc, ctype))
 
 
+FUSED_TUNES = [[(11, 2)], [(11, 6)], [(16, 3)], [(16, 3), (11, 1)]]
+
+
 @pytest.mark.parametrize("k,m,cell,S", [(6, 3, 1 << 16, 3), (10, 4, 1 << 15, 2), (3, 2, 8192 + 512, 4)])
-def test_fused_replicated_crc_vs_oracle(xlib, dev, c_oracle, k, m, cell, S):
-    """Fused encode + CRC32C with the bank-replicated tables (tune key 11 = 2)."""
+@pytest.mark.parametrize("tunes", FUSED_TUNES)
+def test_fused_variants_encode_vs_oracle(xlib, dev, c_oracle, k, m, cell, S, tunes):
+    """Fused encode + CRC32C with the rejected variants: bank-replicated
+    slicing-by-1 / -by-2 tables (tune key 11 = 2 / 6) and one 768-thread
+    block per CU (key 16 = 3, 11-bit slicing or slicing-by-8)."""
     bpc = 512
     data = batch_data(S, k, cell, first=77 + cell)
     par = oracle_batch_encode(c_oracle, k, m, data)
@@ -145,12 +151,50 @@ def test_fused_replicated_crc_vs_oracle(xlib, dev, c_oracle, k, m, cell, S):
     sums = torch.zeros((S, k + m, nch, 4), dtype=torch.uint8, device=dev)
     dp, ds = H.stripe_layout_ptrs(d, k)
     pp, ps = H.stripe_layout_ptrs(p, m)
-    H.tune_set(11, 2, xlib)
+    for key, value in tunes:
+        H.tune_set(key, value, xlib)
     try:
         xcoder(xlib, k, m).encode_crc_device(dp, ds, pp, ps, cell, S, bpc, sums.data_ptr(),
                                               torch.cuda.current_stream().cuda_stream)
         torch.cuda.synchronize()
     finally:
-        H.tune_set(11, 0, xlib)
+        for key, _ in tunes:
+            H.tune_set(key, 0, xlib)
     assert np.array_equal(p.cpu().numpy(), par)
     assert np.array_equal(sums.cpu().numpy(), _oracle_sums(np.concatenate([data, par], axis=1), bpc))
+
+
+@pytest.mark.parametrize("ctype", [H.CHECKSUM_CRC32C, H.CHECKSUM_CRC32])
+@pytest.mark.parametrize("k,m,cell,S", [(6, 3, 1 << 15, 3), (10, 4, 1 << 14, 2)])
+@pytest.mark.parametrize("tunes", [t for t in FUSED_TUNES if t != [(11, 2)]])
+def test_fused_variants_verify_vs_oracle(xlib, dev, c_oracle, ctype, k, m, cell, S, tunes):
+    """Fused decode + verify with the rejected variants: data shard 0 missing,
+    one survivor byte of stripe 1 corrupted -> flagged, re-planned, rebuilt."""
+    bpc = 512
+    data = batch_data(S, k, cell, first=91 + cell + ctype)
+    par = oracle_batch_encode(c_oracle, k, m, data)
+    sums = torch.from_numpy(_oracle_sums(np.concatenate([data, par], axis=1), bpc, ctype)).to(dev)
+    bent = data.copy()
+    bent[1, 2, cell // 3] ^= 0x21
+    d, p = torch.from_numpy(bent).to(dev), torch.from_numpy(par).to(dev)
+    out = torch.zeros_like(d)
+    bad = torch.zeros((S, k + m), dtype=torch.uint8, device=dev)
+    dp, ds = H.stripe_layout_ptrs(d, k)
+    pp, ps = H.stripe_layout_ptrs(p, m)
+    op, os_ = H.stripe_layout_ptrs(out, k)
+    for key, value in tunes:
+        H.tune_set(key, value, xlib)
+    try:
+        xcoder(xlib, k, m).decode_verify_device(ctype, [None] + dp[1:] + pp, ds + ps, op, os_, cell, S, bpc,
+                                                sums.data_ptr(), bad.data_ptr(),
+                                                torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+    finally:
+        for key, _ in tunes:
+            H.tune_set(key, 0, xlib)
+    o, b = out.cpu().numpy(), bad.cpu().numpy()
+    want_bad = np.zeros((S, k + m), dtype=np.uint8)
+    want_bad[1, 2] = 1
+    assert np.array_equal(b, want_bad)
+    assert np.array_equal(o[:, 0], data[:, 0])
+    assert np.array_equal(o[1, 2], data[1, 2])

@@ -320,7 +320,7 @@ def test_tune_set_concurrent_with_launches(dev, c_oracle):
 
 def test_experimental_keys_rejected_by_default_library():
     # the rejected variants exist only in lib/libhdfs_ec_amd_exp.so
-    for key, value in [(5, 3), (5, 4), (5, 5), (13, 1), (15, 2), (11, 2), (11, 9), (6, 3), (16, 1)]:
+    for key, value in [(5, 3), (5, 4), (5, 5), (13, 1), (15, 2), (11, 2), (11, 6), (11, 9), (6, 3), (16, 1), (16, 3)]:
         with pytest.raises(ValueError):
             H.tune_set(key, value)
 
@@ -593,9 +593,11 @@ def test_crc32c_device_published_vector(dev):
     ("rs", 10, 4, 1 << 15, 3), ("rs", 10, 4, 70 * 512 + 256, 2), ("rs", 3, 2, 1 << 17, 3),
     ("rs", 2, 1, 8192 + 512, 4), ("rs", 12, 4, 1 << 14, 2), ("rs", 6, 3, 1000, 2), ("xor", 2, 1, 1 << 14, 3)])
 @pytest.mark.parametrize("fused", [0, 4, 8, None])
-def test_encode_crc_device(dev, c_oracle, codec, k, m, cell, S, fused, scheme=0):
+@pytest.mark.parametrize("scheme", [0, 1])
+def test_encode_crc_device(dev, c_oracle, codec, k, m, cell, S, fused, scheme):
     """Fused encode+CRC (k in {2,3,6,10}) and the two-pass fallback (other k,
-    unaligned cell_len, or tune key 9) against oracle parity + oracle CRCs."""
+    unaligned cell_len, or tune key 9) against oracle parity + oracle CRCs;
+    scheme = tune key 11 (0: 11-bit slicing, 1: slicing-by-8)."""
     bpc = 512
     data = batch_data(S, k, cell, first=31 + cell)
     if codec == "xor":
@@ -739,11 +741,13 @@ def _verified_read_expect(k, m, data, parity, missing, missing_parity, sums_np, 
     (10, 4, 1 << 14, 512, [0, 1, 2, 3], []), (10, 4, 1 << 13, 512, [7], [0]), (3, 2, 1 << 14, 512, [1], []),
     (2, 1, 8192, 512, [0], []), (12, 4, 1 << 13, 512, [2, 5], []), (6, 3, 3000, 100, [0, 5], []),
     (6, 3, 4096 + 16, 4096, [3], [])])
-def test_decode_verify_vs_oracle(dev, c_oracle, ctype, k, m, cell, bpc, missing, missing_parity):
+@pytest.mark.parametrize("scheme", [0, 1])
+def test_decode_verify_vs_oracle(dev, c_oracle, ctype, k, m, cell, bpc, missing, missing_parity, scheme):
     """Fused (k in {2,3,6,10}, 512-B chunks) and two-pass decode+verify: clean
     stripes, corrupt survivors (data and parity), a stripe that runs out of
     verified shards; rebuilt data, bad flags and the error all as the
-    oracle's read_slice restatement."""
+    oracle's read_slice restatement.  scheme = tune key 11 (0: 11-bit
+    slicing, 1: slicing-by-8)."""
     S = 6
     data = batch_data(S, k, cell, first=5 + cell + k)
     parity = oracle_batch_encode(c_oracle, k, m, data)
@@ -775,10 +779,14 @@ def test_decode_verify_vs_oracle(dev, c_oracle, ctype, k, m, cell, bpc, missing,
     op, os_ = H.stripe_layout_ptrs(out, k)
     ptrs = [None if i in missing else dp[i] for i in range(k)] + \
         [None if j in missing_parity else pp[j] for j in range(m)]
-    with pytest.raises(H.ErasureCodingError):
-        cod.decode_verify_device(ctype, ptrs, ds + ps, op, os_, cell, S, bpc, sums.data_ptr(), bad.data_ptr(),
-                                 torch.cuda.current_stream().cuda_stream)
-    torch.cuda.synchronize()
+    H.tune_set(11, scheme)
+    try:
+        with pytest.raises(H.ErasureCodingError):
+            cod.decode_verify_device(ctype, ptrs, ds + ps, op, os_, cell, S, bpc, sums.data_ptr(), bad.data_ptr(),
+                                     torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+    finally:
+        H.tune_set(11, 0)
     o, b = out.cpu().numpy(), bad.cpu().numpy()
     for s in range(S):
         if not oks[s]:
