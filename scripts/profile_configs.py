@@ -37,6 +37,16 @@ CONFIGS = {
     "c64k": (["--cell", "65536", "--stripes", "65536"], 6, 3, 65536, 65536, 2),
 }
 KERNEL_RE = "gf_matmul"
+# the checksum kernels, from bench.py --crc (RS(6,3) 1 MiB x 1024): the fused
+# encode + CRC32C and decode + verify kernels and the CRC-only kernel; per
+# kernel name, bytes per launch = the line's TB/s x ms for that leg
+CRC_CONFIGS = {"crc63": (["--crc", "--corrupt", ""], 6, 3, 1 << 20, 1024)}
+CRC_RE = "gf_fused_crc|checksum_chunks512"
+CRC_LEGS = [  # kernel-name test, leg ms key, leg TB/s key (bytes = TB/s x ms)
+    (lambda n, k, m: f"gf_fused_crc<{k}, {m}, " in n and "false" in n, "encode_crc_ms", "encode_crc_hbm_TBps"),
+    (lambda n, k, m: f"gf_fused_crc<{k}, {m}, " in n and "true" in n, "decode_verify_ms", "decode_verify_hbm_TBps"),
+    (lambda n, k, m: "checksum_chunks512" in n, "crc_only_ms", None),
+]
 
 
 def run(cmd, log, limit):
@@ -63,9 +73,9 @@ def bench_line(log):
     raise SystemExit(f"no bench line in {log}")
 
 
-def counter(d, name):
+def counter(d, name, match=lambda n: KERNEL_RE in n):
     vals = [float(r["Counter_Value"]) for r in rows(d, "*counter_collection.csv")
-            if KERNEL_RE in r.get("Kernel_Name", "") and r.get("Counter_Name") == name]
+            if match(r.get("Kernel_Name", "")) and r.get("Counter_Name") == name]
     if not vals:
         raise SystemExit(f"no {name} rows under {d}")
     return vals
@@ -126,10 +136,73 @@ def profile(out, name):
           f"traffic x{res['traffic_over_algorithmic']}", flush=True)
 
 
+def profile_crc(out, name):
+    args, k, m, cell, stripes = CRC_CONFIGS[name]
+    d = os.path.join(out, name)
+    os.makedirs(d, exist_ok=True)
+    bench = ["python3", "bench.py"] + args + COMMON
+    prof = ["rocprofv3", "--kernel-trace", "--stats", "-d", os.path.join(d, "trace"), "-o", "run",
+            "--output-format", "csv", "--"]
+    run(prof + bench, os.path.join(d, "bench_trace.log"), 400)
+    line = bench_line(os.path.join(d, "bench_trace.log"))
+    crc = line["crc32c"]
+    for cnt in ("FETCH_SIZE", "WRITE_SIZE"):
+        pmc = ["rocprofv3", "--pmc", cnt, "--kernel-include-regex", CRC_RE, "-d",
+               os.path.join(d, cnt.lower()), "-o", "run", "--output-format", "csv", "--"]
+        run(pmc + bench, os.path.join(d, f"bench_{cnt.lower()}.log"), 400)
+    trace = [r for r in rows(os.path.join(d, "trace"), "*kernel_trace.csv")]
+    for match, ms_key, tb_key in CRC_LEGS:
+        mine = sorted((r for r in trace if match(r.get("Kernel_Name", ""), k, m)), key=lambda r: int(r["Dispatch_Id"]))
+        if not mine:
+            raise SystemExit(f"{name}: no dispatch for {ms_key}")
+        algo = (k + m) * cell * stripes if tb_key is None else round(crc[tb_key] * 1e12 * crc[ms_key] * 1e-3)
+
+        def per_dispatch(cnt):  # counter value per dispatch, in dispatch order
+            got = {}
+            for r in rows(os.path.join(d, cnt.lower()), "*counter_collection.csv"):
+                if match(r.get("Kernel_Name", ""), k, m) and r.get("Counter_Name") == cnt:
+                    got[int(r["Dispatch_Id"])] = got.get(int(r["Dispatch_Id"]), 0.0) + float(r["Counter_Value"])
+            return [got[i] for i in sorted(got)]
+        fetch_all = [2.0 * 1024 * v for v in per_dispatch("FETCH_SIZE")]
+        write_all = [1024.0 * v for v in per_dispatch("WRITE_SIZE")]
+        if not (len(fetch_all) == len(write_all) == len(mine)):
+            raise SystemExit(f"{name}: {ms_key}: {len(mine)} traced vs {len(fetch_all)}/{len(write_all)} PMC dispatches")
+        # the same kernel also runs over other cell sets in other legs (the
+        # unfused verify pass checks k cells): keep the dispatches whose HBM
+        # bytes are this leg's (same dispatch order in all three runs)
+        keep = [i for i in range(len(mine)) if abs(fetch_all[i] + write_all[i] - algo) < 0.03 * algo]
+        if not keep:
+            raise SystemExit(f"{name}: {ms_key}: no dispatch moves the leg's bytes")
+        durs = [(int(mine[i]["End_Timestamp"]) - int(mine[i]["Start_Timestamp"])) * 1e-9 for i in keep]
+        avg = sum(durs) / len(durs)
+        fetch_b = sum(fetch_all[i] for i in keep) / len(keep)
+        write_b = sum(write_all[i] for i in keep) / len(keep)
+        fetch = write = keep
+        res = {
+            "config": f"{name}:{ms_key[:-3]}", "args": " ".join(args + COMMON), "k": k, "m": m, "cell": cell,
+            "stripes": stripes, "kernel": sorted({mine[i]["Kernel_Name"] for i in keep}),
+            "dispatches": len(durs), "dispatches_of_kernel": len(mine),
+            "avg_launch_ms_all": round(avg * 1e3, 4), "leg_ms": crc[ms_key],
+            "kernel_within_leg": avg * 1e3 <= crc[ms_key] * 1.02,
+            "algorithmic_bytes_per_launch": algo, "frac_from_trace": round(algo / avg / PEAK, 4),
+            "fetch_bytes_per_launch": fetch_b, "write_bytes_per_launch": write_b,
+            "hbm_bytes_per_launch": fetch_b + write_b,
+            "traffic_over_algorithmic": round((fetch_b + write_b) / algo, 5),
+            "pmc_dispatches": {"fetch": len(fetch), "write": len(write)},
+            "corrections": "FETCH_SIZE KiB x1024 x2 (gfx950 half-count on 16B/lane streaming reads); WRITE_SIZE KiB x1024",
+            "crc_leg": crc,
+        }
+        with open(os.path.join(out, "summary_crc.jsonl"), "a") as f:
+            f.write(json.dumps(res) + "\n")
+        print(f"{res['config']}: kernel {avg * 1e3:.4f} ms (leg {crc[ms_key]} ms) frac trace {res['frac_from_trace']} "
+              f"traffic x{res['traffic_over_algorithmic']}", flush=True)
+
+
 def write_traffic(out, tag):
     """pmc_traffic_configs.json: what bench.py reads for roofline.traffic
     (matched on k, m, cell, stripes and decode mode)."""
-    rows = [json.loads(ln) for ln in open(os.path.join(out, "summary.jsonl"))]
+    path = os.path.join(out, "summary.jsonl")
+    rows = [json.loads(ln) for ln in open(path)] if os.path.exists(path) else []
     cfgs = [{"config": r["config"], "k": r["k"], "m": r["m"], "cell": r["cell"], "stripes": r["stripes"],
              "decode_mode": "uniform", "kernel": r["kernel"],
              "fetch_bytes_per_launch": r["fetch_bytes_per_launch"], "write_bytes_per_launch": r["write_bytes_per_launch"],
@@ -142,11 +215,11 @@ def write_traffic(out, tag):
 
 def main():
     out = sys.argv[1]
-    names = sys.argv[2:] or list(CONFIGS)
+    names = sys.argv[2:] or list(CONFIGS) + list(CRC_CONFIGS)
     os.makedirs(out, exist_ok=True)
     os.environ["TMPDIR"] = "/tmp"
     for n in names:
-        profile(out, n)
+        (profile_crc if n in CRC_CONFIGS else profile)(out, n)
     write_traffic(out, os.path.basename(os.path.normpath(out)))
     print("profile_configs ok", flush=True)
 
