@@ -15,6 +15,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <fstream>
 #include <map>
 #include <memory>
@@ -31,6 +32,7 @@
 #include "checksum.hpp"
 #include "checksum_tables.hpp"
 #include "ec_kernels.hpp"
+#include "copy_pool.hpp"
 #include "gf256.hpp"
 
 namespace {
@@ -57,6 +59,7 @@ struct DecodePlan {
     std::vector<size_t> survivors;  // k
     std::vector<size_t> missing;    // e
     std::vector<uint8_t> matrix;    // e x k
+    std::vector<uint32_t> perm;     // e x k x 8: the matrix's v_perm product tables (mixed-decode plan blobs)
 };
 
 // Restores the caller's current HIP device on scope exit.
@@ -108,10 +111,18 @@ struct hec_coder {
     uint8_t* call_dev = nullptr;
     size_t call_bytes = 0;
     hipEvent_t ev_call[kCallEvents] = {};
+    std::unique_ptr<hec::CopyPool> call_pool;  // the per-call copies' worker threads (lazy)
     // verified read, phase 2: stripe lists + mixed-decode workspace (device),
     // grown geometrically, released by hec_coder_destroy
     uint8_t* verify_ws = nullptr;
     size_t verify_ws_bytes = 0;
+    // mixed decode: two pinned staging images for the workspace upload (so
+    // the H2D is a real async DMA), each reused once its copy has run
+    std::mutex mixed_mu;
+    uint8_t* mixed_host[2] = {nullptr, nullptr};
+    size_t mixed_host_bytes[2] = {0, 0};
+    hipEvent_t ev_mixed[2] = {nullptr, nullptr};
+    int mixed_next = 0;
 };
 
 namespace {
@@ -147,6 +158,11 @@ DecodePlan compute_plan(size_t k, size_t m, const uint8_t* present, const std::v
     p.matrix.resize(p.missing.size() * k);
     for (size_t r = 0; r < p.missing.size(); r++)  // select_rows(invalid), ascending
         std::memcpy(&p.matrix[r * k], &sub[p.missing[r] * k], k);
+    p.perm.resize(p.matrix.size() * 8);
+    for (size_t x = 0; x < p.matrix.size(); x++) {
+        const auto w = hec::perm_table_words(p.matrix[x]);
+        std::memcpy(&p.perm[x * 8], w.data(), sizeof(uint32_t) * 8);
+    }
     return p;
 }
 
@@ -242,12 +258,22 @@ int ensure_call_staging(hec_coder* c, size_t bytes) {
     return HEC_OK;
 }
 
+// The coder's copy workers for a per-call row of `shards` shards: tune key
+// 14 threads (default 4), at most one per shard; null when one would do.
+hec::CopyPool* call_pool(hec_coder* c, size_t shards) {
+    const int tuned = hec::tune_snapshot().host_copy_threads;
+    const int want = int(std::min<size_t>(shards, tuned > 0 ? size_t(tuned) : 4));
+    if (want < 2) return nullptr;
+    if (!c->call_pool) c->call_pool = std::make_unique<hec::CopyPool>();
+    return c->call_pool->ensure(want) >= 2 ? c->call_pool.get() : nullptr;
+}
+
 // One row through the device, pageable caller buffers in and out:
 //   out[j] = sum_i mat[j*nin + i] * in[i], n bytes each.
-// Inputs are copied into the pinned bounce buffer shard by shard, each
-// shard's H2D DMA issued as soon as it is there (the next memcpy overlaps
-// it); outputs come back D2H shard by shard and each is copied out while the
-// next one is still in flight.  No allocation on the hot path.
+// Inputs are copied into the pinned bounce buffer by the coder's copy
+// workers, several shards at once, and each shard's H2D DMA is issued as
+// soon as its copy is there; outputs come back D2H shard by shard and the
+// workers copy each out once its DMA is done.  No allocation on the hot path.
 int call_through_device(hec_coder* c, const uint8_t* const* in, size_t nin, uint8_t* const* out, size_t nout,
                         const uint8_t* mat, size_t n) {
     const size_t pitch = (n + 255) & ~size_t(255);
@@ -258,18 +284,32 @@ int call_through_device(hec_coder* c, const uint8_t* const* in, size_t nin, uint
     uint8_t* dout[HEC_MAX_DATA_UNITS];
     size_t strides[HEC_MAX_DATA_UNITS];
     const bool piecewise = n >= (size_t(64) << 10);  // below that one DMA each way beats per-shard calls
+    hec::CopyPool* pool = piecewise ? call_pool(c, std::max(nin, nout)) : nullptr;
+    hec::PoolBatch batch{pool};  // declared after `drain`: the workers are joined first
     for (size_t i = 0; i < nin; i++) {
-        std::memcpy(c->call_host + i * pitch, in[i], n);
         din[i] = c->call_dev + i * pitch;
         strides[i] = pitch;
-        if (piecewise)
+    }
+    if (pool) {
+        pool->start(int(nin), [&](int i) { std::memcpy(c->call_host + size_t(i) * pitch, in[i], n); });
+        for (size_t i = 0; i < nin; i++) {
+            pool->wait(int(i));
             HEC_HIP(hipMemcpyAsync(c->call_dev + i * pitch, c->call_host + i * pitch, n, hipMemcpyHostToDevice,
                                    c->stream),
                     HEC_ERR_DEVICE);
+        }
+    } else {
+        for (size_t i = 0; i < nin; i++) {
+            std::memcpy(c->call_host + i * pitch, in[i], n);
+            if (piecewise)
+                HEC_HIP(hipMemcpyAsync(c->call_dev + i * pitch, c->call_host + i * pitch, n, hipMemcpyHostToDevice,
+                                       c->stream),
+                        HEC_ERR_DEVICE);
+        }
+        if (!piecewise)
+            HEC_HIP(hipMemcpyAsync(c->call_dev, c->call_host, pitch * (nin - 1) + n, hipMemcpyHostToDevice, c->stream),
+                    HEC_ERR_DEVICE);
     }
-    if (!piecewise)
-        HEC_HIP(hipMemcpyAsync(c->call_dev, c->call_host, pitch * (nin - 1) + n, hipMemcpyHostToDevice, c->stream),
-                HEC_ERR_DEVICE);
     for (size_t j = 0; j < nout; j++) dout[j] = c->call_dev + (nin + j) * pitch;
     rc = matmul_batch(c->device, mat, nout, nin, din, strides, dout, strides, n, 1, c->stream);
     if (rc != HEC_OK) return rc;
@@ -283,6 +323,20 @@ int call_through_device(hec_coder* c, const uint8_t* const* in, size_t nin, uint
     for (size_t j = 0; j < nout; j++) {
         HEC_HIP(hipMemcpyAsync(hout + j * pitch, dout[j], n, hipMemcpyDeviceToHost, c->stream), HEC_ERR_DEVICE);
         HEC_HIP(hipEventRecord(c->ev_call[j], c->stream), HEC_ERR_DEVICE);
+    }
+    if (pool) {
+        pool->wait_all();  // the input batch (done: every H2D was issued after its copy)
+        std::atomic<int> err{int(hipSuccess)};
+        pool->start(int(nout), [&](int j) {
+            const hipError_t e = hipEventSynchronize(c->ev_call[j]);
+            if (e != hipSuccess)
+                err.store(int(e), std::memory_order_relaxed);
+            else
+                std::memcpy(out[j], hout + size_t(j) * pitch, n);
+        });
+        pool->wait_all();
+        const int e = err.load(std::memory_order_relaxed);
+        return e == int(hipSuccess) ? HEC_OK : fail(HEC_ERR_DEVICE, "hipEventSynchronize", hipError_t(e));
     }
     for (size_t j = 0; j < nout; j++) {
         HEC_HIP(hipEventSynchronize(c->ev_call[j]), HEC_ERR_DEVICE);
@@ -422,6 +476,11 @@ void hec_coder_destroy(hec_coder_t* c) {
         if (c->call_dev) (void)hipFree(c->call_dev);
         if (c->call_host) (void)hipHostFree(c->call_host);
         if (c->verify_ws) (void)hipFree(c->verify_ws);
+        for (int i = 0; i < 2; i++) {
+            if (c->ev_mixed[i]) (void)hipEventSynchronize(c->ev_mixed[i]);
+            if (c->mixed_host[i]) (void)hipHostFree(c->mixed_host[i]);
+            if (c->ev_mixed[i]) (void)hipEventDestroy(c->ev_mixed[i]);
+        }
         for (hipEvent_t e : c->ev_call)
             if (e) (void)hipEventDestroy(e);
         for (int i = 0; i < hec_coder::kSlots; i++)
@@ -555,7 +614,6 @@ size_t mixed_workspace(size_t k, size_t m, size_t stripes) {
     return align_up(stripes * sizeof(uint32_t)) + p * plan_bytes(k, m);
 }
 
-void free_host_buffer(void* p) { delete[] static_cast<uint8_t*>(p); }
 
 }  // namespace
 
@@ -655,36 +713,38 @@ int mixed_decode_impl(hec_coder* c, const uint8_t* const* d_shards, const size_t
         }
         const size_t need = blob_pos + blob_bytes;
         if (!d_workspace || workspace_bytes < need || blob_bytes > 0xFFFFFFF0ull) return HEC_ERR_INVALID_ARG;
-        uint8_t* host = new uint8_t[need]();
-        uint32_t* soff = reinterpret_cast<uint32_t*>(host);
-        for (size_t s_ = 0; s_ < stripes; s_++)
-            soff[s_] = stripe_plan[s_] == 0xFFFF ? hec::kNoPlan : plan_off[stripe_plan[s_]];
-        for (size_t pi = 0; pi < plans.size(); pi++) {
-            const DecodePlan& p = *plans[pi];
-            auto* hdr = reinterpret_cast<hec::DevPlanHeader*>(host + blob_pos + plan_off[pi]);
-            hdr->e = uint32_t(p.missing.size());
-            for (size_t r = 0; r < k; r++) hdr->surv[r] = uint8_t(p.survivors[r]);
-            for (size_t r = 0; r < p.missing.size(); r++) hdr->miss[r] = uint8_t(p.missing[r]);
-            auto* tab = reinterpret_cast<uint32_t*>(host + blob_pos + plan_off[pi] + sizeof(hec::DevPlanHeader));
-            for (size_t r = 0; r < p.missing.size(); r++)
-                for (size_t i = 0; i < k; i++) {
-                    const auto w = hec::perm_table_words(p.matrix[r * k + i]);
-                    std::memcpy(tab + (r * k + i) * 8, w.data(), sizeof(uint32_t) * 8);
-                }
-        }
-        const hipError_t ce = hipMemcpyAsync(d_workspace, host, need, hipMemcpyHostToDevice, stream);
-        if (ce != hipSuccess) {
-            delete[] host;
-            (void)hipGetLastError();
-            return fail(HEC_ERR_DEVICE, "hipMemcpyAsync(workspace)", ce);
-        }
-        // the staging image is freed once the copy has run
-        const hipError_t he = hipLaunchHostFunc(stream, free_host_buffer, host);
-        if (he != hipSuccess) {
-            (void)hipStreamSynchronize(stream);
-            delete[] host;
-            (void)hipGetLastError();
-            return fail(HEC_ERR_DEVICE, "hipLaunchHostFunc", he);
+        {
+            // one of the coder's two pinned images, free once its last copy has run
+            std::lock_guard<std::mutex> lk(c->mixed_mu);
+            const int b = c->mixed_next;
+            c->mixed_next ^= 1;
+            if (!c->ev_mixed[b]) HEC_HIP(hipEventCreateWithFlags(&c->ev_mixed[b], hipEventDisableTiming), HEC_ERR_DEVICE);
+            else HEC_HIP(hipEventSynchronize(c->ev_mixed[b]), HEC_ERR_DEVICE);
+            if (c->mixed_host_bytes[b] < need) {
+                if (c->mixed_host[b]) (void)hipHostFree(c->mixed_host[b]);
+                c->mixed_host[b] = nullptr;
+                c->mixed_host_bytes[b] = 0;
+                const size_t want = std::max(need, 2 * c->mixed_host_bytes[b ^ 1]);
+                HEC_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->mixed_host[b]), want, hipHostMallocDefault),
+                        HEC_ERR_NO_MEMORY);
+                c->mixed_host_bytes[b] = want;
+            }
+            uint8_t* host = c->mixed_host[b];
+            uint32_t* soff = reinterpret_cast<uint32_t*>(host);
+            for (size_t s_ = 0; s_ < stripes; s_++)
+                soff[s_] = stripe_plan[s_] == 0xFFFF ? hec::kNoPlan : plan_off[stripe_plan[s_]];
+            for (size_t pi = 0; pi < plans.size(); pi++) {
+                const DecodePlan& p = *plans[pi];
+                auto* hdr = reinterpret_cast<hec::DevPlanHeader*>(host + blob_pos + plan_off[pi]);
+                std::memset(hdr, 0, sizeof(*hdr));
+                hdr->e = uint32_t(p.missing.size());
+                for (size_t r = 0; r < k; r++) hdr->surv[r] = uint8_t(p.survivors[r]);
+                for (size_t r = 0; r < p.missing.size(); r++) hdr->miss[r] = uint8_t(p.missing[r]);
+                std::memcpy(host + blob_pos + plan_off[pi] + sizeof(hec::DevPlanHeader), p.perm.data(),
+                            p.perm.size() * sizeof(uint32_t));
+            }
+            HEC_HIP(hipMemcpyAsync(d_workspace, host, need, hipMemcpyHostToDevice, stream), HEC_ERR_DEVICE);
+            HEC_HIP(hipEventRecord(c->ev_mixed[b], stream), HEC_ERR_DEVICE);
         }
 
         // 3. one launch per group of <= 4 missing rows
