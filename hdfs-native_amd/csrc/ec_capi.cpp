@@ -32,7 +32,6 @@
 #include "checksum.hpp"
 #include "checksum_tables.hpp"
 #include "ec_kernels.hpp"
-#include "copy_pool.hpp"
 #include "gf256.hpp"
 
 namespace {
@@ -106,12 +105,12 @@ struct hec_coder {
     // hec_encode / hec_decode (one row per call, pageable caller buffers):
     // a persistent pinned bounce buffer and device slots of their own, grown
     // geometrically and released only by hec_coder_destroy
-    static constexpr int kCallEvents = HEC_MAX_DATA_UNITS;
+    static constexpr int kCallPieces = 16;  // column pieces of one per-call row (pipeline stages)
+    static constexpr int kCallEvents = 3 * kCallPieces;
     uint8_t* call_host = nullptr;  // hipHostMalloc'd
     uint8_t* call_dev = nullptr;
     size_t call_bytes = 0;
     hipEvent_t ev_call[kCallEvents] = {};
-    std::unique_ptr<hec::CopyPool> call_pool;  // the per-call copies' worker threads (lazy)
     // verified read, phase 2: stripe lists + mixed-decode workspace (device),
     // grown geometrically, released by hec_coder_destroy
     uint8_t* verify_ws = nullptr;
@@ -258,22 +257,17 @@ int ensure_call_staging(hec_coder* c, size_t bytes) {
     return HEC_OK;
 }
 
-// The coder's copy workers for a per-call row of `shards` shards: tune key
-// 14 threads (default 4), at most one per shard; null when one would do.
-hec::CopyPool* call_pool(hec_coder* c, size_t shards) {
-    const int tuned = hec::tune_snapshot().host_copy_threads;
-    const int want = int(std::min<size_t>(shards, tuned > 0 ? size_t(tuned) : 4));
-    if (want < 2) return nullptr;
-    if (!c->call_pool) c->call_pool = std::make_unique<hec::CopyPool>();
-    return c->call_pool->ensure(want) >= 2 ? c->call_pool.get() : nullptr;
-}
-
 // One row through the device, pageable caller buffers in and out:
 //   out[j] = sum_i mat[j*nin + i] * in[i], n bytes each.
-// Inputs are copied into the pinned bounce buffer by the coder's copy
-// workers, several shards at once, and each shard's H2D DMA is issued as
-// soon as its copy is there; outputs come back D2H shard by shard and the
-// workers copy each out once its DMA is done.  No allocation on the hot path.
+// Rows of >= 512 KiB are cut into column pieces (>= 256 KiB of every shard,
+// at most kCallPieces) that flow through a three-stage pipeline: the
+// caller's thread copies piece p of every input into the pinned bounce
+// buffer and queues its H2D (one 2D copy on copy_stream[0]); the compute
+// stream runs the kernel on piece p once it has landed; copy_stream[1]
+// brings piece p of the outputs back (one 2D copy) and the caller copies it
+// out.  Host copies, both PCIe directions and the kernel then overlap within
+// one call.  Smaller rows go through in one piece, one DMA each way.
+// No allocation on the hot path.
 int call_through_device(hec_coder* c, const uint8_t* const* in, size_t nin, uint8_t* const* out, size_t nout,
                         const uint8_t* mat, size_t n) {
     const size_t pitch = (n + 255) & ~size_t(255);
@@ -283,65 +277,60 @@ int call_through_device(hec_coder* c, const uint8_t* const* in, size_t nin, uint
     const uint8_t* din[HEC_MAX_DATA_UNITS];
     uint8_t* dout[HEC_MAX_DATA_UNITS];
     size_t strides[HEC_MAX_DATA_UNITS];
-    const bool piecewise = n >= (size_t(64) << 10);  // below that one DMA each way beats per-shard calls
-    hec::CopyPool* pool = piecewise ? call_pool(c, std::max(nin, nout)) : nullptr;
-    hec::PoolBatch batch{pool};  // declared after `drain`: the workers are joined first
-    for (size_t i = 0; i < nin; i++) {
-        din[i] = c->call_dev + i * pitch;
-        strides[i] = pitch;
-    }
-    if (pool) {
-        pool->start(int(nin), [&](int i) { std::memcpy(c->call_host + size_t(i) * pitch, in[i], n); });
-        for (size_t i = 0; i < nin; i++) {
-            pool->wait(int(i));
-            HEC_HIP(hipMemcpyAsync(c->call_dev + i * pitch, c->call_host + i * pitch, n, hipMemcpyHostToDevice,
-                                   c->stream),
-                    HEC_ERR_DEVICE);
-        }
-    } else {
-        for (size_t i = 0; i < nin; i++) {
-            std::memcpy(c->call_host + i * pitch, in[i], n);
-            if (piecewise)
-                HEC_HIP(hipMemcpyAsync(c->call_dev + i * pitch, c->call_host + i * pitch, n, hipMemcpyHostToDevice,
-                                       c->stream),
-                        HEC_ERR_DEVICE);
-        }
-        if (!piecewise)
-            HEC_HIP(hipMemcpyAsync(c->call_dev, c->call_host, pitch * (nin - 1) + n, hipMemcpyHostToDevice, c->stream),
-                    HEC_ERR_DEVICE);
-    }
-    for (size_t j = 0; j < nout; j++) dout[j] = c->call_dev + (nin + j) * pitch;
-    rc = matmul_batch(c->device, mat, nout, nin, din, strides, dout, strides, n, 1, c->stream);
-    if (rc != HEC_OK) return rc;
+    for (size_t i = 0; i < std::max(nin, nout); i++) strides[i] = pitch;
+    uint8_t* hin = c->call_host;
     uint8_t* hout = c->call_host + nin * pitch;
-    if (!piecewise) {
-        HEC_HIP(hipMemcpyAsync(hout, dout[0], pitch * (nout - 1) + n, hipMemcpyDeviceToHost, c->stream), HEC_ERR_DEVICE);
-        HEC_HIP(hipStreamSynchronize(c->stream), HEC_ERR_DEVICE);
-        for (size_t j = 0; j < nout; j++) std::memcpy(out[j], hout + j * pitch, n);
+    uint8_t* dinb = c->call_dev;
+    uint8_t* doutb = c->call_dev + nin * pitch;
+
+    const int piece_kib = hec::tune_snapshot().call_piece_kib;  // tune key 17 (0 = 256 KiB)
+    const size_t kMinPiece = size_t(piece_kib > 0 ? piece_kib : 256) << 10;
+    if (n >= 2 * kMinPiece) {
+        size_t piece = (n + hec_coder::kCallPieces - 1) / hec_coder::kCallPieces;
+        piece = std::max(kMinPiece, (piece + 4095) & ~size_t(4095));
+        const size_t pieces = (n + piece - 1) / piece;
+        hipStream_t h2d = c->copy_stream[0], d2h = c->copy_stream[1];
+        hipEvent_t* ev_in = c->ev_call;
+        hipEvent_t* ev_k = c->ev_call + hec_coder::kCallPieces;
+        hipEvent_t* ev_out = c->ev_call + 2 * hec_coder::kCallPieces;
+        for (size_t q = 0; q < pieces; q++) {
+            const size_t off = q * piece, len = std::min(piece, n - off);
+            for (size_t i = 0; i < nin; i++) std::memcpy(hin + i * pitch + off, in[i] + off, len);
+            HEC_HIP(hipMemcpy2DAsync(dinb + off, pitch, hin + off, pitch, len, nin, hipMemcpyHostToDevice, h2d),
+                    HEC_ERR_DEVICE);
+            HEC_HIP(hipEventRecord(ev_in[q], h2d), HEC_ERR_DEVICE);
+            HEC_HIP(hipStreamWaitEvent(c->stream, ev_in[q], 0), HEC_ERR_DEVICE);
+            for (size_t i = 0; i < nin; i++) din[i] = dinb + i * pitch + off;
+            for (size_t j = 0; j < nout; j++) dout[j] = doutb + j * pitch + off;
+            rc = matmul_batch(c->device, mat, nout, nin, din, strides, dout, strides, len, 1, c->stream);
+            if (rc != HEC_OK) return rc;
+            HEC_HIP(hipEventRecord(ev_k[q], c->stream), HEC_ERR_DEVICE);
+            HEC_HIP(hipStreamWaitEvent(d2h, ev_k[q], 0), HEC_ERR_DEVICE);
+            HEC_HIP(hipMemcpy2DAsync(hout + off, pitch, doutb + off, pitch, len, nout, hipMemcpyDeviceToHost, d2h),
+                    HEC_ERR_DEVICE);
+            HEC_HIP(hipEventRecord(ev_out[q], d2h), HEC_ERR_DEVICE);
+        }
+        for (size_t q = 0; q < pieces; q++) {
+            const size_t off = q * piece, len = std::min(piece, n - off);
+            HEC_HIP(hipEventSynchronize(ev_out[q]), HEC_ERR_DEVICE);
+            for (size_t j = 0; j < nout; j++) std::memcpy(out[j] + off, hout + j * pitch + off, len);
+        }
         return HEC_OK;
     }
-    for (size_t j = 0; j < nout; j++) {
-        HEC_HIP(hipMemcpyAsync(hout + j * pitch, dout[j], n, hipMemcpyDeviceToHost, c->stream), HEC_ERR_DEVICE);
-        HEC_HIP(hipEventRecord(c->ev_call[j], c->stream), HEC_ERR_DEVICE);
+
+    // one piece: one DMA each way on the compute stream (fewer, larger copies
+    // beat per-shard ones below 512 KiB: profiles/r02_probe_percall*.log)
+    for (size_t i = 0; i < nin; i++) {
+        std::memcpy(hin + i * pitch, in[i], n);
+        din[i] = dinb + i * pitch;
     }
-    if (pool) {
-        pool->wait_all();  // the input batch (done: every H2D was issued after its copy)
-        std::atomic<int> err{int(hipSuccess)};
-        pool->start(int(nout), [&](int j) {
-            const hipError_t e = hipEventSynchronize(c->ev_call[j]);
-            if (e != hipSuccess)
-                err.store(int(e), std::memory_order_relaxed);
-            else
-                std::memcpy(out[j], hout + size_t(j) * pitch, n);
-        });
-        pool->wait_all();
-        const int e = err.load(std::memory_order_relaxed);
-        return e == int(hipSuccess) ? HEC_OK : fail(HEC_ERR_DEVICE, "hipEventSynchronize", hipError_t(e));
-    }
-    for (size_t j = 0; j < nout; j++) {
-        HEC_HIP(hipEventSynchronize(c->ev_call[j]), HEC_ERR_DEVICE);
-        std::memcpy(out[j], hout + j * pitch, n);
-    }
+    HEC_HIP(hipMemcpyAsync(dinb, hin, pitch * (nin - 1) + n, hipMemcpyHostToDevice, c->stream), HEC_ERR_DEVICE);
+    for (size_t j = 0; j < nout; j++) dout[j] = doutb + j * pitch;
+    rc = matmul_batch(c->device, mat, nout, nin, din, strides, dout, strides, n, 1, c->stream);
+    if (rc != HEC_OK) return rc;
+    HEC_HIP(hipMemcpyAsync(hout, doutb, pitch * (nout - 1) + n, hipMemcpyDeviceToHost, c->stream), HEC_ERR_DEVICE);
+    HEC_HIP(hipStreamSynchronize(c->stream), HEC_ERR_DEVICE);
+    for (size_t j = 0; j < nout; j++) std::memcpy(out[j], hout + j * pitch, n);
     return HEC_OK;
 }
 

@@ -319,31 +319,37 @@ int hec_host_alloc(int device, size_t bytes, int numa_node, void **out);
 int hec_host_free(void *ptr);
 
 /* ---- Measurement knobs (not part of the reference interface) ---------- *
- * key 1: 16-B column chunks per lane per tile (1, 2, 3 or 4; 0 = default)
+ * Process-wide atomics; every launch reads one consistent snapshot at its
+ * start, so a concurrent hec_tune_set only affects launches made after it.
+ * "exp" values exist only in the HEC_EXPERIMENTAL build
+ * (lib/libhdfs_ec_amd_exp.so, the measured-and-rejected kernel variants);
+ * the default library answers them with HEC_ERR_INVALID_ARG.
+ * key 1: 16-B column chunks per lane per tile (1, 2 or 4; exp 3; 0 = default)
  * key 2: non-temporal global loads/stores (0 or 1; -1 = default on)
- * key 3: resident blocks per CU for the grid (1..16; 0 = default)
+ * key 3: blocks per CU for the grid (1..16; 0 = default)
  * key 4: threads per block (256 or 512; 0 = default)
- * key 5: kernel pipeline (1 = register, 2 = LDS-DMA prefetch, 3 = register
- *        double-buffered, 4 = output bursts of key-15 column tiles; 0 = default)
- * key 6: chunk mapping (1 = block slabs, 2 = wave-contiguous runs; 0 = default)
+ * key 5: kernel pipeline: 1 = register, 2 = LDS-DMA prefetch; exp 3 = register
+ *        double-buffered (pipe), 4 = output bursts, 5 = double-buffered tiles;
+ *        0 = default
+ * key 6: store drain per tile in the register kernels: 1 = no drain,
+ *        0 / 2 = drain (default)
  * key 7: absolute grid size in blocks (0 = default)
- * key 8: tile order, stripes interleaved per group (1 = stripe-major; 0 = default)
+ * key 8: tile order, stripes interleaved per group (1 = stripe-major; 0 = default 4)
  * key 9: 1 = hec_encode_crc_device as encode + separate CRC pass (0 = fused)
  * key 10: fused encode+CRC slabs per wave: 0 = default, 4 or 8
- * key 11: CRC lookups: 0 = default (11-bit slicing in the checksum kernels,
- *         slice-by-8 in the fused ones), 1 = slice-by-8 tables, 5 = 11-bit slicing, 2 / 3 =
- *         bank-replicated slice-by-1 with 4 / 8 chains per lane (the fused kernels
- *         take 2 for the 4-chain form); 4 = slice-by-8 in 1024-thread blocks, 4 waves
- *         per SIMD (checksum kernels only); 9 = memory side only (WRONG sums)
+ * key 11: CRC lookups: 0 = default (11-bit slicing everywhere), 1 = slice-by-8,
+ *         5 = 11-bit slicing; exp 2 / 3 = bank-replicated slice-by-1 with 4 / 8
+ *         chains, 4 = slice-by-8 at 4 waves per SIMD (checksum kernel), 6 =
+ *         bank-replicated slice-by-2, 9 = memory side only (WRONG sums)
  * key 12: CRC register prefetch depth in 8-KiB tasks: 0 = default (2), 1 or 2
- * key 13: store cache policy of the double-buffered kernel at RS(6,3) / RS(10,4):
- *         0 = nt (default), 1 = sc1, 2 = sc0 sc1, 3 = nt sc1, 4 = plain
+ * key 13: exp: store cache policy of the pipe kernel (0 = nt, 1 = sc1, 2 = sc0 sc1,
+ *         3 = nt sc1, 4 = plain)
  * key 14: host threads that copy the present data cells in hec_decode_host_batch
  *         (0 = default 4)
- * key 15: column tiles per store burst of the output-burst kernel: 2 (default) or 3
- * key 16: 1 = the register kernel maps blocks to tiles XCD-contiguously (each XCD's
- *         blocks take one contiguous run of tiles; 0 = round-robin, default)
- * Process-wide; affects launches made after the call. */
+ * key 15: exp: column tiles per store burst of the output-burst kernel (2 or 3)
+ * key 16: fused kernels' waves per SIMD: 0 / 2 = default; exp 3
+ * key 17: per-call drop-in (hec_encode / hec_decode) pipeline piece in KiB per
+ *         shard, a multiple of 4 (0 = default 256) */
 int hec_tune_set(int key, int value);
 
 #ifdef __cplusplus

@@ -1,9 +1,9 @@
 """Measurement tool (GPU box): the per-call drop-in (hec_encode / hec_decode,
-one RS(6,3) row per call, pageable host buffers) by host copy threads (tune
-key 14: 1 = the caller's thread alone, 2..6 = the coder's copy workers),
+one RS(6,3) row per call, pageable host buffers) across the values of one
+tune key (PROBE_KEY, default 17 = pipeline piece KiB per shard; 0 = default),
 interleaved rounds, median us per call.  Every variant's output is checked.
 
-  PROBE_THREADS=1,2,4,6 PROBE_CELL=1048576 python scripts/probe_percall.py
+  PROBE_KEY=17 PROBE_VALUES=0,128,512 PROBE_CELL=1048576 python scripts/probe_percall.py
 """
 import ctypes
 import os
@@ -20,7 +20,8 @@ from hdfs_native_ec.synth import batch_data  # noqa: E402
 
 K, M = 6, 3
 CELL = int(os.environ.get("PROBE_CELL", str(1 << 20)))
-THREADS = [int(v) for v in os.environ.get("PROBE_THREADS", "1,2,4,6").split(",")]
+KEY = int(os.environ.get("PROBE_KEY", "17"))
+THREADS = [int(v) for v in os.environ.get("PROBE_VALUES", "0").split(",")]
 CALLS = int(os.environ.get("PROBE_CALLS", "32"))
 ROUNDS = int(os.environ.get("PROBE_ROUNDS", "5"))
 coder = H.Coder(K, M, 0)
@@ -38,7 +39,7 @@ dec = {t: [] for t in THREADS}
 ref = None
 for _ in range(ROUNDS):
     for t in THREADS:
-        H.tune_set(14, t)
+        H.tune_set(KEY, t)
         assert lib.hec_encode(coder.handle, ins, CELL, outs) == 0
         rec[:] = 0
         assert lib.hec_decode(coder.handle, shards, CELL, recs) == 0
@@ -57,10 +58,10 @@ for _ in range(ROUNDS):
             td += t2 - t1
         enc[t].append(te / CALLS * 1e6)
         dec[t].append(td / CALLS * 1e6)
-H.tune_set(14, 0)
+H.tune_set(KEY, 0)
 print(f"RS({K},{M}) one row of {CELL} B cells per call, pageable buffers; os.cpu_count() {os.cpu_count()}, "
       f"sched_getaffinity {len(os.sched_getaffinity(0))}", flush=True)
 for t in THREADS:
     e, d = statistics.median(enc[t]), statistics.median(dec[t])
-    print(f"copy threads {t}: encode {e:7.1f} us ({K * CELL / e / 1e3 / 1.073741824:6.2f} GiB/s)  "
+    print(f"key {KEY} = {t}: encode {e:7.1f} us ({K * CELL / e / 1e3 / 1.073741824:6.2f} GiB/s)  "
           f"decode {d:7.1f} us ({K * CELL / d / 1e3 / 1.073741824:6.2f} GiB/s)", flush=True)
