@@ -19,8 +19,10 @@
 //    per (input dword, coefficient): 3 v_perm_b32 + 2 XOR (v_bitop3).
 //  * Grid-stride over (stripe, column-tile) tiles so the table prologue is
 //    paid once per block.
-//  * Tails (cell_len % 16) and unaligned layouts use a byte-granular kernel
-//    with LDS log/antilog lookups -- same results, correctness path.
+//  * Layouts off the 16-B grid take a dword-realigning kernel (8 B per lane,
+//    aligned dword loads + v_alignbyte, 0.79-0.84 of the aligned rate);
+//    tails (cell_len % 16, or % 8 there) a byte-granular kernel with LDS
+//    log/antilog lookups -- same results everywhere.
 // Variants measured and rejected (register double buffering, output bursts,
 // store cache policies) live in ec_experimental.hip, built only into the
 // HEC_EXPERIMENTAL library.
@@ -492,8 +494,74 @@ __global__ __launch_bounds__(BS) void gf_decode_mixed(MixedArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Byte kernel: tails and unaligned layouts.  One thread per (stripe, byte) in
-// [a.byte_begin, a.cell_len); LDS log/antilog lookups.
+// Unaligned layouts: 8 bytes per lane from naturally aligned dword loads.
+// A batch whose base pointers or strides are off the 16-B grid cannot take
+// the dwordx4 kernels.  Here lane g of stripe s owns bytes [8g, 8g+8) of the
+// cell: per input it loads the 2 or 3 aligned dwords that cover them (every
+// such dword holds at least one byte of the cell, so it never leaves the
+// cell's pages) and shifts them into place with v_alignbyte; the GF math is
+// the v_perm product tables of gf_matmul_v16; each output is stored as two
+// dwords, four shorts or eight bytes by its own alignment.  Bytes
+// [8 * (cell_len / 8), cell_len) are left to the byte kernel.
+// ---------------------------------------------------------------------------
+template <int R>
+__global__ __launch_bounds__(256) void gf_matmul_dw(MatmulArgs a) {
+    __shared__ PermTable s_tab[R][kMaxK];
+    __shared__ uint8_t s_exp[512];
+    __shared__ uint8_t s_log[256];
+    __shared__ uint8_t s_coef[R * kMaxK];
+    const int k = a.k;
+    prologue<R, 256>(a, k, s_tab, s_exp, s_log, s_coef);
+    const uint64_t groups = a.cell_len / 8;
+    const uint64_t total = groups * a.stripes;
+    for (uint64_t t = uint64_t(blockIdx.x) * 256 + threadIdx.x; t < total; t += uint64_t(gridDim.x) * 256) {
+        const uint64_t stripe = t / groups;
+        const uint64_t off = (t - stripe * groups) * 8;
+        uint32_t acc[R][2];
+#pragma unroll
+        for (int j = 0; j < R; j++) acc[j][0] = acc[j][1] = 0;
+        for (int i = 0; i < k; i++) {
+            const uintptr_t p = reinterpret_cast<uintptr_t>(a.in[i] + stripe * a.in_stride[i] + off);
+            const uint32_t* w = reinterpret_cast<const uint32_t*>(p & ~uintptr_t(3));
+            const uint32_t sh = uint32_t(p & 3);
+            const uint32_t w0 = w[0], w1 = w[1];
+            const uint32_t w2 = sh ? w[2] : 0u;  // holds bytes 8g+8-sh.. of this group only when sh != 0
+            const uint32_t x[2] = {__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh)};
+#pragma unroll
+            for (int d = 0; d < 2; d++) {
+                const Sel sl = make_sel(x[d]);
+#pragma unroll
+                for (int j = 0; j < R; j++) {
+                    const PermTable& tb = s_tab[j][i];
+                    acc[j][d] ^= gf_mul4(tb.t0lo, tb.t0hi, tb.t1lo, tb.t1hi, tb.t2, sl.s0, sl.s1, sl.s2);
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < R; j++) {
+            uint8_t* q = a.out[j] + stripe * a.out_stride[j] + off;
+            const uintptr_t qa = reinterpret_cast<uintptr_t>(q);
+            if ((qa & 3) == 0) {
+                reinterpret_cast<uint32_t*>(q)[0] = acc[j][0];
+                reinterpret_cast<uint32_t*>(q)[1] = acc[j][1];
+            } else if ((qa & 1) == 0) {
+                uint16_t* h = reinterpret_cast<uint16_t*>(q);
+                h[0] = uint16_t(acc[j][0]);
+                h[1] = uint16_t(acc[j][0] >> 16);
+                h[2] = uint16_t(acc[j][1]);
+                h[3] = uint16_t(acc[j][1] >> 16);
+            } else {
+#pragma unroll
+                for (int b = 0; b < 8; b++) q[b] = uint8_t(acc[j][b / 4] >> (8 * (b % 4)));
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Byte kernel: tails (and, on tune key 18 = 1, whole unaligned batches).  One
+// thread per (stripe, byte) in [a.byte_begin, a.cell_len); LDS log/antilog
+// lookups.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void gf_matmul_bytes(MatmulArgs a) {
     __shared__ uint8_t s_exp[512];
@@ -705,7 +773,23 @@ int launch_gf_matmul(const MatmulArgs& in, int device, hipStream_t stream) {
         const hipError_t e = hipLaunchKernel(fn, dim3(uint32_t(grid)), dim3(sh.block), args, 0, stream);
         if (e != hipSuccess) return int(e);
     }
-    const uint64_t begin = chunks * 16;
+    uint64_t begin = chunks * 16;
+    if (begin == 0 && !aligned && a.cell_len >= 8 && a.r >= 1 && a.r <= kMaxR && tn.unaligned != 1) {
+        // unaligned layout: the dword kernel up to the last whole 8 bytes,
+        // the byte kernel after (tune key 18 = 1: the byte kernel alone)
+        const uint64_t total = (a.cell_len / 8) * a.stripes;
+        uint64_t grid = (total + 255) / 256;
+        const uint64_t cap = uint64_t(cus) * 8;
+        if (grid > cap) grid = cap;
+        const void* fn = a.r == 1   ? reinterpret_cast<const void*>(&gf_matmul_dw<1>)
+                         : a.r == 2 ? reinterpret_cast<const void*>(&gf_matmul_dw<2>)
+                         : a.r == 3 ? reinterpret_cast<const void*>(&gf_matmul_dw<3>)
+                                    : reinterpret_cast<const void*>(&gf_matmul_dw<4>);
+        void* args[] = {&a};
+        const hipError_t e = hipLaunchKernel(fn, dim3(uint32_t(grid)), dim3(256), args, 0, stream);
+        if (e != hipSuccess) return int(e);
+        begin = (a.cell_len / 8) * 8;
+    }
     if (begin < a.cell_len) {
         a.byte_begin = begin;
         const uint64_t total = (a.cell_len - begin) * a.stripes;

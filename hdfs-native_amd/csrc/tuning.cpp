@@ -12,7 +12,7 @@ namespace hec {
 
 namespace {
 
-constexpr int kKeys = 17;
+constexpr int kKeys = 18;
 std::atomic<int> g_knob[kKeys + 1];  // index = key; zero-initialised (static storage)
 std::atomic<int> g_nt{-1};           // key 2 defaults to -1 (non-temporal on)
 
@@ -48,6 +48,7 @@ Tune tune_snapshot() {
     t.burst_tiles = load(15);
     t.fused_wpe = load(16);
     t.call_piece_kib = load(17);
+    t.unaligned = load(18);
     return t;
 }
 
@@ -76,6 +77,7 @@ int tune_store(int key, int value) {
         case 15: ok = kExperimental && (value == 0 || value == 2 || value == 3); break;
         case 16: ok = value == 0 || value == 2 || (kExperimental && value == 3); break;
         case 17: ok = value >= 0 && value <= 65536 && (value & 3) == 0; break;
+        case 18: ok = value == 0 || value == 1; break;
         default: ok = false;
     }
     if (!ok) return HEC_ERR_INVALID_ARG;

@@ -197,6 +197,56 @@ def test_device_unaligned_layout(dev, c_oracle):
     assert np.array_equal(got, want)
 
 
+@pytest.mark.parametrize("k,m,S,cell,in_off,out_off,pitch_extra,per_shard", [
+    (6, 3, 3, 1000, 1, 3, 0, False), (6, 3, 2, 4096 + 7, 5, 0, 12, False), (6, 3, 2, 65536 + 5, 0, 2, 4, False),
+    (10, 4, 2, 8192 + 5, 3, 1, 0, True), (3, 2, 4, 4096, 2, 6, 2, True), (3, 2, 3, 7, 1, 1, 0, False),
+    (2, 1, 3, 24, 7, 5, 1, True)])
+@pytest.mark.parametrize("byte_only", [False, True])
+def test_device_unaligned_layouts(dev, c_oracle, k, m, S, cell, in_off, out_off, pitch_extra, per_shard, byte_only):
+    """Bases and strides off the 16-B grid: the dword-realigning kernel (8 B
+    per lane, aligned dword loads + v_alignbyte, dword / short / byte stores
+    by output alignment) plus the byte tail, or the byte kernel alone (tune
+    key 18 = 1); encode and a decode with m data shards missing vs the oracle."""
+    data = batch_data(S, k, cell, first=13 + cell + in_off)
+    want = oracle_batch_encode(c_oracle, k, m, data)
+    pitch = cell + pitch_extra
+    shard_off = [in_off + (3 * i + 1 if per_shard else 0) for i in range(k)]
+    in_stride = k * pitch + (3 * k + 16 if per_shard else 0)  # per-shard offsets need room between stripes
+    span = S * in_stride + max(shard_off) + 16
+    buf = torch.zeros(span, dtype=torch.uint8, device=dev)
+    hbuf = np.zeros(span, dtype=np.uint8)
+    for s_ in range(S):
+        for i in range(k):
+            at = shard_off[i] + i * pitch + s_ * in_stride
+            hbuf[at:at + cell] = data[s_, i]
+    buf.copy_(torch.from_numpy(hbuf))
+    ip = [buf.data_ptr() + shard_off[i] + i * pitch for i in range(k)]
+    pbuf = torch.zeros(S * m * pitch + out_off + 16, dtype=torch.uint8, device=dev)
+    op = [pbuf.data_ptr() + out_off + j * pitch for j in range(m)]
+    sp = torch.cuda.current_stream().cuda_stream
+    cod = coder(k, m)
+    H.tune_set(18, 1 if byte_only else 0)
+    try:
+        cod.encode_device(ip, [in_stride] * k, op, [m * pitch] * m, cell, S, sp)
+        torch.cuda.synchronize()
+        hp = pbuf.cpu().numpy()
+        got = np.stack([np.stack([hp[out_off + (s_ * m + j) * pitch:][:cell] for j in range(m)]) for s_ in range(S)])
+        assert np.array_equal(got, want)
+        # decode: data shards 0..m-1 missing, rebuilt into an unaligned buffer
+        miss = list(range(min(m, k)))
+        rbuf = torch.zeros(S * k * pitch + out_off + 16, dtype=torch.uint8, device=dev)
+        shards = [None if i in miss else ip[i] for i in range(k)] + op
+        outs = [rbuf.data_ptr() + out_off + i * pitch if i in miss else 0 for i in range(k)]
+        cod.decode_device(shards, [in_stride] * k + [m * pitch] * m, outs, [k * pitch] * k, cell, S, sp)
+        torch.cuda.synchronize()
+        hr = rbuf.cpu().numpy()
+        for s_ in range(S):
+            for i in miss:
+                assert np.array_equal(hr[out_off + (s_ * k + i) * pitch:][:cell], data[s_, i]), (s_, i)
+    finally:
+        H.tune_set(18, 0)
+
+
 def test_gf_matmul_device_arbitrary_matrix(dev):
     # the raw Mul<&[&[u8]]> (matrix.rs:204-231) with a random 7x5 matrix
     rng = np.random.default_rng(3)
@@ -320,7 +370,8 @@ def test_tune_set_concurrent_with_launches(dev, c_oracle):
 
 def test_experimental_keys_rejected_by_default_library():
     # the rejected variants exist only in lib/libhdfs_ec_amd_exp.so
-    for key, value in [(5, 3), (5, 4), (5, 5), (13, 1), (15, 2), (11, 2), (11, 6), (11, 9), (6, 3), (16, 1), (16, 3)]:
+    for key, value in [(5, 3), (5, 4), (5, 5), (13, 1), (15, 2), (11, 2), (11, 6), (11, 9), (6, 3), (16, 1), (16, 3),
+                       (18, 2), (17, 6)]:
         with pytest.raises(ValueError):
             H.tune_set(key, value)
 
