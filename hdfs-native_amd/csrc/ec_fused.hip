@@ -55,7 +55,7 @@ __device__ __forceinline__ const crc::Tables<KIND>& fused_tables() {
 //   VERIFY: checksummed shards 0..K-1 = the survivors; their expected sums
 //     sit at the same index (shard_id = survivor shard numbers), a mismatch
 //     sets bad[stripe * n_total + shard_id[s]].
-template <int K, int R, int SLABS, int SCHEME, int KIND, bool VERIFY, int WPE = 2>
+template <int K, int R, int SLABS, int SCHEME, int KIND, bool VERIFY, int WPE = 2, bool PAIR = false>
 __global__ __launch_bounds__(crcdev::sliced(SCHEME) ? 128 * WPE * (WPE - 1) : 512)
     __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void gf_fused_crc(
     MatmulArgs a, FusedCrcArgs cs) {
@@ -168,55 +168,142 @@ __global__ __launch_bounds__(crcdev::sliced(SCHEME) ? 128 * WPE * (WPE - 1) : 51
         u32x4 x[SLABS], xn[SLABS];
 #pragma unroll
         for (int u = 0; u < SLABS; u++) x[u] = load16<true>(a.in[0] + (uint64_t(stripe) * a.in_stride[0] + wbyte) + voff[u]);
-#pragma unroll
-        for (int i = 0; i < K; i++) {
-            if (PF && i + 1 < K) {
+        if constexpr (PAIR && SPR == 2 && PF) {
+            // Inputs two at a time (one CRC round): both shards' products go
+            // into the accumulators through one chain of 3-input XORs, 3 ops
+            // per (dword, output) for the pair instead of 4.  The next pair's
+            // loads are issued after this pair's GF math, before its round.
+            if (K > 1) {
 #pragma unroll
                 for (int u = 0; u < SLABS; u++)
-                    xn[u] = load16<true>(a.in[i + 1] + (uint64_t(stripe) * a.in_stride[i + 1] + wbyte) + voff[u]);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int u = 0; u < SLABS; u++) stage_piece(i % SPR, u, x[u]);
-            // opaque per-input table offset threaded through the
-            // accumulators: keeps the table reads (and the GF math) of input
-            // i from being hoisted next to those of the other inputs
-            uint32_t toff = uint32_t(i) * uint32_t(sizeof(PermTable));
-            asm volatile("" : "+v"(toff));
-#pragma unroll
-            for (int u = 0; u < SLABS; u++) {
-                asm volatile("" : "+v"(x[u]));
-#pragma unroll
-                for (int j = 0; j < R; j++) asm volatile("" : "+v"(acc[u][j]) : "v"(toff));
-            }
-            uint32_t tb[R][5];
-#pragma unroll
-            for (int j = 0; j < R; j++) {
-                const PermTable& t =
-                    *reinterpret_cast<const PermTable*>(reinterpret_cast<const char*>(&s_tab[j][0]) + toff);
-                tb[j][0] = t.t0lo;
-                tb[j][1] = t.t0hi;
-                tb[j][2] = t.t1lo;
-                tb[j][3] = t.t1hi;
-                tb[j][4] = t.t2;
+                    xn[u] = load16<true>(a.in[1] + (uint64_t(stripe) * a.in_stride[1] + wbyte) + voff[u]);
             }
 #pragma unroll
-            for (int u = 0; u < SLABS; u++)
+            for (int i = 0; i < K; i += 2) {
+                const bool two = i + 1 < K;
+                __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-                for (int d = 0; d < 4; d++) {
-                    const Sel sl = make_sel(x[u][d]);
-#pragma unroll
-                    for (int j = 0; j < R; j++)
-                        acc[u][j][d] ^= gf_mul4(tb[j][0], tb[j][1], tb[j][2], tb[j][3], tb[j][4], sl.s0, sl.s1, sl.s2);
+                for (int u = 0; u < SLABS; u++) {
+                    stage_piece(0, u, x[u]);
+                    if (two) stage_piece(1, u, xn[u]);
                 }
-            __builtin_amdgcn_sched_barrier(0);
-            after_stage(i);
-            __builtin_amdgcn_sched_barrier(0);
-            if (i + 1 < K) {
+                uint32_t toff = uint32_t(i) * uint32_t(sizeof(PermTable));
+                asm volatile("" : "+v"(toff));
+#pragma unroll
+                for (int u = 0; u < SLABS; u++) {
+                    asm volatile("" : "+v"(x[u]), "+v"(xn[u]));
+#pragma unroll
+                    for (int j = 0; j < R; j++) asm volatile("" : "+v"(acc[u][j]) : "v"(toff));
+                }
+                uint32_t ta[R][5], tq[R][5];
+#pragma unroll
+                for (int j = 0; j < R; j++) {
+                    const PermTable& t =
+                        *reinterpret_cast<const PermTable*>(reinterpret_cast<const char*>(&s_tab[j][0]) + toff);
+                    ta[j][0] = t.t0lo;
+                    ta[j][1] = t.t0hi;
+                    ta[j][2] = t.t1lo;
+                    ta[j][3] = t.t1hi;
+                    ta[j][4] = t.t2;
+                    if (two) {
+                        const PermTable& q = (&t)[1];
+                        tq[j][0] = q.t0lo;
+                        tq[j][1] = q.t0hi;
+                        tq[j][2] = q.t1lo;
+                        tq[j][3] = q.t1hi;
+                        tq[j][4] = q.t2;
+                    }
+                }
 #pragma unroll
                 for (int u = 0; u < SLABS; u++)
-                    x[u] = PF ? xn[u]
-                              : load16<true>(a.in[i + 1] + (uint64_t(stripe) * a.in_stride[i + 1] + wbyte) + voff[u]);
+#pragma unroll
+                    for (int d = 0; d < 4; d++) {
+                        const Sel sa = make_sel(x[u][d]);
+                        if (two) {
+                            const Sel sb = make_sel(xn[u][d]);
+#pragma unroll
+                            for (int j = 0; j < R; j++) {
+                                const uint32_t a0 = __builtin_amdgcn_perm(ta[j][1], ta[j][0], sa.s0);
+                                const uint32_t a1 = __builtin_amdgcn_perm(ta[j][3], ta[j][2], sa.s1);
+                                const uint32_t a2 = __builtin_amdgcn_perm(ta[j][4], ta[j][4], sa.s2);
+                                const uint32_t b0 = __builtin_amdgcn_perm(tq[j][1], tq[j][0], sb.s0);
+                                const uint32_t b1 = __builtin_amdgcn_perm(tq[j][3], tq[j][2], sb.s1);
+                                const uint32_t b2 = __builtin_amdgcn_perm(tq[j][4], tq[j][4], sb.s2);
+                                acc[u][j][d] = xor3(xor3(xor3(acc[u][j][d], a0, a1), a2, b0), b1, b2);
+                            }
+                        } else {
+#pragma unroll
+                            for (int j = 0; j < R; j++)
+                                acc[u][j][d] ^= gf_mul4(ta[j][0], ta[j][1], ta[j][2], ta[j][3], ta[j][4], sa.s0,
+                                                        sa.s1, sa.s2);
+                        }
+                    }
+                __builtin_amdgcn_sched_barrier(0);
+                if (i + 2 < K) {
+#pragma unroll
+                    for (int u = 0; u < SLABS; u++)
+                        x[u] = load16<true>(a.in[i + 2] + (uint64_t(stripe) * a.in_stride[i + 2] + wbyte) + voff[u]);
+                }
+                if (i + 3 < K) {
+#pragma unroll
+                    for (int u = 0; u < SLABS; u++)
+                        xn[u] = load16<true>(a.in[i + 3] + (uint64_t(stripe) * a.in_stride[i + 3] + wbyte) + voff[u]);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                after_stage(two ? i + 1 : i);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < K; i++) {
+                if (PF && i + 1 < K) {
+    #pragma unroll
+                    for (int u = 0; u < SLABS; u++)
+                        xn[u] = load16<true>(a.in[i + 1] + (uint64_t(stripe) * a.in_stride[i + 1] + wbyte) + voff[u]);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+    #pragma unroll
+                for (int u = 0; u < SLABS; u++) stage_piece(i % SPR, u, x[u]);
+                // opaque per-input table offset threaded through the
+                // accumulators: keeps the table reads (and the GF math) of input
+                // i from being hoisted next to those of the other inputs
+                uint32_t toff = uint32_t(i) * uint32_t(sizeof(PermTable));
+                asm volatile("" : "+v"(toff));
+    #pragma unroll
+                for (int u = 0; u < SLABS; u++) {
+                    asm volatile("" : "+v"(x[u]));
+    #pragma unroll
+                    for (int j = 0; j < R; j++) asm volatile("" : "+v"(acc[u][j]) : "v"(toff));
+                }
+                uint32_t tb[R][5];
+    #pragma unroll
+                for (int j = 0; j < R; j++) {
+                    const PermTable& t =
+                        *reinterpret_cast<const PermTable*>(reinterpret_cast<const char*>(&s_tab[j][0]) + toff);
+                    tb[j][0] = t.t0lo;
+                    tb[j][1] = t.t0hi;
+                    tb[j][2] = t.t1lo;
+                    tb[j][3] = t.t1hi;
+                    tb[j][4] = t.t2;
+                }
+    #pragma unroll
+                for (int u = 0; u < SLABS; u++)
+    #pragma unroll
+                    for (int d = 0; d < 4; d++) {
+                        const Sel sl = make_sel(x[u][d]);
+    #pragma unroll
+                        for (int j = 0; j < R; j++)
+                            acc[u][j][d] ^= gf_mul4(tb[j][0], tb[j][1], tb[j][2], tb[j][3], tb[j][4], sl.s0, sl.s1, sl.s2);
+                    }
+                __builtin_amdgcn_sched_barrier(0);
+                after_stage(i);
+                __builtin_amdgcn_sched_barrier(0);
+                if (i + 1 < K) {
+    #pragma unroll
+                    for (int u = 0; u < SLABS; u++)
+                        x[u] = PF ? xn[u]
+                                  : load16<true>(a.in[i + 1] + (uint64_t(stripe) * a.in_stride[i + 1] + wbyte) + voff[u]);
+                }
             }
         }
 #pragma unroll
@@ -237,22 +324,30 @@ namespace {
 constexpr int fused_slabs(int k, int r) { return (r <= 3 && k <= 6) ? 8 : 4; }
 
 template <int K, int R, int SCHEME, int WPE = 2>
-const void* encode_sl(int slabs) {
+const void* encode_sl(int slabs, bool pair = false) {
     if constexpr (WPE == 3) return reinterpret_cast<const void*>(&gf_fused_crc<K, R, 4, SCHEME, crc::kCrc32c, false, 3>);
+    if (slabs == 4 && pair)
+        return reinterpret_cast<const void*>(&gf_fused_crc<K, R, 4, SCHEME, crc::kCrc32c, false, 2, true>);
     return slabs == 4 ? reinterpret_cast<const void*>(&gf_fused_crc<K, R, 4, SCHEME, crc::kCrc32c, false>)
                       : reinterpret_cast<const void*>(&gf_fused_crc<K, R, 8, SCHEME, crc::kCrc32c, false>);
 }
 
 template <int K, int R, int SCHEME, int WPE = 2>
-const void* verify_kind(int kind) {
+const void* verify_kind(int kind, bool pair = false) {
     constexpr int SL = WPE == 3 ? 4 : fused_slabs(K, R);
+    if constexpr (SL == 4 && WPE == 2) {
+        if (pair)
+            return kind == crc::kCrc32c
+                       ? reinterpret_cast<const void*>(&gf_fused_crc<K, R, SL, SCHEME, crc::kCrc32c, true, 2, true>)
+                       : reinterpret_cast<const void*>(&gf_fused_crc<K, R, SL, SCHEME, crc::kCksum, true, 2, true>);
+    }
     return kind == crc::kCrc32c ? reinterpret_cast<const void*>(&gf_fused_crc<K, R, SL, SCHEME, crc::kCrc32c, true, WPE>)
                                 : reinterpret_cast<const void*>(&gf_fused_crc<K, R, SL, SCHEME, crc::kCksum, true, WPE>);
 }
 
 // scheme 11 (default) = 11-bit slicing, 1 = slicing-by-8 (tune key 11 = 1)
 template <int K, int R>
-const void* encode_fn(int slabs, int scheme, int wpe) {
+const void* encode_fn(int slabs, int scheme, int wpe, bool pair) {
 #ifdef HEC_EXPERIMENTAL
     // rejected (same-box A/B, profiles/r01_probe_fused_scheme.log,
     // r02_probe_fused_rep2.log, r02_probe_fused_wpe3_*.log):
@@ -263,26 +358,26 @@ const void* encode_fn(int slabs, int scheme, int wpe) {
     if (wpe == 3) return scheme == 11 ? encode_sl<K, R, 11, 3>(slabs) : encode_sl<K, R, 1, 3>(slabs);
 #endif
     (void)wpe;
-    return scheme == 11 ? encode_sl<K, R, 11>(slabs) : encode_sl<K, R, 1>(slabs);
+    return scheme == 11 ? encode_sl<K, R, 11>(slabs, pair) : encode_sl<K, R, 1>(slabs, pair);
 }
 
 template <int K, int R>
-const void* verify_fn(int kind, int scheme, int wpe) {
+const void* verify_fn(int kind, int scheme, int wpe, bool pair) {
 #ifdef HEC_EXPERIMENTAL
     if (scheme == 22) return verify_kind<K, R, 22>(kind);
     if (wpe == 3) return scheme == 11 ? verify_kind<K, R, 11, 3>(kind) : verify_kind<K, R, 1, 3>(kind);
 #endif
     (void)wpe;
-    return scheme == 11 ? verify_kind<K, R, 11>(kind) : verify_kind<K, R, 1>(kind);
+    return scheme == 11 ? verify_kind<K, R, 11>(kind, pair) : verify_kind<K, R, 1>(kind, pair);
 }
 
 template <int K>
-const void* pick_r(bool verify, int r, int slabs, int scheme, int kind, int wpe) {
+const void* pick_r(bool verify, int r, int slabs, int scheme, int kind, int wpe, bool pair) {
     switch (r) {
-        case 1: return verify ? verify_fn<K, 1>(kind, scheme, wpe) : encode_fn<K, 1>(slabs, scheme, wpe);
-        case 2: return verify ? verify_fn<K, 2>(kind, scheme, wpe) : encode_fn<K, 2>(slabs, scheme, wpe);
-        case 3: return verify ? verify_fn<K, 3>(kind, scheme, wpe) : encode_fn<K, 3>(slabs, scheme, wpe);
-        default: return verify ? verify_fn<K, 4>(kind, scheme, wpe) : encode_fn<K, 4>(slabs, scheme, wpe);
+        case 1: return verify ? verify_fn<K, 1>(kind, scheme, wpe, pair) : encode_fn<K, 1>(slabs, scheme, wpe, pair);
+        case 2: return verify ? verify_fn<K, 2>(kind, scheme, wpe, pair) : encode_fn<K, 2>(slabs, scheme, wpe, pair);
+        case 3: return verify ? verify_fn<K, 3>(kind, scheme, wpe, pair) : encode_fn<K, 3>(slabs, scheme, wpe, pair);
+        default: return verify ? verify_fn<K, 4>(kind, scheme, wpe, pair) : encode_fn<K, 4>(slabs, scheme, wpe, pair);
     }
 }
 
@@ -313,13 +408,18 @@ int launch_fused(const MatmulArgs& in, const FusedCrcArgs& cs, bool verify, int 
                        : tn.crc_variant == 1            ? 1
                                                         : 11;
     const int wpe = (tn.fused_wpe == 3 && crcdev::sliced(scheme)) ? 3 : 2;
+    // at 4 slabs (two shards per round) the inputs go two at a time: same-box
+    // A/B (profiles/r02_probe_fused_pair.log) RS(10,4) x 512 encode + CRC
+    // 1.950 -> 1.915 ms, decode + verify 1.878 -> 1.818 ms; at k <= 6 the
+    // 8-slab kernel (no pairs) stays faster than 4 slabs with pairs
+    const bool pair = tn.fused_pair != 1;
     const int waves = !crcdev::sliced(scheme) ? 8 : wpe == 3 ? 12 : 4;
     const void* fn = nullptr;
     switch (a.k) {
-        case 2: fn = pick_r<2>(verify, a.r, slabs, scheme, cs.kind, wpe); break;
-        case 3: fn = pick_r<3>(verify, a.r, slabs, scheme, cs.kind, wpe); break;
-        case 6: fn = pick_r<6>(verify, a.r, slabs, scheme, cs.kind, wpe); break;
-        case 10: fn = pick_r<10>(verify, a.r, slabs, scheme, cs.kind, wpe); break;
+        case 2: fn = pick_r<2>(verify, a.r, slabs, scheme, cs.kind, wpe, pair); break;
+        case 3: fn = pick_r<3>(verify, a.r, slabs, scheme, cs.kind, wpe, pair); break;
+        case 6: fn = pick_r<6>(verify, a.r, slabs, scheme, cs.kind, wpe, pair); break;
+        case 10: fn = pick_r<10>(verify, a.r, slabs, scheme, cs.kind, wpe, pair); break;
         default: return -1;
     }
     if (!aligned) return -1;

@@ -12,7 +12,7 @@ namespace hec {
 
 namespace {
 
-constexpr int kKeys = 18;
+constexpr int kKeys = 19;
 std::atomic<int> g_knob[kKeys + 1];  // index = key; zero-initialised (static storage)
 std::atomic<int> g_nt{-1};           // key 2 defaults to -1 (non-temporal on)
 
@@ -49,6 +49,7 @@ Tune tune_snapshot() {
     t.fused_wpe = load(16);
     t.call_piece_kib = load(17);
     t.unaligned = load(18);
+    t.fused_pair = load(19);
     return t;
 }
 
@@ -78,6 +79,7 @@ int tune_store(int key, int value) {
         case 16: ok = value == 0 || value == 2 || (kExperimental && value == 3); break;
         case 17: ok = value >= 0 && value <= 65536 && (value & 3) == 0; break;
         case 18: ok = value == 0 || value == 1; break;
+        case 19: ok = value >= 0 && value <= 2; break;
         default: ok = false;
     }
     if (!ok) return HEC_ERR_INVALID_ARG;

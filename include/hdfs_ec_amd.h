@@ -349,7 +349,11 @@ int hec_host_free(void *ptr);
  * key 15: exp: column tiles per store burst of the output-burst kernel (2 or 3)
  * key 16: fused kernels' waves per SIMD: 0 / 2 = default; exp 3
  * key 17: per-call drop-in (hec_encode / hec_decode) pipeline piece in KiB per
- *         shard, a multiple of 4 (0 = default 256) */
+ *         shard, a multiple of 4 (0 = default 256)
+ * key 18: unaligned layouts: 0 = default (dword-realigning kernel + byte tail),
+ *         1 = the byte kernel alone
+ * key 19: fused kernels at 4 slabs per wave: 0 / 2 = inputs two at a time
+ *         (default), 1 = one at a time */
 int hec_tune_set(int key, int value);
 
 #ifdef __cplusplus

@@ -2,7 +2,8 @@
 and fused decode + verify (hec_decode_verify_device) across CRC lookup
 schemes (tune key 11: 0/1 = slicing-by-8, 2 = bank-replicated (encode only, exp
 library), 5 = 11-bit slicing; suffix w = tune key 16 = 3, one 768-thread
-block per CU), interleaved rounds, median per variant.  Every variant's
+block per CU (exp library); suffix p = tune key 19 = 2, inputs two at a
+time; suffix q = tune key 10 = 4, 4 slabs per wave), interleaved rounds, median per variant.  Every variant's
 sums are checked against the default's.
 
   PROBE_K=6 PROBE_M=3 PROBE_S=1024 python scripts/probe_fused.py
@@ -63,8 +64,10 @@ variants = [("encode+crc", v, enc) for v in ENC] + [("decode+verify", v, ver) fo
 times = {(n, v): [] for n, v, _ in variants}
 for _ in range(ROUNDS):
     for name, v, fn in variants:
-        H.tune_set(11, int(v.rstrip("w")))
-        H.tune_set(16, 3 if v.endswith("w") else 0)
+        H.tune_set(11, int(v.rstrip("wpq")))
+        H.tune_set(16, 3 if "w" in v else 0)
+        H.tune_set(19, 2 if "p" in v else 0)
+        H.tune_set(10, 4 if "q" in v else 0)
         fn()
         torch.cuda.synchronize()
         if name == "encode+crc":
@@ -80,6 +83,8 @@ for _ in range(ROUNDS):
         times[(name, v)].append(ev[0].elapsed_time(ev[1]) / REPS)
 H.tune_set(11, 0)
 H.tune_set(16, 0)
+H.tune_set(19, 0)
+H.tune_set(10, 0)
 print(f"RS({K},{M}) S={S} cell={CELL}")
 for (name, v), t in times.items():
     ms = statistics.median(t)

@@ -371,7 +371,7 @@ def test_tune_set_concurrent_with_launches(dev, c_oracle):
 def test_experimental_keys_rejected_by_default_library():
     # the rejected variants exist only in lib/libhdfs_ec_amd_exp.so
     for key, value in [(5, 3), (5, 4), (5, 5), (13, 1), (15, 2), (11, 2), (11, 6), (11, 9), (6, 3), (16, 1), (16, 3),
-                       (18, 2), (17, 6)]:
+                       (18, 2), (17, 6), (19, 3)]:
         with pytest.raises(ValueError):
             H.tune_set(key, value)
 
@@ -677,6 +677,47 @@ def test_encode_crc_device(dev, c_oracle, codec, k, m, cell, S, fused, scheme):
     assert np.array_equal(p.cpu().numpy(), par)
     want = _oracle_sums(np.concatenate([data, par], axis=1), bpc)
     assert np.array_equal(sums.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("k,m,cell,S,slabs", [(10, 4, 1 << 15, 3, 0), (3, 2, 8192 + 512, 4, 4), (6, 3, 1 << 14, 2, 4)])
+@pytest.mark.parametrize("pair", [1, 2])
+def test_fused_input_pairing(dev, c_oracle, k, m, cell, S, slabs, pair):
+    """Fused encode + CRC32C and decode + verify at 4 slabs per wave with the
+    inputs two at a time (tune key 19 = 2, the default) and one at a time (1),
+    an odd k included, against the oracle."""
+    bpc = 512
+    data = batch_data(S, k, cell, first=57 + cell + pair)
+    par = oracle_batch_encode(c_oracle, k, m, data)
+    d = torch.from_numpy(data).to(dev)
+    p = torch.zeros((S, m, cell), dtype=torch.uint8, device=dev)
+    nch = cell // bpc
+    sums = torch.zeros((S, k + m, nch, 4), dtype=torch.uint8, device=dev)
+    dp, ds = H.stripe_layout_ptrs(d, k)
+    pp, ps = H.stripe_layout_ptrs(p, m)
+    sp = torch.cuda.current_stream().cuda_stream
+    cod = coder(k, m)
+    H.tune_set(19, pair)
+    H.tune_set(10, slabs)
+    try:
+        cod.encode_crc_device(dp, ds, pp, ps, cell, S, bpc, sums.data_ptr(), sp)
+        torch.cuda.synchronize()
+        assert np.array_equal(p.cpu().numpy(), par)
+        want = _oracle_sums(np.concatenate([data, par], axis=1), bpc)
+        assert np.array_equal(sums.cpu().numpy(), want)
+        out = torch.zeros_like(d)
+        bad = torch.zeros((S, k + m), dtype=torch.uint8, device=dev)
+        op, os_ = H.stripe_layout_ptrs(out, k)
+        miss = list(range(min(m, k)))
+        cod.decode_verify_device(H.CHECKSUM_CRC32C, [None if i in miss else dp[i] for i in range(k)] + pp, ds + ps,
+                                 op, os_, cell, S, bpc, sums.data_ptr(), bad.data_ptr(), sp)
+        torch.cuda.synchronize()
+        assert not bad.cpu().numpy().any()
+        o = out.cpu().numpy()
+        for i in miss:
+            assert np.array_equal(o[:, i], data[:, i])
+    finally:
+        H.tune_set(19, 0)
+        H.tune_set(10, 0)
 
 
 def test_encode_crc_full_size_properties(dev):
