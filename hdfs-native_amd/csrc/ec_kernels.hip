@@ -335,7 +335,7 @@ __global__ __launch_bounds__(BS) void gf_matmul_dma(MatmulArgs a) {
 //  otherwise: blocks walk contiguous runs of whole stripes and restage the
 //    plan into LDS once per stripe.
 // ---------------------------------------------------------------------------
-template <int K, int R, int U, int BS, bool RESIDENT>
+template <int K, int R, int U, int BS, bool RESIDENT, bool MIXED_SKIP = true>
 __global__ __launch_bounds__(BS) void gf_decode_mixed(MixedArgs a) {
     static_assert(K > 0, "compile-time k");
     __shared__ PermTable s_tab[RESIDENT ? 1 : R][K];  // non-resident: the current plan's rows
@@ -461,7 +461,9 @@ __global__ __launch_bounds__(BS) void gf_decode_mixed(MixedArgs a) {
                 for (int d = 0; d < 4; d++) sl[u][d] = make_sel(x[u][i][d]);
 #pragma unroll
             for (int j = 0; j < R; j++) {
-                // rows past the plan's e read zero tables / stale rows: computed, never stored
+                // rows past the plan's e are skipped (nrows is wave-uniform: a
+                // scalar branch); their accumulators are never stored
+                if (MIXED_SKIP && j > 0 && j >= nrows) break;
                 const PermTable& t =
                     *reinterpret_cast<const PermTable*>(reinterpret_cast<const char*>(tabs + j * K) + toff);
                 const uint32_t t0lo = t.t0lo, t0hi = t.t0hi, t1lo = t.t1lo, t1hi = t.t1hi, t2 = t.t2;
@@ -807,21 +809,27 @@ int launch_gf_matmul(const MatmulArgs& in, int device, hipStream_t stream) {
 
 namespace {
 
-template <int K, int R, bool RES>
+template <int K, int R, bool RES, bool SKIP>
 const void* mixed_fn() {
     if constexpr (K > 6)
-        return reinterpret_cast<const void*>(&gf_decode_mixed<K, R, 2, 512, RES>);
+        return reinterpret_cast<const void*>(&gf_decode_mixed<K, R, 2, 512, RES, SKIP>);
     else
-        return reinterpret_cast<const void*>(&gf_decode_mixed<K, R, 4, 256, RES>);
+        return reinterpret_cast<const void*>(&gf_decode_mixed<K, R, 4, 256, RES, SKIP>);
+}
+
+template <int K, int R>
+const void* mixed_sel(bool res, bool skip) {
+    return res ? (skip ? mixed_fn<K, R, true, true>() : mixed_fn<K, R, true, false>())
+               : (skip ? mixed_fn<K, R, false, true>() : mixed_fn<K, R, false, false>());
 }
 
 template <int K>
-const void* mixed_pick_r(int r, bool res) {
+const void* mixed_pick_r(int r, bool res, bool skip) {
     switch (r) {
-        case 1: return res ? mixed_fn<K, 1, true>() : mixed_fn<K, 1, false>();
-        case 2: return res ? mixed_fn<K, 2, true>() : mixed_fn<K, 2, false>();
-        case 3: return res ? mixed_fn<K, 3, true>() : mixed_fn<K, 3, false>();
-        default: return res ? mixed_fn<K, 4, true>() : mixed_fn<K, 4, false>();
+        case 1: return mixed_sel<K, 1>(res, skip);
+        case 2: return mixed_sel<K, 2>(res, skip);
+        case 3: return mixed_sel<K, 3>(res, skip);
+        default: return mixed_sel<K, 4>(res, skip);
     }
 }
 
@@ -837,12 +845,17 @@ int launch_decode_mixed(const MixedArgs& in, int rows, int device, hipStream_t s
     if (a.cell_len % 16 != 0 || a.cell_len / 16 > 0xFFFFFFFFull) return -1;
     const uint64_t dyn = ((a.stripes * 4 + 15) & ~uint64_t(15)) + a.blob_bytes;
     const bool res = dyn <= kResidentMax && a.blob_bytes % 4 == 0;
+    // rows past a stripe's e skipped behind a scalar branch for k <= 6 (RS(6,3)
+    // mixed +1.7 %), computed and dropped at the store for k = 10 (skipping
+    // costs 3.5-4 % there); same-box A/B profiles/r02_ab_mixed_skip.txt.
+    // Tune key 20: 1 = compute every row, 2 = skip.
+    const bool skip = tn.mixed_skip == 2 || (tn.mixed_skip == 0 && a.k <= 6);
     const void* fn = nullptr;
     switch (a.k) {
-        case 2: fn = mixed_pick_r<2>(rows, res); break;
-        case 3: fn = mixed_pick_r<3>(rows, res); break;
-        case 6: fn = mixed_pick_r<6>(rows, res); break;
-        case 10: fn = mixed_pick_r<10>(rows, res); break;
+        case 2: fn = mixed_pick_r<2>(rows, res, skip); break;
+        case 3: fn = mixed_pick_r<3>(rows, res, skip); break;
+        case 6: fn = mixed_pick_r<6>(rows, res, skip); break;
+        case 10: fn = mixed_pick_r<10>(rows, res, skip); break;
         default: return -1;
     }
     const int U = a.k > 6 ? 2 : 4, BS = a.k > 6 ? 512 : 256;

@@ -353,7 +353,10 @@ int hec_host_free(void *ptr);
  * key 18: unaligned layouts: 0 = default (dword-realigning kernel + byte tail),
  *         1 = the byte kernel alone
  * key 19: fused kernels at 4 slabs per wave: 0 / 2 = inputs two at a time
- *         (default), 1 = one at a time */
+ *         (default), 1 = one at a time
+ * key 20: mixed-pattern decode, rows past a stripe's erasure count: 0 = default
+ *         (skipped for k <= 6, computed and dropped for larger k), 1 = computed,
+ *         2 = skipped */
 int hec_tune_set(int key, int value);
 
 #ifdef __cplusplus

@@ -371,7 +371,7 @@ def test_tune_set_concurrent_with_launches(dev, c_oracle):
 def test_experimental_keys_rejected_by_default_library():
     # the rejected variants exist only in lib/libhdfs_ec_amd_exp.so
     for key, value in [(5, 3), (5, 4), (5, 5), (13, 1), (15, 2), (11, 2), (11, 6), (11, 9), (6, 3), (16, 1), (16, 3),
-                       (18, 2), (17, 6), (19, 3)]:
+                       (18, 2), (17, 6), (19, 3), (20, 3)]:
         with pytest.raises(ValueError):
             H.tune_set(key, value)
 
@@ -457,7 +457,10 @@ def _random_masks(k, m, S, seed, allow_fail=False):
 
 @pytest.mark.parametrize("k,m,cell", [(6, 3, 4096), (6, 3, 65536 + 64), (10, 4, 8192), (3, 2, 4096 + 16),
                                       (2, 1, 1024), (4, 2, 4096), (6, 3, 1000)])
-def test_device_decode_mixed_patterns(dev, c_oracle, k, m, cell):
+@pytest.mark.parametrize("skip", [0, 1, 2])
+def test_device_decode_mixed_patterns(dev, c_oracle, k, m, cell, skip):
+    """Random per-stripe patterns; tune key 20: rows past a stripe's erasure
+    count skipped (2), computed and dropped (1), or the per-k default (0)."""
     S = 40
     data = batch_data(S, k, cell, first=900 + k)
     par = oracle_batch_encode(c_oracle, k, m, data)
@@ -473,8 +476,12 @@ def test_device_decode_mixed_patterns(dev, c_oracle, k, m, cell):
             if not (mask >> i) & 1:
                 (d[s, i] if i < k else p[s, i - k]).fill_(0xEE)
     out = torch.full_like(d, 0x5A)
-    H.decode_batch_mixed(coder(k, m), d, p, masks, out)
-    torch.cuda.synchronize()
+    H.tune_set(20, skip)
+    try:
+        H.decode_batch_mixed(coder(k, m), d, p, masks, out)
+        torch.cuda.synchronize()
+    finally:
+        H.tune_set(20, 0)
     o = out.cpu().numpy()
     for s, mask in enumerate(masks):
         for i in range(k):
