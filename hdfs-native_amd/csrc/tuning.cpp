@@ -12,7 +12,7 @@ namespace hec {
 
 namespace {
 
-constexpr int kKeys = 20;
+constexpr int kKeys = 21;
 std::atomic<int> g_knob[kKeys + 1];  // index = key; zero-initialised (static storage)
 std::atomic<int> g_nt{-1};           // key 2 defaults to -1 (non-temporal on)
 
@@ -51,6 +51,7 @@ Tune tune_snapshot() {
     t.unaligned = load(18);
     t.fused_pair = load(19);
     t.mixed_skip = load(20);
+    t.fused_split = load(21);
     return t;
 }
 
@@ -81,7 +82,8 @@ int tune_store(int key, int value) {
         case 17: ok = value >= 0 && value <= 65536 && (value & 3) == 0; break;
         case 18: ok = value == 0 || value == 1; break;
         case 19: ok = value >= 0 && value <= 2; break;
-        case 20: ok = value >= 0 && value <= 2; break;
+        case 20: ok = value >= 0 && value <= 3; break;
+        case 21: ok = value == 0 || value == 1 || (kExperimental && (value == 2 || value == 3)); break;
         default: ok = false;
     }
     if (!ok) return HEC_ERR_INVALID_ARG;

@@ -3,7 +3,9 @@ and fused decode + verify (hec_decode_verify_device) across CRC lookup
 schemes (tune key 11: 0/1 = slicing-by-8, 2 = bank-replicated (encode only, exp
 library), 5 = 11-bit slicing; suffix w = tune key 16 = 3, one 768-thread
 block per CU (exp library); suffix p = tune key 19 = 2, inputs two at a
-time; suffix q = tune key 10 = 4, 4 slabs per wave), interleaved rounds, median per variant.  Every variant's
+time; suffix q = tune key 10 = 4, 4 slabs per wave; suffix s / S = tune key 21
+= 2 / 3, role-split GF / CRC waves, S with the CRC waves at raised priority),
+interleaved rounds, median per variant.  Every variant's
 sums are checked against the default's.
 
   PROBE_K=6 PROBE_M=3 PROBE_S=1024 python scripts/probe_fused.py
@@ -64,7 +66,8 @@ variants = [("encode+crc", v, enc) for v in ENC] + [("decode+verify", v, ver) fo
 times = {(n, v): [] for n, v, _ in variants}
 for _ in range(ROUNDS):
     for name, v, fn in variants:
-        H.tune_set(11, int(v.rstrip("wpq")))
+        H.tune_set(11, int(v.rstrip("wpqsS")))
+        H.tune_set(21, 3 if "S" in v else 2 if "s" in v else 0)
         H.tune_set(16, 3 if "w" in v else 0)
         H.tune_set(19, 2 if "p" in v else 0)
         H.tune_set(10, 4 if "q" in v else 0)
@@ -85,6 +88,7 @@ H.tune_set(11, 0)
 H.tune_set(16, 0)
 H.tune_set(19, 0)
 H.tune_set(10, 0)
+H.tune_set(21, 0)
 print(f"RS({K},{M}) S={S} cell={CELL}")
 for (name, v), t in times.items():
     ms = statistics.median(t)

@@ -457,10 +457,11 @@ def _random_masks(k, m, S, seed, allow_fail=False):
 
 @pytest.mark.parametrize("k,m,cell", [(6, 3, 4096), (6, 3, 65536 + 64), (10, 4, 8192), (3, 2, 4096 + 16),
                                       (2, 1, 1024), (4, 2, 4096), (6, 3, 1000)])
-@pytest.mark.parametrize("skip", [0, 1, 2])
+@pytest.mark.parametrize("skip", [0, 1, 2, 3])
 def test_device_decode_mixed_patterns(dev, c_oracle, k, m, cell, skip):
     """Random per-stripe patterns; tune key 20: rows past a stripe's erasure
-    count skipped (2), computed and dropped (1), or the per-k default (0)."""
+    count skipped (2), computed and dropped (1), the per-k default (0), or
+    one launch per erasure count over a stripe map (3)."""
     S = 40
     data = batch_data(S, k, cell, first=900 + k)
     par = oracle_batch_encode(c_oracle, k, m, data)
@@ -489,6 +490,43 @@ def test_device_decode_mixed_patterns(dev, c_oracle, k, m, cell, skip):
                 assert (o[s, i] == 0x5A).all(), (s, i)  # untouched
             else:
                 assert np.array_equal(o[s, i], data[s, i]), (s, i, bin(mask))
+
+
+@pytest.mark.parametrize("skip", [0, 3])
+def test_device_decode_mixed_many_plans(dev, skip):
+    """RS(10,4), 512 stripes with random 1..4 erased shards: a few hundred
+    distinct plans, more than the kernel keeps resident in LDS (the per-stripe
+    restaging path), whole batch and per erasure count."""
+    k, m, S, cell = 10, 4, 512, 4096
+    rng = np.random.default_rng(1234)
+    data = rng.integers(0, 256, size=(S, k, cell), dtype=np.uint8)
+    d = torch.from_numpy(data).to(dev)
+    p = torch.empty((S, m, cell), dtype=torch.uint8, device=dev)
+    H.encode_batch(coder(k, m), d, p)
+    full = (1 << (k + m)) - 1
+    masks = []
+    for s in range(S):
+        miss = rng.choice(k + m, size=int(rng.integers(1, m + 1)), replace=False)
+        masks.append(full & ~sum(1 << int(i) for i in miss))
+    dm = d.clone()
+    pm = p.clone()
+    for s, mask in enumerate(masks):
+        for i in range(k + m):
+            if not (mask >> i) & 1:
+                (dm[s, i] if i < k else pm[s, i - k]).fill_(0xEE)
+    out = torch.full_like(d, 0x5A)
+    H.tune_set(20, skip)
+    try:
+        H.decode_batch_mixed(coder(k, m), dm, pm, masks, out)
+        torch.cuda.synchronize()
+    finally:
+        H.tune_set(20, 0)
+    for s, mask in enumerate(masks):
+        for i in range(k):
+            if (mask >> i) & 1:
+                assert bool((out[s, i] == 0x5A).all()), (s, i)
+            else:
+                assert torch.equal(out[s, i], d[s, i]), (s, i, bin(mask))
 
 
 def test_device_decode_mixed_not_enough_shards_launches_nothing(dev):
