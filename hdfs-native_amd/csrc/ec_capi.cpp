@@ -597,12 +597,10 @@ size_t plan_bytes(size_t k, size_t m) {
     return sizeof(hec::DevPlanHeader) + std::min(k, m) * k * sizeof(hec::PermTable);
 }
 
-// [per-stripe plan offset: u32 x stripes][stripe map: u32 x stripes][plan
-// blob] (hec::MixedArgs); the map orders the stripes by erasure count when
-// the batch is decoded one launch per count
+// [per-stripe plan offset: u32 x stripes][plan blob] (hec::MixedArgs)
 size_t mixed_workspace(size_t k, size_t m, size_t stripes) {
     const size_t p = max_plans(k, m, stripes);
-    return 2 * align_up(stripes * sizeof(uint32_t)) + p * plan_bytes(k, m);
+    return align_up(stripes * sizeof(uint32_t)) + p * plan_bytes(k, m);
 }
 
 
@@ -694,16 +692,8 @@ int mixed_decode_impl(hec_coder* c, const uint8_t* const* d_shards, const size_t
             return HEC_OK;
         }
 
-        std::vector<size_t> class_begin;  // by_e: the stripes of erasure count e at [class_begin[e], class_begin[e + 1])
-        // 2. workspace image: per-stripe plan offsets | stripe map | plan blobs.
-        // By erasure count (tune key 20 = 3): stripes grouped by their plan's e
-        // (offsets and map in that order), one launch per count, each compiled
-        // for exactly its e rows.  Otherwise one launch for the batch's largest
-        // e, in stripe order (rows past a stripe's own e skipped or dropped).
-        const hec::Tune tn = hec::tune_snapshot();
-        const bool by_e = tn.mixed_skip == 3;
-        const size_t map_pos = align_up(stripes * sizeof(uint32_t));
-        const size_t blob_pos = 2 * map_pos;
+        // 2. workspace image: per-stripe plan offsets | plan blobs
+        const size_t blob_pos = align_up(stripes * sizeof(uint32_t));
         size_t blob_bytes = 0;
         std::vector<uint32_t> plan_off(plans.size());
         for (size_t pi = 0; pi < plans.size(); pi++) {
@@ -730,24 +720,8 @@ int mixed_decode_impl(hec_coder* c, const uint8_t* const* d_shards, const size_t
             }
             uint8_t* host = c->mixed_host[b];
             uint32_t* soff = reinterpret_cast<uint32_t*>(host);
-            if (by_e) {
-                // counting sort of the stripes that need a rebuild by e
-                uint32_t* smap = reinterpret_cast<uint32_t*>(host + map_pos);
-                class_begin.assign(max_e + 2, 0);
-                for (size_t s_ = 0; s_ < stripes; s_++)
-                    if (stripe_plan[s_] != 0xFFFF) class_begin[plans[stripe_plan[s_]]->missing.size() + 1]++;
-                for (size_t e = 1; e <= max_e + 1; e++) class_begin[e] += class_begin[e - 1];
-                std::vector<size_t> at(class_begin);
-                for (size_t s_ = 0; s_ < stripes; s_++) {
-                    if (stripe_plan[s_] == 0xFFFF) continue;
-                    const size_t pos = at[plans[stripe_plan[s_]]->missing.size()]++;
-                    soff[pos] = plan_off[stripe_plan[s_]];
-                    smap[pos] = uint32_t(s_);
-                }
-            } else {
-                for (size_t s_ = 0; s_ < stripes; s_++)
-                    soff[s_] = stripe_plan[s_] == 0xFFFF ? hec::kNoPlan : plan_off[stripe_plan[s_]];
-            }
+            for (size_t s_ = 0; s_ < stripes; s_++)
+                soff[s_] = stripe_plan[s_] == 0xFFFF ? hec::kNoPlan : plan_off[stripe_plan[s_]];
             for (size_t pi = 0; pi < plans.size(); pi++) {
                 const DecodePlan& p = *plans[pi];
                 auto* hdr = reinterpret_cast<hec::DevPlanHeader*>(host + blob_pos + plan_off[pi]);
@@ -780,28 +754,11 @@ int mixed_decode_impl(hec_coder* c, const uint8_t* const* d_shards, const size_t
         a.k = int32_t(k);
         a.cell_len = cell_len;
         a.stripes = stripes;
-        if (!by_e) {
-            for (size_t r0 = 0; r0 < max_e; r0 += hec::kMaxR) {
-                a.row0 = int32_t(r0);
-                const int rows = int(std::min(max_e - r0, size_t(hec::kMaxR)));
-                const int rc = hec::launch_decode_mixed(a, rows, c->device, stream);
-                if (rc != 0) return to_status(rc);
-            }
-            return HEC_OK;
-        }
-        const uint32_t* w_off = reinterpret_cast<const uint32_t*>(ws);
-        const uint32_t* w_map = reinterpret_cast<const uint32_t*>(ws + map_pos);
-        for (size_t e = 1; e <= max_e; e++) {
-            const size_t b0 = class_begin[e], b1 = class_begin[e + 1];
-            if (b1 == b0) continue;
-            a.stripe_off = w_off + b0;
-            a.stripe_map = w_map + b0;
-            a.stripes = b1 - b0;
-            for (size_t r0 = 0; r0 < e; r0 += hec::kMaxR) {
-                a.row0 = int32_t(r0);
-                const int rc = hec::launch_decode_mixed(a, int(std::min(e - r0, size_t(hec::kMaxR))), c->device, stream);
-                if (rc != 0) return to_status(rc);
-            }
+        for (size_t r0 = 0; r0 < max_e; r0 += hec::kMaxR) {
+            a.row0 = int32_t(r0);
+            const int rows = int(std::min(max_e - r0, size_t(hec::kMaxR)));
+            const int rc = hec::launch_decode_mixed(a, rows, c->device, stream);
+            if (rc != 0) return to_status(rc);
         }
         return HEC_OK;
     }

@@ -341,8 +341,7 @@ __global__ __launch_bounds__(BS) void gf_decode_mixed(MixedArgs a) {
     __shared__ PermTable s_tab[RESIDENT ? 1 : R][K];  // non-resident: the current plan's rows
     __shared__ DevPlanHeader s_hdr;
     __shared__ uint64_t s_base[kMaxShards], s_stride[kMaxShards], s_obase[kMaxK], s_ostride[kMaxK];
-    // RESIDENT: [stripe plan offsets: u32 x stripes, 16-B padded][stripe map:
-    // u32 x stripes, 16-B padded, when a.stripe_map][plan blob]
+    // RESIDENT: [stripe plan offsets: u32 x stripes, 16-B padded][plan blob]
     extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
     const int tid = threadIdx.x;
     if (tid < kMaxShards) {
@@ -353,15 +352,10 @@ __global__ __launch_bounds__(BS) void gf_decode_mixed(MixedArgs a) {
         s_obase[tid] = reinterpret_cast<uint64_t>(a.out[tid]);
         s_ostride[tid] = a.out_stride[tid];
     }
-    const uint32_t map_bytes = (uint32_t(a.stripes) * 4u + 15u) & ~15u;
-    const uint32_t off_bytes = map_bytes + (a.stripe_map ? map_bytes : 0u);  // where the blob starts
-    const uint32_t* s_map = reinterpret_cast<const uint32_t*>(s_dyn + map_bytes);
+    const uint32_t off_bytes = (uint32_t(a.stripes) * 4u + 15u) & ~15u;
     if constexpr (RESIDENT) {
         const uint32_t off_words = uint32_t(a.stripes);
         for (uint32_t t = tid; t < off_words; t += BS) reinterpret_cast<uint32_t*>(s_dyn)[t] = a.stripe_off[t];
-        if (a.stripe_map)
-            for (uint32_t t = tid; t < off_words; t += BS)
-                reinterpret_cast<uint32_t*>(s_dyn + map_bytes)[t] = a.stripe_map[t];
         const uint32_t words = a.blob_bytes / 4;
         for (uint32_t t = tid; t < words; t += BS)
             reinterpret_cast<uint32_t*>(s_dyn + off_bytes)[t] = reinterpret_cast<const uint32_t*>(a.plans)[t];
@@ -396,15 +390,6 @@ __global__ __launch_bounds__(BS) void gf_decode_mixed(MixedArgs a) {
     for (uint32_t tile = t_begin; tile < t_end; tile += t_step) {
         uint32_t stripe, tcol;
         tile_coords(tile, order, stripe, tcol);
-        // the batch stripe this launch stripe addresses (an erasure-count class
-        // launch maps its stripes; wave-uniform)
-        uint32_t gs = stripe;
-        if (a.stripe_map) {
-            if constexpr (RESIDENT)
-                gs = __builtin_amdgcn_readfirstlane(s_map[stripe]);
-            else
-                gs = a.stripe_map[stripe];
-        }
         const DevPlanHeader* hdr = &s_hdr;
         const PermTable* tabs = &s_tab[0][0];  // row r, input i at tabs[r * K + i]
         if constexpr (RESIDENT) {
@@ -450,7 +435,7 @@ __global__ __launch_bounds__(BS) void gf_decode_mixed(MixedArgs a) {
 #pragma unroll
         for (int i = 0; i < K; i++) {
             const int sh = __builtin_amdgcn_readfirstlane(hdr->surv[i]);
-            const uint8_t* ib = reinterpret_cast<const uint8_t*>(s_base[sh]) + uint64_t(gs) * s_stride[sh];
+            const uint8_t* ib = reinterpret_cast<const uint8_t*>(s_base[sh]) + uint64_t(stripe) * s_stride[sh];
 #pragma unroll
             for (int u = 0; u < U; u++) x[u][i] = load16<true>(ib + offs[u]);
         }
@@ -501,7 +486,7 @@ __global__ __launch_bounds__(BS) void gf_decode_mixed(MixedArgs a) {
         for (int j = 0; j < R; j++) {
             if (j >= nrows) break;  // block-uniform
             const int mi = __builtin_amdgcn_readfirstlane(hdr->miss[a.row0 + j]);
-            uint8_t* ob = reinterpret_cast<uint8_t*>(s_obase[mi]) + uint64_t(gs) * s_ostride[mi];
+            uint8_t* ob = reinterpret_cast<uint8_t*>(s_obase[mi]) + uint64_t(stripe) * s_ostride[mi];
 #pragma unroll
             for (int u = 0; u < U; u++)
                 if (full || live[u]) store16<true>(ob + offs[u], acc[u][j]);
@@ -858,7 +843,7 @@ int launch_decode_mixed(const MixedArgs& in, int rows, int device, hipStream_t s
     MixedArgs a = in;
     const Tune tn = tune_snapshot();
     if (a.cell_len % 16 != 0 || a.cell_len / 16 > 0xFFFFFFFFull) return -1;
-    const uint64_t dyn = ((a.stripes * 4 + 15) & ~uint64_t(15)) * (a.stripe_map ? 2 : 1) + a.blob_bytes;
+    const uint64_t dyn = ((a.stripes * 4 + 15) & ~uint64_t(15)) + a.blob_bytes;
     const bool res = dyn <= kResidentMax && a.blob_bytes % 4 == 0;
     // rows past a stripe's e skipped behind a scalar branch for k <= 6 (RS(6,3)
     // mixed +1.7 %), computed and dropped at the store for k = 10 (skipping

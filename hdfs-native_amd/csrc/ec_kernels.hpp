@@ -62,7 +62,6 @@ struct MixedArgs {
     uint64_t out_stride[kMaxK];
     const uint8_t* plans;             // blob: plan of stripe s at plans + stripe_off[s]
     const uint32_t* stripe_off;       // per stripe; kNoPlan = nothing missing
-    const uint32_t* stripe_map;       // null, or launch stripe s = batch stripe stripe_map[s] (one erasure-count class)
     uint32_t blob_bytes;              // size of the blob
     int32_t k;
     int32_t row0;                     // first missing row handled by this launch

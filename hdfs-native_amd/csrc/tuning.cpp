@@ -82,7 +82,7 @@ int tune_store(int key, int value) {
         case 17: ok = value >= 0 && value <= 65536 && (value & 3) == 0; break;
         case 18: ok = value == 0 || value == 1; break;
         case 19: ok = value >= 0 && value <= 2; break;
-        case 20: ok = value >= 0 && value <= 3; break;
+        case 20: ok = value >= 0 && value <= 2; break;
         case 21: ok = value == 0 || value == 1 || (kExperimental && (value == 2 || value == 3)); break;
         default: ok = false;
     }

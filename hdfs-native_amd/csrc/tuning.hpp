@@ -31,7 +31,7 @@ struct Tune {
     int call_piece_kib;     // key 17: per-call drop-in pipeline piece, KiB per shard (0 = 256)
     int unaligned;          // key 18: unaligned layouts: 0 default = dword kernel + byte tail, 1 = byte kernel only
     int fused_pair;         // key 19: fused kernels at 4 slabs: 0 default / 2 = inputs two at a time, 1 = one at a time
-    int mixed_skip;         // key 20: mixed decode rows past a stripe's e: 0 default (skip for k <= 6), 1 compute all, 2 skip, 3 one launch per erasure count
+    int mixed_skip;         // key 20: mixed decode rows past a stripe's e: 0 default (skip for k <= 6), 1 compute all, 2 skip
     int fused_split;        // key 21: fused kernels' wave roles: 0 default = 1 = every wave alternates (exp: 2 / 3 role-split GF / CRC waves)
     int fused_wpe;          // key 16: fused kernels' waves per SIMD (0 default = 2; exp: 3, one 768-thread block per CU)
 };

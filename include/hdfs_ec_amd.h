@@ -356,8 +356,7 @@ int hec_host_free(void *ptr);
  *         (default), 1 = one at a time
  * key 20: mixed-pattern decode, rows past a stripe's erasure count: 0 = default
  *         (skipped for k <= 6, computed and dropped for larger k), 1 = computed,
- *         2 = skipped, 3 = none: the stripes are grouped by erasure count and
- *         each count gets its own launch compiled for exactly its rows
+ *         2 = skipped
  * key 21: fused kernels' wave roles: 0 / 1 = every wave alternates GF math
  *         and CRC rounds (default); exp 2 = role-split GF / CRC waves (one
  *         512-thread block per CU, RS(6,3) and RS(10,4) only), 3 = role-split

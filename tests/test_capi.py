@@ -153,5 +153,5 @@ def test_tune_set_validates_without_device():
     assert H.lib.hec_tune_set(3, 2) == H.HEC_OK
     assert H.lib.hec_tune_set(3, 0) == H.HEC_OK
     for key, value in [(5, 3), (5, 4), (5, 5), (6, 3), (13, 1), (15, 2), (16, 1), (16, 3), (11, 2), (11, 6), (11, 9), (3, 99),
-                       (18, 2), (17, 6), (19, 3), (20, 4), (21, 2), (21, 4), (22, 0), (0, 0)]:
+                       (18, 2), (17, 6), (19, 3), (20, 3), (21, 2), (21, 4), (22, 0), (0, 0)]:
         assert H.lib.hec_tune_set(key, value) == H.HEC_ERR_INVALID_ARG, (key, value)
