@@ -386,6 +386,20 @@ int hec_gen_rs_matrix(size_t data_units, size_t parity_units, uint8_t* out) {
     });
 }
 
+int hec_gen_codec_matrix(const char* codec, size_t data_units, size_t parity_units, uint8_t* out) {
+    if (!out || data_units == 0 || parity_units == 0 || data_units + parity_units > 255) return HEC_ERR_INVALID_ARG;
+    const std::string name = codec ? codec : "rs";
+    if (name != "rs" && name != "xor" && name != "rs-legacy") return HEC_ERR_UNSUPPORTED_CODEC;
+    if (name == "xor" && parity_units != 1) return HEC_ERR_INVALID_ARG;
+    return guarded([&] {
+        const std::vector<uint8_t> m = name == "xor"         ? hec::gen_xor_matrix(data_units)
+                                       : name == "rs-legacy" ? hec::gen_rs_legacy_matrix(data_units, parity_units)
+                                                             : hec::gen_rs_matrix(data_units, parity_units);
+        std::memcpy(out, m.data(), m.size());
+        return HEC_OK;
+    });
+}
+
 int hec_matrix_invert(uint8_t* mat, size_t n) {
     if (!mat || n == 0) return HEC_ERR_INVALID_ARG;
     return guarded([&] { return hec::invert(mat, n) ? HEC_OK : HEC_ERR_SINGULAR; });
@@ -414,7 +428,7 @@ int hec_coder_create_codec(const char* codec, size_t data_units, size_t parity_u
         parity_units > HEC_MAX_PARITY_UNITS)
         return HEC_ERR_INVALID_ARG;
     const std::string name = codec ? codec : "rs";
-    if (name != "rs" && name != "xor") return HEC_ERR_UNSUPPORTED_CODEC;  // e.g. "rs-legacy"
+    if (name != "rs" && name != "xor" && name != "rs-legacy") return HEC_ERR_UNSUPPORTED_CODEC;
     if (name == "xor" && parity_units != 1) return HEC_ERR_INVALID_ARG;  // XOR-k-1 only
     return guarded([&] {
         int ndev = 0;
@@ -425,7 +439,9 @@ int hec_coder_create_codec(const char* codec, size_t data_units, size_t parity_u
         c->m = parity_units;
         c->device = device;
         c->xor_codec = name == "xor";
-        c->enc = c->xor_codec ? hec::gen_xor_matrix(data_units) : hec::gen_rs_matrix(data_units, parity_units);
+        c->enc = c->xor_codec            ? hec::gen_xor_matrix(data_units)
+                 : name == "rs-legacy" ? hec::gen_rs_legacy_matrix(data_units, parity_units)
+                                       : hec::gen_rs_matrix(data_units, parity_units);
         int rc = [&] {
             DeviceGuard g(device);
             if (!g.ok) return fail(HEC_ERR_DEVICE, "hipSetDevice", hipErrorInvalidDevice);

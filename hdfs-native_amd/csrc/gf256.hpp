@@ -61,6 +61,37 @@ inline std::vector<uint8_t> gen_xor_matrix(size_t k) {
     return mat;
 }
 
+// Hadoop's rs-legacy codec (policy 3, RS-LEGACY-6-3-1024k; the reference
+// resolves the schema at ec/mod.rs:118-124 but has no coder for it).  Hadoop
+// 3.x RSRawEncoderLegacy is a systematic cyclic RS code: generator polynomial
+// g(x) = prod_{i<m} (x + 2^i) over this same field (RSUtil.getPrimitivePower,
+// GaloisField.multiply), codeword = data unit i at degree m+i, parity unit j
+// = coefficient j of (sum_i d_i x^(m+i)) mod g(x) (GaloisField.remainder).
+// That is linear in the data, so it is a (k+m) x k matrix like the others:
+// parity row k+j, column i = coefficient j of x^(m+i) mod g(x).  The code is
+// MDS (m consecutive roots, k+m <= 255), so every k rows are invertible and
+// the generic decode gives the unique codeword the legacy decoder finds.
+inline std::vector<uint8_t> gen_rs_legacy_matrix(size_t k, size_t m) {
+    std::vector<uint8_t> g(m + 1, 0);  // g[d] = coefficient of x^d, monic
+    g[0] = 1;
+    for (size_t i = 0; i < m; i++) {   // g *= (x + 2^i)
+        const uint8_t root = kGf.exp[i % 255];
+        for (size_t d = i + 1; d > 0; d--) g[d] = static_cast<uint8_t>(g[d - 1] ^ gf_mul(g[d], root));
+        g[0] = gf_mul(g[0], root);
+    }
+    std::vector<uint8_t> mat((k + m) * k, 0);
+    for (size_t r = 0; r < k; r++) mat[r * k + r] = 1;
+    std::vector<uint8_t> rem(m, 0);  // x^m mod g, then x^(m+i) mod g by shifting
+    for (size_t j = 0; j < m; j++) rem[j] = g[j];  // x^m = sum_{j<m} g_j x^j (char 2)
+    for (size_t c = 0; c < k; c++) {
+        for (size_t j = 0; j < m; j++) mat[(k + j) * k + c] = rem[j];
+        const uint8_t top = rem[m - 1];  // rem * x mod g
+        for (size_t j = m - 1; j > 0; j--) rem[j] = static_cast<uint8_t>(rem[j - 1] ^ gf_mul(top, g[j]));
+        rem[0] = gf_mul(top, g[0]);
+    }
+    return mat;
+}
+
 // Matrix::invert (rust/src/ec/matrix.rs:101-162): Gauss-Jordan over GF(2^8)
 // on [M | I].  The inverse is unique, so any pivoting gives the reference's
 // result; we pick the first non-zero pivot below.  Returns false where the

@@ -39,6 +39,7 @@ CHECKSUM_CRC32C = 2  # crc CRC_32_ISCSI (connection.rs:38)
 # Every symbol include/hdfs_ec_amd.h declares (checked by tests/test_capi.py).
 EXPORTS = [
     "hec_strerror", "hec_abi_version", "hec_last_error", "hec_gen_rs_matrix", "hec_matrix_invert",
+    "hec_gen_codec_matrix",
     "hec_decode_plan", "hec_coder_create", "hec_coder_destroy", "hec_coder_data_units",
     "hec_coder_parity_units", "hec_coder_device", "hec_encode", "hec_decode",
     "hec_encode_device", "hec_decode_device", "hec_gf_matmul_device",
@@ -106,6 +107,7 @@ def _load(path: str = LIB_PATH) -> ctypes.CDLL:
         "hec_abi_version": ([], I),
         "hec_last_error": ([], ctypes.c_char_p),
         "hec_gen_rs_matrix": ([S, S, P], I),
+        "hec_gen_codec_matrix": ([ctypes.c_char_p, S, S, P], I),
         "hec_matrix_invert": ([P, S], I),
         "hec_decode_plan": ([S, S, P, SP, SP, SP, P], I),
         "hec_coder_create": ([S, S, I, ctypes.POINTER(P)], I),
@@ -196,6 +198,14 @@ def _sp(vals: Sequence[int]):
 def gen_rs_matrix(data_units: int, parity_units: int) -> List[List[int]]:
     buf = (ctypes.c_uint8 * ((data_units + parity_units) * data_units))()
     _check(lib.hec_gen_rs_matrix(data_units, parity_units, buf))
+    k = data_units
+    return [list(buf[r * k:(r + 1) * k]) for r in range(data_units + parity_units)]
+
+
+def gen_codec_matrix(codec: str, data_units: int, parity_units: int) -> List[List[int]]:
+    """The (k+m) x k matrix a coder of `codec` ("rs", "xor", "rs-legacy") uses."""
+    buf = (ctypes.c_uint8 * ((data_units + parity_units) * data_units))()
+    _check(lib.hec_gen_codec_matrix(codec.encode(), data_units, parity_units, buf))
     k = data_units
     return [list(buf[r * k:(r + 1) * k]) for r in range(data_units + parity_units)]
 

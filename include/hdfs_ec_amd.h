@@ -71,6 +71,11 @@ const char *hec_last_error(void);
  * row-major, into out[(k+m)*k]. */
 int hec_gen_rs_matrix(size_t data_units, size_t parity_units, uint8_t *out);
 
+/* The same for a codec name as hec_coder_create_codec ("rs", "xor",
+ * "rs-legacy"): the (k+m) x k matrix a coder of that codec encodes and
+ * decodes with.  HEC_ERR_UNSUPPORTED_CODEC for other names. */
+int hec_gen_codec_matrix(const char *codec, size_t data_units, size_t parity_units, uint8_t *out);
+
 /* Matrix::invert (matrix.rs:101-162): in-place inverse of an n x n
  * row-major matrix over GF(2^8).  HEC_ERR_SINGULAR where the reference panics. */
 int hec_matrix_invert(uint8_t *mat, size_t n);
@@ -91,11 +96,13 @@ int hec_decode_plan(size_t data_units, size_t parity_units, const uint8_t *prese
 /* Creates a coder for RS(data_units, parity_units) on HIP device `device`.
  * 1 <= data_units <= HEC_MAX_DATA_UNITS, 1 <= parity_units <= HEC_MAX_PARITY_UNITS. */
 int hec_coder_create(size_t data_units, size_t parity_units, int device, hec_coder_t **out);
-/* Same with a codec name: "rs" (the default above) or "xor" (Hadoop XOR-k-1:
- * parity = XOR of the data units; parity_units must be 1).  The reference
- * names XOR-2-1 (policy 4, ec/mod.rs:119-125) but rejects it on read
- * (mod.rs:74-78); this engine codes it on the same kernels.  Any other name
- * (e.g. "rs-legacy") -> HEC_ERR_UNSUPPORTED_CODEC. */
+/* Same with a codec name: "rs" (the default above), "xor" (Hadoop XOR-k-1:
+ * parity = XOR of the data units; parity_units must be 1) or "rs-legacy"
+ * (Hadoop RSRawEncoderLegacy: systematic cyclic RS, generator roots 2^0 ..
+ * 2^(m-1), data unit i at degree m+i; policy 3, RS-LEGACY-6-3-1024k).  The
+ * reference resolves policies 3 and 4 (ec/mod.rs:118-131) but decodes only
+ * "rs" (mod.rs:69-78); this engine codes all three on the same kernels.  Any
+ * other name -> HEC_ERR_UNSUPPORTED_CODEC. */
 int hec_coder_create_codec(const char *codec, size_t data_units, size_t parity_units, int device,
                            hec_coder_t **out);
 void hec_coder_destroy(hec_coder_t *coder);

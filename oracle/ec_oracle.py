@@ -86,6 +86,91 @@ def gen_xor_matrix(k: int) -> List[List[int]]:
     return [[1 if i == j else 0 for j in range(k)] for i in range(k)] + [[1] * k]
 
 
+# ---- rs-legacy (policy 3) -------------------------------
+# The reference resolves RS-LEGACY-6-3-1024k (ec/mod.rs:118-124) but has no
+# coder for it (mod.rs:69-78 decodes "rs" only), and Hadoop's Java coder is
+# not under /root/reference.  Restated from Hadoop 3.x (published source):
+#   RSUtil.getPrimitivePower  primitivePower[i] = GF.power(2, i)
+#   RSRawEncoderLegacy.<init> gen = prod_{i<m} (primitivePower[i] + x)
+#                             (GaloisField.multiply on coefficient arrays,
+#                              index = degree)
+#   RSRawEncoderLegacy.doEncode  all = [parity units (zeroed), data units];
+#                             GaloisField.remainder(all, gen)
+#   GaloisField.remainder     long division, highest degree first
+# PARITY UNPINNED: no reference-held vector exists for this codec; tests pin
+# it by the code's defining property (every codeword vanishes at 2^0..2^(m-1))
+# and by this long division, which is independent of the matrix form.
+
+def _poly_mul(p: Sequence[int], q: Sequence[int]) -> List[int]:
+    """GaloisField.multiply(int[] p, int[] q): coefficient index = degree."""
+    out = [0] * (len(p) + len(q) - 1)
+    for i, a in enumerate(p):
+        for j, b in enumerate(q):
+            out[i + j] ^= gf_mul(a, b)
+    return out
+
+
+def legacy_generator(m: int) -> List[int]:
+    """RSRawEncoderLegacy generating polynomial, lowest degree first, monic."""
+    gen = [1]
+    for i in range(m):
+        gen = _poly_mul(gen, [EXP[i % 255], 1])
+    return gen
+
+
+def legacy_remainder(dividend: List[np.ndarray], divisor: Sequence[int]) -> None:
+    """GaloisField.remainder(byte[][] dividend, int[] divisor), in place:
+    for i from len(dividend)-len(divisor) down to 0, for every j, unit i+j
+    ^= (unit[i+deg] / divisor[deg]) * divisor[j] (bytewise)."""
+    deg = len(divisor) - 1
+    inv_top = gf_inv(divisor[deg])
+    for i in range(len(dividend) - len(divisor), -1, -1):
+        ratio = MUL_TABLE[inv_top][dividend[i + deg]].copy()  # read before j = deg zeroes it
+        for j in range(len(divisor)):
+            if divisor[j]:
+                dividend[i + j] ^= MUL_TABLE[divisor[j]][ratio]
+
+
+def legacy_encode(k: int, m: int, data: Sequence[np.ndarray]) -> List[np.ndarray]:
+    """RSRawEncoderLegacy.doEncode: parity unit j = coefficient j of
+    (sum_i data_i x^(m+i)) mod gen."""
+    assert len(data) == k
+    n = len(data[0])
+    allu = [np.zeros(n, dtype=np.uint8) for _ in range(m)] + [np.array(d, dtype=np.uint8) for d in data]
+    legacy_remainder(allu, legacy_generator(m))
+    return allu[:m]
+
+
+def gen_rs_legacy_matrix(k: int, m: int) -> List[List[int]]:
+    """(k+m) x k matrix of the legacy code: identity, then parity row j,
+    column i = legacy_encode of the unit vector e_i (the code is linear)."""
+    mat = [[1 if i == j else 0 for j in range(k)] for i in range(k)] + [[0] * k for _ in range(m)]
+    for c in range(k):
+        unit = [np.array([1 if i == c else 0], dtype=np.uint8) for i in range(k)]
+        par = legacy_encode(k, m, unit)
+        for j in range(m):
+            mat[k + j][c] = int(par[j][0])
+    return mat
+
+
+def codec_matrix(codec: str, k: int, m: int) -> List[List[int]]:
+    if codec == "xor":
+        return gen_xor_matrix(k)
+    if codec == "rs-legacy":
+        return gen_rs_legacy_matrix(k, m)
+    if codec == "rs":
+        return gen_rs_matrix(k, m)
+    raise NotImplementedError(f"codec: {codec}")
+
+
+def poly_eval_units(units: Sequence[np.ndarray], x: int) -> np.ndarray:
+    """Evaluates sum_d units[d] * x^d bytewise (Horner, highest degree first)."""
+    acc = np.zeros(len(units[0]), dtype=np.uint8)
+    for u in reversed(units):
+        acc = MUL_TABLE[x][acc] ^ np.asarray(u, dtype=np.uint8)
+    return acc
+
+
 def select_rows(mat: List[List[int]], rows) -> List[List[int]]:
     """matrix.rs:74-84 -- HashSet filter: rows come out in ORIGINAL order."""
     keep = set(rows)
@@ -179,7 +264,7 @@ def decode_plan(k: int, m: int, present: Sequence[bool], codec: str = "rs"):
     if len(valid) < k:
         raise NotEnoughShards("Not enough valid shards")
     surv = valid[:k]
-    enc = gen_xor_matrix(k) if codec == "xor" else gen_rs_matrix(k, m)
+    enc = codec_matrix(codec, k, m)
     dm = invert(select_rows(enc, surv))
     dm = select_rows(dm, invalid)
     return surv, invalid, dm

@@ -105,7 +105,7 @@ unsafe impl Send for GpuCoder {}
 unsafe impl Sync for GpuCoder {}
 
 impl GpuCoder {
-    /// `Coder::new` on device `device` for codec "rs" (or "xor").
+    /// `Coder::new` on device `device` for codec "rs" (or "xor", "rs-legacy").
     pub fn new(codec: &str, data_units: usize, parity_units: usize, device: i32) -> Result<Self> {
         assert_eq!(unsafe { hec_abi_version() }, ABI_VERSION, "libhdfs_ec_amd ABI mismatch");
         let name = std::ffi::CString::new(codec).map_err(|_| HdfsError::InvalidArgument(codec.to_string()))?;

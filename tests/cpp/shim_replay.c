@@ -51,8 +51,8 @@ int main(void) {
         return 2;
     }
     hec_coder_t *bad = NULL;
-    CHECK(hec_coder_create_codec("rs-legacy", K, M, 0, &bad) == HEC_ERR_UNSUPPORTED_CODEC && bad == NULL,
-          "rs-legacy must be UnsupportedErasureCodingPolicy");
+    CHECK(hec_coder_create_codec("lrc", K, M, 0, &bad) == HEC_ERR_UNSUPPORTED_CODEC && bad == NULL,
+          "an unknown codec must be UnsupportedErasureCodingPolicy");
 
     const size_t n = (1u << 20) + 5; /* a full cell plus a tail the 16-B kernels do not cover */
     uint8_t *data[K], *par[M], *want[M];

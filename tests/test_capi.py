@@ -104,9 +104,36 @@ def test_coder_create_without_device_is_clean_error():
     assert not h.value
 
 
+@pytest.mark.parametrize("codec,k,m", [("rs", 6, 3), ("rs", 32, 16), ("xor", 2, 1), ("xor", 7, 1),
+                                       ("rs-legacy", 6, 3), ("rs-legacy", 3, 2), ("rs-legacy", 10, 4),
+                                       ("rs-legacy", 1, 1), ("rs-legacy", 32, 16)])
+def test_gen_codec_matrix_matches_oracle(codec, k, m):
+    # rs-legacy: the oracle's matrix comes from Hadoop's long division
+    # (GaloisField.remainder) on unit vectors; the library's from g(x) directly
+    assert H.gen_codec_matrix(codec, k, m) == O.codec_matrix(codec, k, m)
+
+
+def test_gen_codec_matrix_errors():
+    buf = (ctypes.c_uint8 * 64)()
+    assert H.lib.hec_gen_codec_matrix(b"lrc", 3, 2, buf) == H.HEC_ERR_UNSUPPORTED_CODEC
+    assert H.lib.hec_gen_codec_matrix(b"xor", 3, 2, buf) == H.HEC_ERR_INVALID_ARG
+    assert H.lib.hec_gen_codec_matrix(b"rs-legacy", 0, 2, buf) == H.HEC_ERR_INVALID_ARG
+    assert H.lib.hec_gen_codec_matrix(b"rs-legacy", 3, 2, None) == H.HEC_ERR_INVALID_ARG
+
+
+@pytest.mark.parametrize("k,m", [(3, 2), (6, 3), (10, 4)])
+def test_rs_legacy_is_mds(k, m):
+    # every k of the k+m rows invertible: any k survivors decode (the unique
+    # codeword Hadoop's RSRawDecoderLegacy also finds)
+    mat = H.gen_codec_matrix("rs-legacy", k, m)
+    for rows in itertools.combinations(range(k + m), k):
+        sub = (ctypes.c_uint8 * (k * k))(*[v for r in rows for v in mat[r]])
+        assert H.lib.hec_matrix_invert(sub, k) == H.HEC_OK, rows
+
+
 def test_codec_names_validated():
     h = ctypes.c_void_p()
-    assert H.lib.hec_coder_create_codec(b"rs-legacy", 6, 3, 0, ctypes.byref(h)) == H.HEC_ERR_UNSUPPORTED_CODEC
+    assert H.lib.hec_coder_create_codec(b"lrc", 6, 3, 0, ctypes.byref(h)) == H.HEC_ERR_UNSUPPORTED_CODEC
     assert H.lib.hec_coder_create_codec(b"xor", 2, 2, 0, ctypes.byref(h)) == H.HEC_ERR_INVALID_ARG
     assert not h.value
 

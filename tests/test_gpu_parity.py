@@ -564,6 +564,50 @@ def test_device_decode_mixed_matches_uniform_decode(dev, c_oracle):
     assert torch.equal(o1[:, 0], d[:, 0]) and torch.equal(o1[:, 2], d[:, 2])
 
 
+# ---- rs-legacy codec (parity unpinned, see oracle) -----
+
+@pytest.mark.parametrize("k,m", [(6, 3), (3, 2), (10, 4)])
+def test_rs_legacy_codec_encode_decode(dev, k, m):
+    cell, S = 8192 + 48, 6
+    c = H.Coder(k, m, 0, codec="rs-legacy")
+    data = batch_data(S, k, cell, first=7000 + k)
+    d = torch.from_numpy(data).to(dev)
+    p = torch.zeros((S, m, cell), dtype=torch.uint8, device=dev)
+    H.encode_batch(c, d, p)
+    torch.cuda.synchronize()
+    got = p.cpu().numpy()
+    for s in range(S):  # against Hadoop's long division (GaloisField.remainder)
+        want = O.legacy_encode(k, m, list(data[s]))
+        assert all(np.array_equal(got[s, j], want[j]) for j in range(m)), s
+    # every data-erasure pattern of up to m shards (k = 10: a spread of them)
+    pats = [lost for e in range(1, m + 1) for lost in itertools.combinations(range(k), e)]
+    for lost in (pats if k <= 6 else pats[::7]):
+        out = torch.zeros_like(d)
+        H.decode_batch(c, d, p, list(lost), out)
+        torch.cuda.synchronize()
+        for i in lost:
+            assert torch.equal(out[:, i], d[:, i]), lost
+    # per-stripe patterns with parity shards missing too (other survivor sets)
+    rng = np.random.default_rng(k)
+    masks = []
+    for s in range(S):
+        lost = rng.choice(k + m, size=m, replace=False)
+        masks.append(sum(1 << i for i in range(k + m) if i not in lost))
+    out = torch.zeros_like(d)
+    H.decode_batch_mixed(c, d, p, masks, out)
+    torch.cuda.synchronize()
+    for s, mask in enumerate(masks):
+        for i in range(k):
+            if not (mask >> i) & 1:
+                assert torch.equal(out[s, i], d[s, i]), (s, i)
+    # host API (Coder::decode shape)
+    shards = [bytes(x) for x in data[0]] + [got[0, j].tobytes() for j in range(m)]
+    shards[0] = None
+    shards[k] = None
+    c.decode(shards)
+    assert shards[0] == data[0, 0].tobytes()
+
+
 # ---- XOR-k-1 codec ------------------------------------
 
 @pytest.mark.parametrize("k", [2, 3, 6])
@@ -1076,7 +1120,7 @@ def test_group_errors_and_slot_coders(dev, c_oracle):
     with pytest.raises(H.DeviceError):
         H.CoderGroup(6, 3, [0, 4096])  # no such device: the slots created so far are released
     with pytest.raises(H.UnsupportedErasureCodingPolicy):
-        H.CoderGroup(6, 3, [0], codec="rs-legacy")
+        H.CoderGroup(6, 3, [0], codec="lrc")
     g = H.CoderGroup(6, 3, [0, 0, 0])
     assert len(g) == 3
     from hdfs_native_ec.dist import shard_range

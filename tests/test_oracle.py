@@ -313,3 +313,44 @@ def test_device_crc_tables_vs_oracle(tmp_path):
         want32 = O.chunk_checksums(c, 512, O.CHECKSUM_CRC32).hex()
         assert lines[6 * i:6 * i + 3] == [want32c] * 3, i
         assert lines[6 * i + 3:6 * i + 6] == [want32] * 3, i
+
+
+# ---- rs-legacy (Hadoop RSRawEncoderLegacy; parity unpinned, see oracle) ----
+
+@pytest.mark.parametrize("k,m", [(6, 3), (3, 2), (10, 4), (2, 1), (20, 10)])
+def test_legacy_codewords_vanish_at_generator_roots(k, m):
+    # the defining property of the legacy code: the codeword polynomial
+    # (parity j at degree j, data i at degree m+i) is a multiple of
+    # g(x) = prod_{i<m} (x + 2^i), so it vanishes at 2^0 .. 2^(m-1)
+    rng = np.random.default_rng(100 + k)
+    data = [rng.integers(0, 256, 333, dtype=np.uint8) for _ in range(k)]
+    par = O.legacy_encode(k, m, data)
+    for i in range(m):
+        assert not O.poly_eval_units(par + data, O.EXP[i]).any()
+    # and the long division equals the matrix form the engine runs
+    mat = O.gen_rs_legacy_matrix(k, m)
+    want = O.matmul_shards(O.select_rows(mat, range(k, k + m)), data)
+    assert all(np.array_equal(a, b) for a, b in zip(par, want))
+
+
+def test_legacy_generator_small_cases():
+    # g for m = 1 is x + 1 (parity = XOR of the data, as Hadoop's legacy
+    # coder with one parity unit); m = 2: (x + 1)(x + 2) = x^2 + 3x + 2
+    assert O.legacy_generator(1) == [1, 1]
+    assert O.legacy_generator(2) == [2, 3, 1]
+    assert O.gen_rs_legacy_matrix(4, 1)[4] == [1, 1, 1, 1]
+
+
+def test_legacy_decode_plan_round_trip():
+    k, m = 6, 3
+    rng = np.random.default_rng(7)
+    data = [rng.integers(0, 256, 64, dtype=np.uint8) for _ in range(k)]
+    shards = data + O.legacy_encode(k, m, data)
+    for lost in itertools.combinations(range(k + m), m):
+        present = [i not in lost for i in range(k + m)]
+        surv, miss, dm = O.decode_plan(k, m, present, codec="rs-legacy")
+        if not miss:
+            continue
+        rec = O.matmul_shards(dm, [shards[i] for i in surv])
+        for idx, arr in zip(miss, rec):
+            assert np.array_equal(arr, data[idx])
