@@ -67,6 +67,8 @@ def parse(argv=None):
     ap.add_argument("--traffic", default=TRAFFIC_FILE)
     ap.add_argument("--tune", default="", help="key=value,... passed to hec_tune_set (measurement)")
     ap.add_argument("--encode-only", action="store_true")
+    ap.add_argument("--codec", default="rs", choices=["rs", "xor", "rs-legacy"],
+                    help="coding matrix (same kernels): the reference's rs, xor (m = 1) or Hadoop rs-legacy")
     ap.add_argument("--decode-mode", default="uniform", choices=["uniform", "mixed"],
                     help="uniform: data shards 0..m-1 missing in every stripe; mixed: a random pattern of "
                          "1..m missing data shards per stripe (hec_decode_device_mixed)")
@@ -417,7 +419,7 @@ def main():
     else:
         first, S = rank * args.stripes, args.stripes
         scaling = "weak"
-    coder = H.Coder(k, m, local)
+    coder = H.Coder(k, m, local, codec=args.codec)
     g = torch.Generator(device=dev)
     g.manual_seed(0x5EED_EC00 + first)
     data = torch.randint(0, 256, (S, k, cell), dtype=torch.uint8, device=dev, generator=g)
@@ -504,7 +506,12 @@ def main():
     import ec_oracle
     clib = ec_oracle.load_c_oracle()
     s0 = data[0].cpu().numpy()
-    want = ec_oracle.c_encode(clib, k, m, list(s0))
+    if args.codec == "rs":
+        want = ec_oracle.c_encode(clib, k, m, list(s0))
+    else:  # xor / rs-legacy: the Python oracle's matrix (rs-legacy: Hadoop's long division)
+        want = (ec_oracle.legacy_encode(k, m, list(s0)) if args.codec == "rs-legacy" else
+                ec_oracle.matmul_shards(ec_oracle.select_rows(ec_oracle.codec_matrix(args.codec, k, m),
+                                                              range(k, k + m)), list(s0)))
     assert all(np.array_equal(parity[0, j].cpu().numpy(), want[j]) for j in range(m)), "parity != oracle"
 
     enc_ms = [evs[i][0].elapsed_time(evs[i][1]) for i in range(args.steps)]
@@ -549,6 +556,7 @@ def main():
             "global_stripes": args.global_stripes or S * world,
             "parallelism": f"stripe-sharded x{world}, no collectives",
             "decode_mode": args.decode_mode,
+            "codec": args.codec,
         },
         "roofline": {
             "bound": "hbm",
