@@ -105,7 +105,7 @@ __device__ __forceinline__ void load_task(const CrcArgs& a, uint64_t groups, uin
 
 template <int SCHEME>
 struct CrcShape : crcdev::TableLayout<SCHEME> {
-    static constexpr int kBlock = SCHEME == 16 ? 1024 : (SCHEME <= 1 || SCHEME == 11) ? 256 : 512;
+    static constexpr int kBlock = SCHEME == 16 ? 1024 : (SCHEME <= 1 || crcdev::w11(SCHEME)) ? 256 : 512;
     static constexpr int kWaves = kBlock / 64;
 };
 
@@ -235,6 +235,7 @@ const void* crc_pick(int scheme, int pf) {
     // (profiles/r02_probe_crc_rep2.log)
     if (scheme == 22) return crc_fn<KIND, 22>(pf);
 #endif
+    if (scheme == 12) return crc_fn<KIND, 12>(pf);
     return scheme == 1 ? crc_fn<KIND, 1>(pf) : crc_fn<KIND, 11>(pf);
 }
 
@@ -277,6 +278,7 @@ int launch_checksum(const CrcArgs& in, int device, hipStream_t stream) {
                            : tn.crc_variant == 4 ? 16
                            : tn.crc_variant == 9 ? 0
                            : tn.crc_variant == 6 ? 22
+                           : tn.crc_variant == 7 ? 12
                                                  : 11;
         const int pf = tn.crc_prefetch == 1 ? 1 : 2;  // scheme 16: always 1 (128 VGPRs at 4 waves/SIMD)
         const int waves = scheme == 16 ? CrcShape<16>::kWaves : crcdev::sliced(scheme) ? CrcShape<1>::kWaves : CrcShape<4>::kWaves;

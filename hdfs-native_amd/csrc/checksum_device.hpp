@@ -77,6 +77,67 @@ __device__ __forceinline__ uint32_t quarter_w11(const uint32_t* t, const uint8_t
     return r;
 }
 
+// Scheme 12: fold, then 11-bit slicing over the last 32 B only.  CRC is the
+// remainder mod P, and Q(x) = x^209 + x^144 + x^54 + x^39 + x^14 + 1 is a
+// multiple of the CRC32C polynomial (found by a collision search over
+// residues x^t mod P; CRC32C's Hamming distance 6 up to 5243 bits rules out
+// sparser ones this short).  So a message bit at degree g >= 209 equals the
+// five bits at degrees g - 209 + {0, 14, 39, 54, 144}: in a reflected
+// register (bit b of little-endian dword j = message position 32j + b) it
+// moves 209, 195, 170, 155 and 65 positions later.  Folding dwords 0..23 of
+// the quarter forward that way (one v_alignbit per source pair and offset,
+// 3-input XORs) leaves a 256-bit message with the same remainder: its
+// linear CRC from state 0 is the quarter's.  4 steps = 24 lookups instead of
+// 96, for ~120 more VALU.  Reflected (CRC32C) only; the MSB-first register
+// keeps quarter_w11.  Checked bit for bit by tests/cpp/crc_tables_check.cpp.
+struct Fold {
+    static constexpr int kN = 5, kDwords = 24;                // offsets; folded dwords
+    static constexpr int q[kN] = {6, 6, 5, 4, 2}, s[kN] = {17, 3, 10, 27, 1};  // offset = 32q + s
+};
+
+template <bool REFL>
+__device__ __forceinline__ uint32_t quarter_fold(const uint32_t* t, const uint8_t* row) {
+    if constexpr (!REFL) {
+        return quarter_w11<REFL>(t, row);
+    } else {
+        uint32_t w[32];
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const v4u v = *reinterpret_cast<const v4u*>(row + i * 16);
+            w[4 * i] = v.x, w[4 * i + 1] = v.y, w[4 * i + 2] = v.z, w[4 * i + 3] = v.w;
+        }
+        // target i takes (w[i-q] << s) | (w[i-q-1] >> (32-s)) from folded
+        // sources only (indices < 24); sources are at i-2 or earlier, so
+        // every source is final when a target reads it
+#pragma unroll
+        for (int i = 2; i < 32; i++) {
+            uint32_t acc = w[i], pend = 0;
+            bool has = false;
+#pragma unroll
+            for (int o = 0; o < Fold::kN; o++) {
+                const int hi = i - Fold::q[o], lo = hi - 1;
+                const bool h = hi >= 0 && hi < Fold::kDwords, l = lo >= 0 && lo < Fold::kDwords;
+                if (!h && !l) continue;
+                const uint32_t c = h && l ? __builtin_amdgcn_alignbit(w[hi], w[lo], 32 - Fold::s[o])
+                                   : h    ? w[hi] << Fold::s[o]
+                                          : w[lo] >> (32 - Fold::s[o]);
+                if (has) {
+                    acc = x3(acc, pend, c);
+                    has = false;
+                } else {
+                    pend = c;
+                    has = true;
+                }
+            }
+            w[i] = has ? acc ^ pend : acc;
+        }
+        uint32_t r = 0;
+#pragma unroll
+        for (int i = Fold::kDwords; i < 32; i += 2) r = step8_w11<REFL>(t, r, w[i], w[i + 1]);
+        return r;
+    }
+}
+
 template <bool REFL>
 __device__ __forceinline__ uint32_t quarter_s8(const uint32_t (*tab)[256], const uint8_t* row) {
     uint32_t r = 0;
@@ -183,8 +244,9 @@ __device__ __forceinline__ uint32_t apply_shift_nib(const uint32_t (*t)[16], uin
 // 1024-thread blocks (4 waves per SIMD) with nibble shift tables so the
 // tables (9.5 KiB) and 16 wave images (144 KiB) fit one CU's LDS; 4 / 8 =
 // bank-replicated slicing-by-1; 0 = memory side only.
-constexpr bool sliced(int scheme) { return scheme <= 1 || scheme == 16 || scheme == 11; }
-constexpr bool nib_shift(int scheme) { return scheme == 16 || scheme == 11; }
+constexpr bool w11(int scheme) { return scheme == 11 || scheme == 12; }  // 11-bit field tables
+constexpr bool sliced(int scheme) { return scheme <= 1 || scheme == 16 || w11(scheme); }
+constexpr bool nib_shift(int scheme) { return scheme == 16 || w11(scheme); }
 
 // slice[8][256] (schemes 1, 16) | rep[256][32] (schemes 4, 8) ; shift[3][4][256]
 // (shift_nib[3][8][16] for scheme 16) ; seg[7][4][256] (schemes 4, 8)
@@ -192,7 +254,7 @@ constexpr bool nib_shift(int scheme) { return scheme == 16 || scheme == 11; }
 template <int SCHEME>
 struct TableLayout {
     static constexpr int kMainWords = SCHEME == 22   ? 2 * 256 * 32 + 4 * 256
-                                      : SCHEME == 11 ? 4 * 2048 + 2 * 1024
+                                      : w11(SCHEME) ? 4 * 2048 + 2 * 1024
                                       : sliced(SCHEME) ? 8 * 256
                                                        : 256 * 32;
     static constexpr int kShiftOff = kMainWords;
@@ -207,7 +269,7 @@ struct TableLayout {
 // the step is field bits 0..7, so slice[0][x] = w11[5][x].
 template <int SCHEME>
 struct ByteTable {
-    static constexpr int off = SCHEME == 11 ? 9216 : SCHEME == 22 ? 8192 : 0;
+    static constexpr int off = w11(SCHEME) ? 9216 : SCHEME == 22 ? 8192 : 0;
     static constexpr int stride = sliced(SCHEME) ? 1 : 32;
     static constexpr bool bswap = SCHEME == 22;  // MSB-first kind: stored byte-swapped
 };
@@ -232,7 +294,7 @@ __device__ __forceinline__ void stage_tables(uint32_t* s, const crc::Tables<KIND
             s[t] = REFL ? v : __builtin_bswap32(v);
         }
         for (int t = threadIdx.x; t < 4 * 256; t += BS) s[2 * 256 * 32 + t] = (&tab.seg[5][0][0])[t];
-    } else if constexpr (SCHEME == 11) {
+    } else if constexpr (w11(SCHEME)) {
         constexpr int off[6] = {0, 2048, 4096, 5120, 7168, 9216}, len[6] = {2048, 2048, 1024, 2048, 2048, 1024};
 #pragma unroll
         for (int f = 0; f < 6; f++)
@@ -256,6 +318,8 @@ __device__ __forceinline__ uint32_t quarter(const uint32_t* s, const uint8_t* ro
         return quarter_rep2<REFL>(s, reinterpret_cast<const uint32_t(*)[256]>(s + 2 * 256 * 32), row, lane & 31);
     else if constexpr (SCHEME == 11)
         return quarter_w11<REFL>(s, row);
+    else if constexpr (SCHEME == 12)
+        return quarter_fold<REFL>(s, row);
     else if constexpr (sliced(SCHEME))
         return quarter_s8<REFL>(reinterpret_cast<const uint32_t(*)[256]>(s), row);
     else

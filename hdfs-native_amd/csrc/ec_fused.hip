@@ -581,6 +581,7 @@ const void* encode_fn(int slabs, int scheme, int wpe, bool pair) {
     if (wpe == 3) return scheme == 11 ? encode_sl<K, R, 11, 3>(slabs) : encode_sl<K, R, 1, 3>(slabs);
 #endif
     (void)wpe;
+    if (scheme == 12) return encode_sl<K, R, 12>(slabs, pair);
     return scheme == 11 ? encode_sl<K, R, 11>(slabs, pair) : encode_sl<K, R, 1>(slabs, pair);
 }
 
@@ -591,6 +592,7 @@ const void* verify_fn(int kind, int scheme, int wpe, bool pair) {
     if (wpe == 3) return scheme == 11 ? verify_kind<K, R, 11, 3>(kind) : verify_kind<K, R, 1, 3>(kind);
 #endif
     (void)wpe;
+    if (scheme == 12) return verify_kind<K, R, 12>(kind, pair);
     return scheme == 11 ? verify_kind<K, R, 11>(kind, pair) : verify_kind<K, R, 1>(kind, pair);
 }
 
@@ -652,6 +654,7 @@ int launch_fused(const MatmulArgs& in, const FusedCrcArgs& cs, bool verify, int 
     const int scheme = (!verify && tn.crc_variant == 2) ? 4
                        : tn.crc_variant == 6            ? 22
                        : tn.crc_variant == 1            ? 1
+                       : tn.crc_variant == 7            ? 12
                                                         : 11;
     const int wpe = (tn.fused_wpe == 3 && crcdev::sliced(scheme)) ? 3 : 2;
     // at 4 slabs (two shards per round) the inputs go two at a time: same-box

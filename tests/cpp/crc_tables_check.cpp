@@ -5,6 +5,9 @@
 //   s8  : 4 quarters by slicing-by-8 from state 0, placed with the
 //         "append 384/256/128 zero bytes" byte tables, + final512;
 //   w11 : the same quarters by 11-bit slicing, placed with the nibble tables;
+//   fold: (CRC32C) each quarter's dwords 0..23 folded forward by the sparse
+//         multiple x^209+x^144+x^54+x^39+x^14+1 of the polynomial, then
+//         11-bit slicing over its last 32 B (checksum_device.hpp Fold);
 //   byte: the classic byte-serial loop, from the table slot the 11-bit
 //         scheme's tail reads (w11[5][x]);
 // and printed as hex, one line per chunk, for tests/test_oracle.py to compare
@@ -66,10 +69,29 @@ struct Check {
         for (int q = 0; q < 8; q++) v ^= t.shift_nib[k][q][(r >> (4 * q)) & 15];
         return v;
     }
-    uint32_t chunk(const uint8_t* c, bool w11) const {
+    // scheme 12: the kernel's fold, the same offsets (32q + s) and order
+    uint32_t q_fold(const uint8_t* q) const {
+        static const int kq[5] = {6, 6, 5, 4, 2}, ks[5] = {17, 3, 10, 27, 1};
+        uint32_t w[32];
+        for (int i = 0; i < 32; i++) w[i] = le32(q + 4 * i);
+        for (int i = 2; i < 32; i++)
+            for (int o = 0; o < 5; o++) {
+                const int hi = i - kq[o], lo = hi - 1;
+                const uint32_t h = hi >= 0 && hi < 24 ? w[hi] : 0, l = lo >= 0 && lo < 24 ? w[lo] : 0;
+                w[i] ^= (h << ks[o]) | (l >> (32 - ks[o]));
+            }
+        uint32_t r = 0;
+        for (int i = 24; i < 32; i += 2) {
+            const uint32_t lo = w[i] ^ pre(r), hi = w[i + 1];
+            r = t.w11[0][f0(lo)] ^ t.w11[1][f1(lo)] ^ t.w11[2][f2(lo)] ^ t.w11[3][f0(hi)] ^ t.w11[4][f1(hi)] ^
+                t.w11[5][f2(hi)];
+        }
+        return r;
+    }
+    uint32_t chunk(const uint8_t* c, bool w11, bool fold = false) const {
         uint32_t v = 0;
         for (int qi = 0; qi < 4; qi++) {
-            const uint32_t r = w11 ? q_w11(c + 128 * qi) : q_s8(c + 128 * qi);
+            const uint32_t r = fold ? q_fold(c + 128 * qi) : w11 ? q_w11(c + 128 * qi) : q_s8(c + 128 * qi);
             v ^= qi < 3 ? (w11 ? shift_nib(qi, r) : shift_byte(qi, r)) : r;
         }
         return v ^ t.final512;
@@ -99,8 +121,9 @@ int main(int argc, char** argv) {
     Check<kCksum> cck(kTck);
     for (int k = 0; k < chunks; k++) {
         const uint8_t* c = data.data() + 512 * k;
-        std::printf("%08x %08x %08x %08x %08x %08x\n", c32c.chunk(c, false), c32c.chunk(c, true),
-                    c32c.chunk_bytes(c), cck.chunk(c, false), cck.chunk(c, true), cck.chunk_bytes(c));
+        std::printf("%08x %08x %08x %08x %08x %08x %08x\n", c32c.chunk(c, false), c32c.chunk(c, true),
+                    c32c.chunk_bytes(c), cck.chunk(c, false), cck.chunk(c, true), cck.chunk_bytes(c),
+                    c32c.chunk(c, true, true));
     }
     std::fflush(stdout);
     // the data itself, for the oracle side

@@ -289,9 +289,9 @@ def test_verified_read_row_semantics():
 
 def test_device_crc_tables_vs_oracle(tmp_path):
     """The compile-time tables the CRC kernels read (csrc/checksum_tables.hpp)
-    recombined on the host with the kernels' own algebra (slicing-by-8 and
-    11-bit quarters placed by zero-append tables, plus the byte-serial tail
-    slot) give the oracle's per-512-B-chunk CRC32C and CRC32 bit for bit."""
+    recombined on the host with the kernels' own algebra (slicing-by-8,
+    11-bit and folded quarters placed by zero-append tables, plus the
+    byte-serial tail slot) give the oracle's per-512-B-chunk CRC32C and CRC32 bit for bit."""
     import os
     import shutil
     import subprocess
@@ -306,13 +306,14 @@ def test_device_crc_tables_vs_oracle(tmp_path):
     data = res.stderr
     assert len(data) == 512 * chunks
     lines = res.stdout.decode().split()
-    assert len(lines) == 6 * chunks
+    assert len(lines) == 7 * chunks
     for i in range(chunks):
         c = data[512 * i:512 * (i + 1)]
         want32c = O.chunk_checksums(c, 512, O.CHECKSUM_CRC32C).hex()
         want32 = O.chunk_checksums(c, 512, O.CHECKSUM_CRC32).hex()
-        assert lines[6 * i:6 * i + 3] == [want32c] * 3, i
-        assert lines[6 * i + 3:6 * i + 6] == [want32] * 3, i
+        row = lines[7 * i:7 * i + 7]
+        assert row[0:3] + row[6:7] == [want32c] * 4, i  # s8, w11, byte, fold (scheme 12)
+        assert row[3:6] == [want32] * 3, i
 
 
 # ---- rs-legacy (Hadoop RSRawEncoderLegacy; parity unpinned, see oracle) ----
