@@ -266,21 +266,28 @@ int launch_checksum(const CrcArgs& in, int device, hipStream_t stream) {
     if (aligned && a.bytes_per_checksum == 512) {
         a.groups_per_cell = (a.chunks_per_cell + 15) / 16;
         const uint64_t tasks = a.groups_per_cell * a.n_shards * a.stripes;
-        // default: 11-bit slicing (6 LDS lookups per 8 bytes), 2 tasks of
-        // prefetch.  Interleaved A/B (profiles/r01d_probe_crc_w11.log): 5.32
+        // 11-bit slicing (6 LDS lookups per 8 bytes), 2 tasks of prefetch,
+        // was the default until the fold.  Interleaved A/B (profiles/r01d_probe_crc_w11.log): 5.32
         // TB/s vs 4.84-4.89 for slicing-by-8 (profiles/r01_probe_crc.log: 4.91
         // vs 4.80 replicated, 4 chains, and 4.64, 8 chains; 4.64 for
         // slicing-by-8 at 4 waves per SIMD, r01d_probe_crc_1024.log); the
         // memory side alone reaches 6.4.
+        // default since round 2 (session k): the fold (scheme 12, CRC32C; the
+        // MSB-first kind runs 11-bit slicing inside it) with one task of
+        // prefetch: same box, 9 x 1 MiB x 1024, 1.598 ms (6.05 TB/s) vs 1.804
+        // (5.36) for 11-bit slicing at its best prefetch
+        // (profiles/r02k_fold/probe_crc.log); 11-bit slicing on key 11 = 5
         const int scheme = tn.crc_variant == 1   ? 1
                            : tn.crc_variant == 2 ? 4
                            : tn.crc_variant == 3 ? 8
                            : tn.crc_variant == 4 ? 16
                            : tn.crc_variant == 9 ? 0
                            : tn.crc_variant == 6 ? 22
-                           : tn.crc_variant == 7 ? 12
-                                                 : 11;
-        const int pf = tn.crc_prefetch == 1 ? 1 : 2;  // scheme 16: always 1 (128 VGPRs at 4 waves/SIMD)
+                           : tn.crc_variant == 5 ? 11
+                                                 : 12;
+        // prefetch depth: key 12 (0 = the scheme's default: 1 for the fold, 2 otherwise)
+        const int pf = tn.crc_prefetch == 1 ? 1 : tn.crc_prefetch == 2 ? 2 : scheme == 12 ? 1 : 2;
+        // scheme 16: always 1 (128 VGPRs at 4 waves/SIMD)
         const int waves = scheme == 16 ? CrcShape<16>::kWaves : crcdev::sliced(scheme) ? CrcShape<1>::kWaves : CrcShape<4>::kWaves;
         const int per_cu = (crcdev::sliced(scheme) && scheme != 16) ? 2 : 1;  // LDS: 56 / 77.5 KiB; ~144 / ~154 KiB
         uint64_t grid = (tasks + waves - 1) / waves;

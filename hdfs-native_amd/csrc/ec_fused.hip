@@ -645,17 +645,22 @@ int launch_fused(const MatmulArgs& in, const FusedCrcArgs& cs, bool verify, int 
                       : (tn.fused_slabs == 4 || tn.fused_slabs == 8) ? tn.fused_slabs
                                                                              : fused_slabs(a.k, a.r);
     // checksum lookups (checksum_device.hpp): 11-bit slicing (6 lookups per
-    // 8 bytes) by default, slicing-by-8 on tune key 11 = 1; both in 256-thread
+    // 8 bytes; the default before the fold), slicing-by-8 on tune key 11 = 1; both in 256-thread
     // blocks, 2 per CU.  Same-box A/B (profiles/r02_probe_fused_w11_*.log):
     // encode + CRC 5-7 % faster with 11-bit slicing, decode + verify within
     // +-1 %.  The kernel is bound by its VALU/issue stream more than by the
     // LDS: the bank-replicated tables (conflict-free, half the LDS cycles,
     // 1.5x the VALU) lose 10-20 % (r02_probe_fused_rep2.log).
+    // Default since round 2 (session k): the fold (scheme 12, checksum_device.hpp
+    // quarter_fold), 24 lookups per 128-B quarter instead of 96; same box,
+    // RS(6,3) x 1024 (profiles/r02k_fold/crc63_v*.json): encode + CRC 2.18-2.21
+    // -> 1.96-1.97 ms (4.38-4.43 -> 4.90-4.94 TB/s), decode + verify 1.96-1.99
+    // -> 1.82 ms.  11-bit slicing on key 11 = 5.
     const int scheme = (!verify && tn.crc_variant == 2) ? 4
                        : tn.crc_variant == 6            ? 22
                        : tn.crc_variant == 1            ? 1
-                       : tn.crc_variant == 7            ? 12
-                                                        : 11;
+                       : tn.crc_variant == 5            ? 11
+                                                        : 12;
     const int wpe = (tn.fused_wpe == 3 && crcdev::sliced(scheme)) ? 3 : 2;
     // at 4 slabs (two shards per round) the inputs go two at a time: same-box
     // A/B (profiles/r02_probe_fused_pair.log) RS(10,4) x 512 encode + CRC

@@ -23,7 +23,7 @@ struct Tune {
     int group;              // key 8: stripes per tile-order group (0 = default 4)
     int crc_unfused;        // key 9: 1 = hec_encode_crc_device as encode + checksum passes
     int fused_slabs;        // key 10: fused encode+CRC slabs per wave (0, 4, 8)
-    int crc_variant;        // key 11: 0 default (11-bit), 1 slicing-by-8, 5 11-bit (exp: 2, 3, 4, 6, 9)
+    int crc_variant;        // key 11: 0 default (fold, = 7), 1 slicing-by-8, 5 11-bit (exp: 2, 3, 4, 6, 9)
     int crc_prefetch;       // key 12: CRC kernel register prefetch depth (0 = 2, 1, 2)
     int store_pol;          // key 13 (exp): store cache policy of the pipe kernel
     int host_copy_threads;  // key 14: hec_decode_host_batch host copy threads (0 = 4)
