@@ -344,11 +344,14 @@ int hec_host_free(void *ptr);
  * key 8: tile order, stripes interleaved per group (1 = stripe-major; 0 = default 4)
  * key 9: 1 = hec_encode_crc_device as encode + separate CRC pass (0 = fused)
  * key 10: fused encode+CRC slabs per wave: 0 = default, 4 or 8
- * key 11: CRC lookups: 0 = default (11-bit slicing everywhere), 1 = slice-by-8,
- *         5 = 11-bit slicing; exp 2 / 3 = bank-replicated slice-by-1 with 4 / 8
+ * key 11: CRC lookups: 0 = default (CRC32C: each 128-B quarter folded by the
+ *         sparse multiple x^209+x^144+x^54+x^39+x^14+1 of the polynomial, then
+ *         11-bit slicing over its last 32 B; CRC32: 11-bit slicing), 7 = the
+ *         same, 1 = slice-by-8, 5 = 11-bit slicing everywhere; exp 2 / 3 = bank-replicated slice-by-1 with 4 / 8
  *         chains, 4 = slice-by-8 at 4 waves per SIMD (checksum kernel), 6 =
  *         bank-replicated slice-by-2, 9 = memory side only (WRONG sums)
- * key 12: CRC register prefetch depth in 8-KiB tasks: 0 = default (2), 1 or 2
+ * key 12: CRC register prefetch depth in 8-KiB tasks: 0 = default (1 with the
+ *         fold, else 2), 1 or 2
  * key 13: exp: store cache policy of the pipe kernel (0 = nt, 1 = sc1, 2 = sc0 sc1,
  *         3 = nt sc1, 4 = plain)
  * key 14: host threads that copy the present data cells in hec_decode_host_batch
