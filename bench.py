@@ -82,6 +82,12 @@ def parse(argv=None):
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / rank / reduction plumbing only: no GPU, no engine, value null (CPU tests)")
     ap.add_argument("--spinup", type=float, default=0.5, help="untimed seconds of steps before warmup")
+    ap.add_argument("--extra-configs", type=int, default=-1,
+                    help="also time the other multi-GPU BASELINE configs (RS(10,4) 1 MiB x 2048 and RS(6,3) "
+                         "64 KiB x 65536, both split over the ranks): 1 = yes, 0 = no, -1 = default (yes for the "
+                         "default RS(6,3) run)")
+    ap.add_argument("--verify", default="full", choices=["full", "sample"],
+                    help="post-timing correctness gate: every stripe against the C oracle (full) or stripe 0")
     return ap.parse_args(argv)
 
 
@@ -208,12 +214,18 @@ def dry_run(args, world, rank):
         dist.barrier()
     el = max_over_ranks(time.perf_counter() - t0)
     total = sum_over_ranks(float(S))
+    extra = {}
+    for cfg in EXTRA_CONFIGS:  # the same per-rank split extra_configs() runs
+        _, share = shard_range(cfg["global_stripes"], world, rank)
+        extra[cfg["name"]] = {"scaling": "strong", "stripes_per_gpu_rank0": share,
+                              "stripes_summed_over_ranks": int(sum_over_ranks(float(share))), "value_GiBps": None}
     if rank == 0:
         print(json.dumps({"metric": METRIC, "value": None, "unit": "GiB/s", "n_gpus": world, "dry_run": True,
                           "scaling": "strong" if args.global_stripes else "weak",
                           "config": {"k": args.k, "m": args.m, "cell_bytes": args.cell, "stripes_per_gpu": S,
                                      "global_stripes": args.global_stripes or S * world,
                                      "stripes_summed_over_ranks": int(total)},
+                          "extra_configs": extra,
                           "max_elapsed_s": el}), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -269,6 +281,67 @@ def per_call_leg(H, k, m, cell, calls, oracle_lib):
                    f"hec_decode with data shards 0..{m - 1} missing (the Rust shim's per-row calls); cpu_port = "
                    "oracle/ec_oracle.c on one core, same calls")
     return res
+
+
+def per_call_sizes(H, k, m, oracle_lib):
+    """The per-call drop-in (hec_encode + hec_decode of one row, pageable
+    buffers) by row size, three ways -- the coder's default routing (rows up
+    to its host limit on the host routine), the device forced (host limit 0)
+    and the host routine forced -- beside the CPU port of the reference loop
+    on one core; the crossover is the smallest size where the device wins."""
+    import ctypes
+
+    import numpy as np
+
+    from hdfs_native_ec.synth import batch_data
+    sizes = [16, 512, 4096, 16384, 65536, 262144, 1 << 20]
+    coder = H.Coder(k, m, 0)
+    default_limit = coder.host_limit
+    lib = H.lib
+    rows = []
+    for n in sizes:
+        data = batch_data(1, k, n, first=n)[0]
+        par = np.empty((m, n), dtype=np.uint8)
+        rec = np.empty((k, n), dtype=np.uint8)
+        ins = (ctypes.c_void_p * k)(*[data[i].ctypes.data for i in range(k)])
+        outs = (ctypes.c_void_p * m)(*[par[j].ctypes.data for j in range(m)])
+        shards = (ctypes.c_void_p * (k + m))(*([0] * m + [data[i].ctypes.data for i in range(m, k)] +
+                                                [par[j].ctypes.data for j in range(m)]))
+        recs = (ctypes.c_void_p * (k + m))(*([rec[i].ctypes.data for i in range(k)] + [0] * m))
+        row = {"shard_bytes": n}
+        for name, limit in (("engine", default_limit), ("engine_device", 0), ("engine_host", 1 << 40),
+                            ("cpu_port", None)):
+            if limit is not None:
+                coder.host_limit = limit
+                enc = lambda: lib.hec_encode(coder.handle, ins, n, outs)  # noqa: E731
+                dec = lambda: lib.hec_decode(coder.handle, shards, n, recs)  # noqa: E731
+            else:
+                enc = lambda: oracle_lib.orc_encode(k, m, ins, n, outs)  # noqa: E731
+                dec = lambda: oracle_lib.orc_decode(k, m, shards, n, recs)  # noqa: E731
+            assert enc() == 0 and dec() == 0
+            budget = 0.15 if limit is not None else 0.3
+            per = {}
+            for op, fn in (("encode", enc), ("decode", dec)):
+                reps, t = 0, 0.0
+                t0 = time.perf_counter()
+                while t < budget or reps < 3:
+                    fn()
+                    reps += 1
+                    t = time.perf_counter() - t0
+                per[op] = t / reps
+            assert np.array_equal(rec[:m], data[:m]), f"per-call {name} {n}"
+            row[name] = {"encode_us": round(per["encode"] * 1e6, 3), "decode_us": round(per["decode"] * 1e6, 3),
+                         "encode_GiBps": round(k * n / per["encode"] / GIB, 3)}
+        rows.append(row)
+    coder.host_limit = default_limit
+    coder.close()
+    cross = next((r["shard_bytes"] for r in rows if r["engine_device"]["encode_us"] < r["engine_host"]["encode_us"]),
+                 None)
+    return {"rows": rows, "default_host_limit": default_limit, "host_isa": H.host_isa(),
+            "device_beats_host_from": cross,
+            "note": f"RS({k},{m}), one row per hec_encode / hec_decode (data shards 0..{m - 1} missing), pageable "
+                    "buffers; engine = default routing, engine_device = host limit 0, engine_host = the engine's "
+                    "host routine forced; cpu_port = oracle/ec_oracle.c on one core"}
 
 
 def ref_cases(args):
@@ -408,9 +481,12 @@ def main():
             dist.init_process_group(args.backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    # --tune: measurement knobs exist only in the HEC_EXPERIMENTAL build
+    # (include/hdfs_ec_amd_exp.h); the coder then runs on that library
+    xlib = H.experimental_lib() if args.tune else None
     for kv in filter(None, args.tune.split(",")):
         key, val = kv.split("=")
-        H.tune_set(int(key), int(val))
+        H.tune_set(int(key), int(val), xlib)
 
     k, m, cell = args.k, args.m, args.cell
     if args.global_stripes:
@@ -419,7 +495,7 @@ def main():
     else:
         first, S = rank * args.stripes, args.stripes
         scaling = "weak"
-    coder = H.Coder(k, m, local, codec=args.codec)
+    coder = H.Coder(k, m, local, codec=args.codec, lib=xlib)
     g = torch.Generator(device=dev)
     g.manual_seed(0x5EED_EC00 + first)
     data = torch.randint(0, 256, (S, k, cell), dtype=torch.uint8, device=dev, generator=g)
@@ -494,25 +570,19 @@ def main():
         dist.barrier()
     elapsed = max_over_ranks(t1 - t0, dev)
 
-    # correctness gate (after the timed region): decode reconstructs the erased shards and
-    # one stripe matches the oracle bit for bit
+    # correctness gate (after the timed region): decode reconstructs the
+    # erased shards of every stripe (on the device), and every stripe's parity
+    # and rebuilt cells match the C oracle bit for bit (stripe-parallel on the
+    # host's CPU share; --verify sample: stripe 0 only)
     if not args.encode_only and not mixed:
         assert torch.equal(rec, data[:, :m]), "decode != original"
     if not args.encode_only and mixed:
-        for s_ in range(0, S, max(1, S // 8)):
-            for i in range(k):
-                if not (masks[s_] >> i) & 1:
-                    assert torch.equal(rec[s_, i], data[s_, i]), "mixed decode != original"
+        lost = torch.tensor([[not (mk >> i) & 1 for i in range(k)] for mk in masks], device=dev)
+        assert bool(((rec == data) | ~lost[:, :, None]).all()), "mixed decode != original"
     import ec_oracle
     clib = ec_oracle.load_c_oracle()
-    s0 = data[0].cpu().numpy()
-    if args.codec == "rs":
-        want = ec_oracle.c_encode(clib, k, m, list(s0))
-    else:  # xor / rs-legacy: the Python oracle's matrix (rs-legacy: Hadoop's long division)
-        want = (ec_oracle.legacy_encode(k, m, list(s0)) if args.codec == "rs-legacy" else
-                ec_oracle.matmul_shards(ec_oracle.select_rows(ec_oracle.codec_matrix(args.codec, k, m),
-                                                              range(k, k + m)), list(s0)))
-    assert all(np.array_equal(parity[0, j].cpu().numpy(), want[j]) for j in range(m)), "parity != oracle"
+    verified = verify_batch(args, ec_oracle, clib, data, parity, None if (args.encode_only or mixed) else rec, k, m)
+
 
     enc_ms = [evs[i][0].elapsed_time(evs[i][1]) for i in range(args.steps)]
     dec_ms = [evs[i][1].elapsed_time(evs[i][2]) for i in range(args.steps)] if not args.encode_only else []
@@ -574,7 +644,7 @@ def main():
         },
         "encode_GiBps": round(k * cell * S / (sum(enc_ms) / len(enc_ms) * 1e-3) / GIB, 2),
         "decode_GiBps": round(k * cell * S / (sum(dec_ms) / len(dec_ms) * 1e-3) / GIB, 2) if dec_ms else None,
-        "parity_check": "ok",
+        "parity_check": verified,
     }
 
     if args.crc:
@@ -585,6 +655,7 @@ def main():
     if host_path and rank == 0 and not mixed:
         result["host_path"] = pinned_leg(coder, data, parity, k, m, cell, S, torch)
         result["host_path"]["per_call"] = per_call_leg(H, k, m, cell, 64, clib)
+        result["host_path"]["per_call_by_size"] = per_call_sizes(H, k, m, clib)
 
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         result["cpu_baseline"] = cpu_baseline(k, m, cell, args.cpu_seconds, 1)
@@ -593,11 +664,128 @@ def main():
     elif rank == 0:
         result["cpu_baseline"] = None
 
+    extra = args.extra_configs if args.extra_configs >= 0 else int(
+        (k, m, cell, args.codec, args.decode_mode) == (6, 3, 1 << 20, "rs", "uniform") and not args.global_stripes
+        and not args.encode_only and not args.tune)
+    if extra:
+        del data, parity, rec
+        torch.cuda.empty_cache()
+        result["extra_configs"] = extra_configs(args, H, dist, world, rank, dev, max_over_ranks, shard_range)
+
     if rank == 0:
         print(json.dumps(result), flush=True)
     coder.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def verify_batch(args, ec_oracle, clib, data, parity, rec, k, m):
+    """Every stripe against the oracle (test infrastructure, the checker):
+    parity, and with rec ([S, m, cell] = data shards 0..m-1 rebuilt) the
+    oracle's decode of the same survivors; <= 2 GiB of data per host slice.
+    xor / rs-legacy (and --verify sample): stripe 0 against the Python oracle."""
+    import numpy as np
+    S, _, cell = data.shape
+    if args.codec != "rs" or args.verify == "sample":
+        s0 = data[0].cpu().numpy()
+        want = (ec_oracle.c_encode(clib, k, m, list(s0)) if args.codec == "rs" else
+                ec_oracle.legacy_encode(k, m, list(s0)) if args.codec == "rs-legacy" else
+                ec_oracle.matmul_shards(ec_oracle.select_rows(ec_oracle.codec_matrix(args.codec, k, m),
+                                                              range(k, k + m)), list(s0)))
+        assert all(np.array_equal(parity[0, j].cpu().numpy(), want[j]) for j in range(m)), "parity != oracle"
+        return "ok: stripe 0 vs oracle"
+    threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 8)))
+    present = ((1 << (k + m)) - 1) & ~((1 << m) - 1)
+    step = max(1, (1 << 31) // (k * cell))
+    t0 = time.perf_counter()
+    for a in range(0, S, step):
+        b = min(S, a + step)
+        ec_oracle.c_check_batch(clib, k, m, data[a:b].cpu().numpy(), parity[a:b].cpu().numpy(),
+                                present if rec is not None else None,
+                                rec[a:b].cpu().numpy() if rec is not None else None, threads=threads)
+    return (f"ok: all {S} stripes' parity" + (f" and rebuilt shards 0..{m - 1}" if rec is not None else "") +
+            f" == C oracle ({threads} threads, {time.perf_counter() - t0:.1f} s)")
+
+
+EXTRA_CONFIGS = [  # the other multi-GPU BASELINE configs (BASELINE.json configs[3], [4]), split over the ranks
+    {"name": "rs104_1MiB_x2048", "k": 10, "m": 4, "cell": 1 << 20, "global_stripes": 2048},
+    {"name": "rs63_64KiB_x65536", "k": 6, "m": 3, "cell": 1 << 16, "global_stripes": 65536},
+]
+
+
+def extra_configs(args, H, dist, world, rank, dev, max_over_ranks, shard_range):
+    """RS(10,4) 1 MiB x 2048 and RS(6,3) 64 KiB x 65536, each split into
+    contiguous per-rank shares (strong scaling, no collective): encode +
+    worst-case decode per step, allocation and warmup outside the timed
+    loop, barrier + max-over-ranks time, every rank's batch checked against
+    its own device copy after timing."""
+    import torch
+    out = {}
+    steps = max(3, min(args.steps, 10))
+    stream = torch.cuda.current_stream(dev)
+    sp = stream.cuda_stream
+    for cfg in EXTRA_CONFIGS:
+        k, m, cell = cfg["k"], cfg["m"], cfg["cell"]
+        first, S = shard_range(cfg["global_stripes"], world, rank)
+        coder = H.Coder(k, m, dev.index)
+        g = torch.Generator(device=dev)
+        g.manual_seed(0x5EED_EC00 + first)
+        data = torch.randint(0, 256, (S, k, cell), dtype=torch.uint8, device=dev, generator=g)
+        parity = torch.empty((S, m, cell), dtype=torch.uint8, device=dev)
+        rec = torch.empty((S, m, cell), dtype=torch.uint8, device=dev)
+        dp, ds = H.stripe_layout_ptrs(data, k)
+        pp, ps = H.stripe_layout_ptrs(parity, m)
+        rp, rs = H.stripe_layout_ptrs(rec, m)
+        shard_ptrs = [None] * m + dp[m:] + pp
+        out_ptrs = rp + [0] * (k - m)
+
+        def step(ev=None):
+            if ev:
+                ev[0].record(stream)
+            coder.encode_device(dp, ds, pp, ps, cell, S, sp)
+            if ev:
+                ev[1].record(stream)
+            coder.decode_device(shard_ptrs, ds + ps, out_ptrs, [rs[0]] * k, cell, S, sp)
+            if ev:
+                ev[2].record(stream)
+
+        for _ in range(3):
+            step()
+        torch.cuda.synchronize(dev)
+        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for i in range(steps):
+            step(evs[i])
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        if world > 1:
+            dist.barrier()
+        elapsed = max_over_ranks(t1 - t0, dev)
+        assert torch.equal(rec, data[:, :m]), f"{cfg['name']}: decode != original"
+        launch = [evs[i][0].elapsed_time(evs[i][1]) for i in range(steps)] + \
+                 [evs[i][1].elapsed_time(evs[i][2]) for i in range(steps)]
+        avg_ms = sum(launch) / len(launch)
+        avg_max = max_over_ranks(avg_ms, dev)
+        algo = (k + m) * cell * S
+        total = cfg["global_stripes"]
+        out[cfg["name"]] = {
+            "workload": f"RS({k},{m}) {cell >> 10} KiB cells, {total} stripes split over {world} GPU(s): encode + "
+                        f"decode with data shards {{0..{m - 1}}} missing",
+            "scaling": "strong", "stripes_per_gpu_rank0": S, "steps": steps,
+            "value_GiBps": round(2 * k * cell * total * steps / elapsed / GIB, 2),
+            "ms_per_step": round(elapsed / steps * 1e3, 4),
+            "avg_launch_ms_rank0": round(avg_ms, 4), "avg_launch_ms_max_over_ranks": round(avg_max, 4),
+            "frac_rank0": round(algo / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "algorithmic_bytes_per_launch_rank0": algo,
+            "check": "rebuilt == original on every rank (device)",
+        }
+        coder.close()
+        del data, parity, rec
+        torch.cuda.empty_cache()
+    return out
 
 
 def pinned_leg(coder, data, parity, k, m, cell, S, torch):
@@ -679,16 +867,21 @@ def crc_leg(args, H, coder, data, parity, rec, dp, ds, pp, ps, rp, rs, shard_ptr
     s0_cells = torch.cat([data[0], parity[0]]).cpu().numpy()
     want = b"".join(ec_oracle.chunk_crc32c(s0_cells[i].tobytes(), bpc) for i in range(k + m))
     assert sums[0].cpu().numpy().tobytes() == want, "crc32c != oracle"
+    # algorithmic bytes per launch, the 4-B chunk sums included
+    # (scripts/profile_configs.py crc_leg_bytes): k+m cells + their sums
+    enc_crc_bytes = ((k + m) * cell + 4 * nch * (k + m)) * S
     res = {
         "bytes_per_checksum": bpc,
         "encode_crc_GiBps": round(k * cell * S / t_ec / GIB, 2),
         "encode_crc_ms": round(t_ec * 1e3, 3),
-        "encode_crc_hbm_TBps": round((k + m) * cell * S / t_ec / 1e12, 3),
-        "encode_crc_frac": round((k + m) * cell * S / t_ec / 1e9 / HBM_PEAK_GBS, 4),
+        "encode_crc_hbm_TBps": round(enc_crc_bytes / t_ec / 1e12, 3),
+        "encode_crc_frac": round(enc_crc_bytes / t_ec / 1e9 / HBM_PEAK_GBS, 4),
+        "encode_crc_algorithmic_bytes": enc_crc_bytes,
         "encode_then_crc_GiBps": round(k * cell * S / t_u / GIB, 2),
         "encode_then_crc_ms": round(t_u * 1e3, 3),
-        "crc_only_GBps": round((k + m) * cell * S / t_c / 1e9, 1),
+        "crc_only_GBps": round(enc_crc_bytes / t_c / 1e9, 1),
         "crc_only_ms": round(t_c * 1e3, 3),
+        "crc_only_frac": round(enc_crc_bytes / t_c / 1e9 / HBM_PEAK_GBS, 4),
         "note": "CRC32C of all k+m cells per 512-B chunk (WritePacket::calculate_checksum), big-endian",
     }
     if args.encode_only or mixed:
@@ -732,7 +925,8 @@ def crc_leg(args, H, coder, data, parity, rec, dp, ds, pp, ps, rp, rs, shard_ptr
     res.update({
         "decode_verify_GiBps": round(k * cell * S / tv["fused"] / GIB, 2),
         "decode_verify_ms": round(tv["fused"] * 1e3, 3),
-        "decode_verify_hbm_TBps": round((k + e_) * cell * S / tv["fused"] / 1e12, 3),
+        "decode_verify_hbm_TBps": round(((k + e_) * cell + 4 * nch * k) * S / tv["fused"] / 1e12, 3),
+        "decode_verify_frac": round(((k + e_) * cell + 4 * nch * k) * S / tv["fused"] / 1e9 / HBM_PEAK_GBS, 4),
         "verify_then_decode_GiBps": round(k * cell * S / tv["unfused"] / GIB, 2),
         "verify_then_decode_ms": round(tv["unfused"] * 1e3, 3),
         "read_note": "CRC32C of the k survivors verified against their packet sums while data shards "

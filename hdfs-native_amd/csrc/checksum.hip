@@ -235,8 +235,17 @@ const void* crc_pick(int scheme, int pf) {
     // (profiles/r02_probe_crc_rep2.log)
     if (scheme == 22) return crc_fn<KIND, 22>(pf);
 #endif
+#ifndef HEC_EXPERIMENTAL
+    // product: the fold (CRC32C, one task of prefetch) / 11-bit slicing inside
+    // scheme 12 (CRC32, two tasks)
+    (void)scheme;
+    (void)pf;
+    return KIND == crc::kCrc32c ? reinterpret_cast<const void*>(&checksum_chunks512<KIND, 12, 1>)
+                                : reinterpret_cast<const void*>(&checksum_chunks512<KIND, 12, 2>);
+#else
     if (scheme == 12) return crc_fn<KIND, 12>(pf);
     return scheme == 1 ? crc_fn<KIND, 1>(pf) : crc_fn<KIND, 11>(pf);
+#endif
 }
 
 }  // namespace
@@ -285,8 +294,13 @@ int launch_checksum(const CrcArgs& in, int device, hipStream_t stream) {
                            : tn.crc_variant == 6 ? 22
                            : tn.crc_variant == 5 ? 11
                                                  : 12;
-        // prefetch depth: key 12 (0 = the scheme's default: 1 for the fold, 2 otherwise)
-        const int pf = tn.crc_prefetch == 1 ? 1 : tn.crc_prefetch == 2 ? 2 : scheme == 12 ? 1 : 2;
+        // prefetch depth: key 12 (0 = the scheme's default: 1 for the CRC32C
+        // fold, 2 otherwise -- the MSB-first CRC32 kind has no fold and runs
+        // 11-bit slicing inside scheme 12, whose best depth is 2)
+        const int pf = tn.crc_prefetch == 1   ? 1
+                       : tn.crc_prefetch == 2 ? 2
+                       : (scheme == 12 && a.kind == crc::kCrc32c) ? 1
+                                                                    : 2;
         // scheme 16: always 1 (128 VGPRs at 4 waves/SIMD)
         const int waves = scheme == 16 ? CrcShape<16>::kWaves : crcdev::sliced(scheme) ? CrcShape<1>::kWaves : CrcShape<4>::kWaves;
         const int per_cu = (crcdev::sliced(scheme) && scheme != 16) ? 2 : 1;  // LDS: 56 / 77.5 KiB; ~144 / ~154 KiB

@@ -18,6 +18,7 @@
 #include <atomic>
 #include <fstream>
 #include <map>
+#include <tuple>
 #include <memory>
 #include <cstdio>
 #include <cstring>
@@ -29,10 +30,12 @@
 #include <vector>
 
 #include "../../include/hdfs_ec_amd.h"
+#include "../../include/hdfs_ec_amd_exp.h"
 #include "checksum.hpp"
 #include "checksum_tables.hpp"
 #include "ec_kernels.hpp"
 #include "gf256.hpp"
+#include "host_gf.hpp"
 
 namespace {
 
@@ -59,6 +62,7 @@ struct DecodePlan {
     std::vector<size_t> missing;    // e
     std::vector<uint8_t> matrix;    // e x k
     std::vector<uint32_t> perm;     // e x k x 8: the matrix's v_perm product tables (mixed-decode plan blobs)
+    std::vector<uint64_t> aff;      // e x k: the matrix's host affine qwords (small-row host path)
 };
 
 // Restores the caller's current HIP device on scope exit.
@@ -80,7 +84,14 @@ struct hec_coder {
     size_t k = 0, m = 0;
     int device = 0;
     bool xor_codec = false;
+    std::string codec;         // "rs", "xor" or "rs-legacy"
+    bool pooled = false;       // handed out by hec_coder_acquire (returned by hec_coder_release)
     std::vector<uint8_t> enc;  // (k+m) x k
+    std::vector<uint64_t> enc_aff;  // m x k: host affine qwords of the parity rows
+    // hec_encode / hec_decode rows of at most this many bytes per shard are
+    // coded on the host (hec::host), larger ones go through the device
+    std::atomic<size_t> host_limit{kDefaultHostLimit};
+    static constexpr size_t kDefaultHostLimit = size_t(256) << 10;
 
     // Decode plans keyed by presence bitmask (k+m <= 48), bounded: at most
     // kPlanCacheMax entries; past that the least recently used eighth is
@@ -112,7 +123,11 @@ struct hec_coder {
     size_t call_bytes = 0;
     hipEvent_t ev_call[kCallEvents] = {};
     // verified read, phase 2: stripe lists + mixed-decode workspace (device),
-    // grown geometrically, released by hec_coder_destroy
+    // grown geometrically, released by hec_coder_destroy.  verify_mu is held
+    // from the first list upload until the holder's stream has drained, so two
+    // threads verifying on one coder never share (or free) it under each
+    // other's queued work.
+    std::mutex verify_mu;
     uint8_t* verify_ws = nullptr;
     size_t verify_ws_bytes = 0;
     // mixed decode: two pinned staging images for the workspace upload (so
@@ -162,6 +177,7 @@ DecodePlan compute_plan(size_t k, size_t m, const uint8_t* present, const std::v
         const auto w = hec::perm_table_words(p.matrix[x]);
         std::memcpy(&p.perm[x * 8], w.data(), sizeof(uint32_t) * 8);
     }
+    p.aff = hec::host::affine_matrices(p.matrix.data(), p.matrix.size());
     return p;
 }
 
@@ -334,6 +350,21 @@ int call_through_device(hec_coder* c, const uint8_t* const* in, size_t nin, uint
     return HEC_OK;
 }
 
+// One row of pageable host buffers, routed by size: rows of at most the
+// coder's host limit are coded on this thread (hec::host, no lock), larger
+// ones through the device under the coder's host lock.
+int code_row(hec_coder* c, const uint8_t* mat, const uint64_t* aff, const uint8_t* const* in, size_t nin,
+             uint8_t* const* out, size_t nout, size_t n) {
+    if (n <= c->host_limit.load(std::memory_order_relaxed)) {
+        hec::host::gf_matmul(mat, aff, nout, nin, in, out, n);
+        return HEC_OK;
+    }
+    std::lock_guard<std::mutex> lk(c->host_mu);
+    DeviceGuard g(c->device);
+    if (!g.ok) return fail(HEC_ERR_DEVICE, "hipSetDevice", hipErrorInvalidDevice);
+    return call_through_device(c, in, nin, out, nout, mat, n);
+}
+
 int ensure_dbuf(hec_coder* c, size_t bytes) {
     if (c->dbuf_bytes >= bytes) return HEC_OK;
     if (c->dbuf) (void)hipFree(c->dbuf);
@@ -439,9 +470,11 @@ int hec_coder_create_codec(const char* codec, size_t data_units, size_t parity_u
         c->m = parity_units;
         c->device = device;
         c->xor_codec = name == "xor";
+        c->codec = name;
         c->enc = c->xor_codec            ? hec::gen_xor_matrix(data_units)
                  : name == "rs-legacy" ? hec::gen_rs_legacy_matrix(data_units, parity_units)
                                        : hec::gen_rs_matrix(data_units, parity_units);
+        c->enc_aff = hec::host::affine_matrices(c->enc.data() + data_units * data_units, parity_units * data_units);
         int rc = [&] {
             DeviceGuard g(device);
             if (!g.ok) return fail(HEC_ERR_DEVICE, "hipSetDevice", hipErrorInvalidDevice);
@@ -499,9 +532,123 @@ void hec_coder_destroy(hec_coder_t* c) {
     delete c;
 }
 
+}  // extern "C"
+
+// ---- coder pool: Coder::new per row (gf256.rs:32-38, ec/mod.rs:71) ----------
+
+namespace {
+
+// Idle coders by (codec, k, m, device).  hec_coder_acquire pops one (or
+// creates one); hec_coder_release pushes it back, so a caller that builds a
+// Coder per decoded row pays a mutex and a vector pop, not 3 streams, 60
+// events and the staging buffers.  A coder is exclusively the acquirer's
+// until it is released.  The pool is never destroyed (coders are not freed
+// from a static destructor, after the HIP runtime may be gone).
+struct CoderPool {
+    std::mutex mu;
+    std::map<std::tuple<std::string, size_t, size_t, int>, std::vector<hec_coder*>> idle;
+    std::atomic<unsigned> next_device{0};
+};
+constexpr size_t kPoolIdlePerKey = 64;  // idle coders kept per key; more are destroyed on release
+
+CoderPool& coder_pool() {
+    static CoderPool* p = new CoderPool;
+    return *p;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hec_coder_acquire(const char* codec, size_t data_units, size_t parity_units, int device, hec_coder_t** out) {
+    if (!out) return HEC_ERR_INVALID_ARG;
+    *out = nullptr;
+    if (device < -1) return HEC_ERR_INVALID_ARG;
+    return guarded([&] {
+        const std::string name = codec ? codec : "rs";
+        if (device < 0) {  // any device: round-robin over the visible ones
+            int ndev = 0;
+            HEC_HIP(hipGetDeviceCount(&ndev), HEC_ERR_DEVICE);
+            if (ndev <= 0) return fail(HEC_ERR_DEVICE, "no device", hipErrorNoDevice);
+            device = int(coder_pool().next_device.fetch_add(1, std::memory_order_relaxed) % unsigned(ndev));
+        }
+        CoderPool& pool = coder_pool();
+        {
+            std::lock_guard<std::mutex> lk(pool.mu);
+            auto it = pool.idle.find(std::make_tuple(name, data_units, parity_units, device));
+            if (it != pool.idle.end() && !it->second.empty()) {
+                *out = it->second.back();
+                it->second.pop_back();
+                return int(HEC_OK);
+            }
+        }
+        hec_coder_t* c = nullptr;
+        const int rc = hec_coder_create_codec(name.c_str(), data_units, parity_units, device, &c);
+        if (rc != HEC_OK) return rc;
+        c->pooled = true;
+        *out = c;
+        return int(HEC_OK);
+    });
+}
+
+void hec_coder_release(hec_coder_t* c) {
+    if (!c) return;
+    if (c->pooled) {
+        try {
+            CoderPool& pool = coder_pool();
+            std::lock_guard<std::mutex> lk(pool.mu);
+            auto& v = pool.idle[std::make_tuple(c->codec, c->k, c->m, c->device)];
+            if (v.size() < kPoolIdlePerKey) {
+                v.push_back(c);
+                return;
+            }
+        } catch (...) {
+        }
+    }
+    hec_coder_destroy(c);
+}
+
+size_t hec_coder_pool_trim(void) {
+    std::vector<hec_coder*> drop;
+    try {
+        CoderPool& pool = coder_pool();
+        std::lock_guard<std::mutex> lk(pool.mu);
+        for (auto& kv : pool.idle) drop.insert(drop.end(), kv.second.begin(), kv.second.end());
+        pool.idle.clear();
+    } catch (...) {
+        return 0;
+    }
+    for (hec_coder* c : drop) hec_coder_destroy(c);
+    return drop.size();
+}
+
 size_t hec_coder_data_units(const hec_coder_t* c) { return c ? c->k : 0; }
 size_t hec_coder_parity_units(const hec_coder_t* c) { return c ? c->m : 0; }
 int hec_coder_device(const hec_coder_t* c) { return c ? c->device : -1; }
+
+int hec_coder_set_host_limit(hec_coder_t* c, size_t max_shard_len) {
+    if (!c) return HEC_ERR_INVALID_ARG;
+    c->host_limit.store(max_shard_len, std::memory_order_relaxed);
+    return HEC_OK;
+}
+
+size_t hec_coder_host_limit(const hec_coder_t* c) { return c ? c->host_limit.load(std::memory_order_relaxed) : 0; }
+
+const char* hec_host_isa(void) { return hec::host::isa_name(hec::host::best_isa()); }
+
+int hec_gf_matmul_host(const uint8_t* matrix, size_t rows, size_t cols, const uint8_t* const* in, uint8_t* const* out,
+                       size_t len) {
+    if (!matrix || !in || !out || rows == 0 || cols == 0 || cols > HEC_MAX_DATA_UNITS || len == 0)
+        return HEC_ERR_INVALID_ARG;
+    for (size_t i = 0; i < cols; i++)
+        if (!in[i]) return HEC_ERR_INVALID_ARG;
+    for (size_t j = 0; j < rows; j++)
+        if (!out[j]) return HEC_ERR_INVALID_ARG;
+    return guarded([&] {
+        hec::host::gf_matmul(matrix, nullptr, rows, cols, in, out, len);
+        return int(HEC_OK);
+    });
+}
 
 int hec_gf_matmul_device(hec_coder_t* c, const uint8_t* matrix, size_t rows, size_t cols,
                          const uint8_t* const* d_in, const size_t* in_strides, uint8_t* const* d_out,
@@ -561,10 +708,8 @@ int hec_encode(hec_coder_t* c, const uint8_t* const* data, size_t shard_len, uin
     for (size_t j = 0; j < c->m; j++)
         if (!parity[j]) return HEC_ERR_INVALID_ARG;
     return guarded([&] {
-        std::lock_guard<std::mutex> lk(c->host_mu);
-        DeviceGuard g(c->device);
-        if (!g.ok) return fail(HEC_ERR_DEVICE, "hipSetDevice", hipErrorInvalidDevice);
-        return call_through_device(c, data, c->k, parity, c->m, c->enc.data() + c->k * c->k, shard_len);
+        // small rows are coded on this thread (no PCIe round trip, no lock)
+        return code_row(c, c->enc.data() + c->k * c->k, c->enc_aff.data(), data, c->k, parity, c->m, shard_len);
     });
 }
 
@@ -584,10 +729,7 @@ int hec_decode(hec_coder_t* c, const uint8_t* const* shards, size_t shard_len, u
         uint8_t* dst[HEC_MAX_DATA_UNITS];
         for (size_t r = 0; r < c->k; r++) in[r] = shards[p.survivors[r]];
         for (size_t r = 0; r < p.missing.size(); r++) dst[r] = out[p.missing[r]];
-        std::lock_guard<std::mutex> lk(c->host_mu);
-        DeviceGuard g(c->device);
-        if (!g.ok) return fail(HEC_ERR_DEVICE, "hipSetDevice", hipErrorInvalidDevice);
-        return call_through_device(c, in, c->k, dst, p.missing.size(), p.matrix.data(), shard_len);
+        return code_row(c, p.matrix.data(), p.aff.data(), in, c->k, dst, p.missing.size(), shard_len);
     });
 }
 
@@ -985,6 +1127,160 @@ int hec_decode_host_batch(hec_coder_t* c, const uint8_t* const* h_vertical, size
     });
 }
 
+// ---- whole files: rows of k cells, the last one possibly short ---------------
+// CellBuffer (block_writer.rs:791-851) fills cell 0 of a row before cell 1,
+// so the last row of a file of data_len bytes holds L = data_len - full*k*cell
+// bytes: cell i has min(cell, max(0, L - i*cell)) of them, and encode pads
+// every cell with zeros to len(cell 0) = n0 = min(cell, L) and emits parity
+// cells of n0 bytes.  The reader pads every short or absent cell with zeros
+// to cell_size (CellReader::next_cell, block_reader.rs:343-378) before
+// ec_decode, then trims the row to the file length (:524-549).
+
+size_t hec_encode_rows_workspace_size(const hec_coder_t* c, size_t cell_len) {
+    if (!c) return 0;
+    return c->k * cell_len;  // the last row's short data cells, zero-padded
+}
+
+int hec_encode_rows_host(hec_coder_t* c, const uint8_t* h_data, size_t data_len, uint8_t* h_parity, size_t cell_len,
+                         size_t chunk_stripes) {
+    if (!c || !h_data || !h_parity || cell_len == 0 || chunk_stripes == 0) return HEC_ERR_INVALID_ARG;
+    if (data_len == 0) return HEC_OK;
+    const size_t k = c->k, m = c->m, row = k * cell_len;
+    const size_t full = data_len / row, L = data_len - full * row;
+    if (full) {
+        const int rc = hec_encode_host_batch(c, h_data, h_parity, cell_len, full, chunk_stripes);
+        if (rc != HEC_OK || L == 0) return rc;
+    }
+    return guarded([&] {
+        // the short last row: cells padded to n0 on the host, one row coded
+        const size_t n0 = std::min(cell_len, L);
+        const uint8_t* base = h_data + full * row;
+        std::vector<uint8_t> pad(k * n0, 0);
+        const uint8_t* in[HEC_MAX_DATA_UNITS];
+        uint8_t* out[HEC_MAX_PARITY_UNITS];
+        for (size_t i = 0; i < k; i++) {
+            const size_t have = L > i * cell_len ? std::min(cell_len, L - i * cell_len) : 0;
+            if (have == n0) {
+                in[i] = base + i * cell_len;  // a full-length cell is read in place
+            } else {
+                std::memcpy(&pad[i * n0], base + i * cell_len, have);
+                in[i] = &pad[i * n0];
+            }
+        }
+        uint8_t* pbase = h_parity + full * m * cell_len;
+        for (size_t j = 0; j < m; j++) {
+            out[j] = pbase + j * cell_len;
+            std::memset(out[j] + n0, 0, cell_len - n0);  // the parity cell holds n0 bytes
+        }
+        return code_row(c, c->enc.data() + k * k, c->enc_aff.data(), in, k, out, m, n0);
+    });
+}
+
+int hec_encode_rows_device(hec_coder_t* c, const uint8_t* d_data, size_t data_len, uint8_t* d_parity, size_t cell_len,
+                           void* d_workspace, size_t workspace_bytes, void* hip_stream) {
+    if (!c || !d_data || !d_parity || cell_len == 0) return HEC_ERR_INVALID_ARG;
+    if (data_len == 0) return HEC_OK;
+    const size_t k = c->k, m = c->m, row = k * cell_len;
+    const size_t full = data_len / row, L = data_len - full * row;
+    const uint8_t* din[HEC_MAX_DATA_UNITS];
+    uint8_t* dout[HEC_MAX_PARITY_UNITS];
+    size_t ist[HEC_MAX_DATA_UNITS], ost[HEC_MAX_PARITY_UNITS];
+    for (size_t i = 0; i < k; i++) {
+        din[i] = d_data + i * cell_len;
+        ist[i] = row;
+    }
+    for (size_t j = 0; j < m; j++) {
+        dout[j] = d_parity + j * cell_len;
+        ost[j] = m * cell_len;
+    }
+    if (full) {
+        const int rc = hec_encode_device(c, din, ist, dout, ost, cell_len, full, hip_stream);
+        if (rc != HEC_OK || L == 0) return rc;
+    }
+    const size_t n0 = std::min(cell_len, L);
+    if (!d_workspace || workspace_bytes < k * n0) return HEC_ERR_INVALID_ARG;
+    return guarded([&] {
+        DeviceGuard g(c->device);
+        if (!g.ok) return fail(HEC_ERR_DEVICE, "hipSetDevice", hipErrorInvalidDevice);
+        hipStream_t stream = static_cast<hipStream_t>(hip_stream);
+        const uint8_t* base = d_data + full * row;
+        uint8_t* ws = static_cast<uint8_t*>(d_workspace);
+        for (size_t i = 0; i < k; i++) {
+            const size_t have = L > i * cell_len ? std::min(cell_len, L - i * cell_len) : 0;
+            din[i] = base + i * cell_len;
+            if (have < n0) {  // short or empty cell: zero-padded copy (never read past the data)
+                uint8_t* p = ws + i * n0;
+                if (have)
+                    HEC_HIP(hipMemcpyAsync(p, base + i * cell_len, have, hipMemcpyDeviceToDevice, stream),
+                            HEC_ERR_DEVICE);
+                HEC_HIP(hipMemsetAsync(p + have, 0, n0 - have, stream), HEC_ERR_DEVICE);
+                din[i] = p;
+            }
+        }
+        for (size_t j = 0; j < m; j++) {
+            dout[j] = d_parity + full * m * cell_len + j * cell_len;
+            if (n0 < cell_len) HEC_HIP(hipMemsetAsync(dout[j] + n0, 0, cell_len - n0, stream), HEC_ERR_DEVICE);
+        }
+        return matmul_batch(c->device, c->enc.data() + k * k, m, k, din, ist, dout, ost, n0, 1, stream);
+    });
+}
+
+int hec_decode_rows_host(hec_coder_t* c, const uint8_t* const* h_vertical, const size_t* vertical_len,
+                         size_t cell_len, uint8_t* h_file, size_t file_len, size_t chunk_rows) {
+    if (!c || !h_vertical || !vertical_len || !h_file || cell_len == 0 || chunk_rows == 0) return HEC_ERR_INVALID_ARG;
+    if (file_len == 0) return HEC_OK;
+    const size_t k = c->k, m = c->m, row = k * cell_len;
+    const size_t full = file_len / row, L = file_len - full * row;
+    // full rows: every present shard holds full * cell_len bytes (max_offset)
+    for (size_t i = 0; i < k + m; i++)
+        if (h_vertical[i] && vertical_len[i] < full * cell_len) return HEC_ERR_INVALID_ARG;
+    if (full) {
+        const int rc = hec_decode_host_batch(c, h_vertical, cell_len, full, h_file, chunk_rows);
+        if (rc != HEC_OK || L == 0) return rc;
+    }
+    return guarded([&] {
+        // the short last row: each present cell zero-padded (CellReader), only
+        // the first n0 = min(cell, L) bytes carry data (every data cell of the
+        // row is zero past n0, so are the parity cells)
+        const size_t n0 = std::min(cell_len, L);
+        uint8_t present[HEC_MAX_DATA_UNITS + HEC_MAX_PARITY_UNITS];
+        for (size_t i = 0; i < k + m; i++) present[i] = h_vertical[i] != nullptr;
+        const PlanRef p_ref = cached_plan(c, present);
+        const DecodePlan& p = *p_ref;
+        if (p.status != HEC_OK) return p.status;
+        uint8_t* frow = h_file + full * row;
+        auto cell_have = [&](size_t i) {  // bytes of cell i of the row inside the file
+            return L > i * cell_len ? std::min(cell_len, L - i * cell_len) : size_t(0);
+        };
+        for (size_t i = 0; i < k; i++) {  // present data cells: copied, zero-padded
+            if (!h_vertical[i]) continue;
+            const size_t want = cell_have(i);
+            const size_t avail = vertical_len[i] > full * cell_len ? vertical_len[i] - full * cell_len : 0;
+            const size_t cp = std::min(want, avail);
+            std::memcpy(frow + i * cell_len, h_vertical[i] + full * cell_len, cp);
+            std::memset(frow + i * cell_len + cp, 0, want - cp);
+        }
+        if (p.missing.empty()) return int(HEC_OK);
+        std::vector<uint8_t> surv(k * n0, 0), rec(p.missing.size() * n0);
+        const uint8_t* in[HEC_MAX_DATA_UNITS];
+        uint8_t* out[HEC_MAX_DATA_UNITS];
+        for (size_t r = 0; r < k; r++) {
+            const size_t s = p.survivors[r];
+            const size_t avail = vertical_len[s] > full * cell_len ? vertical_len[s] - full * cell_len : 0;
+            std::memcpy(&surv[r * n0], h_vertical[s] + full * cell_len, std::min(avail, n0));
+            in[r] = &surv[r * n0];
+        }
+        for (size_t r = 0; r < p.missing.size(); r++) out[r] = &rec[r * n0];
+        const int rc = code_row(c, p.matrix.data(), p.aff.data(), in, k, out, p.missing.size(), n0);
+        if (rc != HEC_OK) return rc;
+        for (size_t r = 0; r < p.missing.size(); r++) {
+            const size_t i = p.missing[r];
+            std::memcpy(frow + i * cell_len, &rec[r * n0], cell_have(i));
+        }
+        return int(HEC_OK);
+    });
+}
+
 // ---- Chunk checksums ------------------------------------
 
 namespace {
@@ -1232,6 +1528,18 @@ int hec_decode_verify_device(hec_coder_t* c, int checksum_type, const uint8_t* c
             if (any) F.push_back(uint32_t(s));
         }
         if (F.empty()) return HEC_OK;
+        // phase 2 uses the coder's shared device scratch (verify_ws): one
+        // verifier at a time, and the stream drained before the lock is
+        // released on every path (error returns included), so no queued
+        // launch of ours still reads the scratch when another thread grows it
+        std::lock_guard<std::mutex> vlk(c->verify_mu);
+        struct DrainOnExit {
+            hipStream_t s;
+            ~DrainOnExit() {
+                (void)hipStreamSynchronize(s);
+                (void)hipGetLastError();
+            }
+        } drain_on_exit{stream};
         int status = HEC_OK;
         std::vector<uint8_t> ok(F.size() * n, 0);  // cell verified good
         for (size_t f = 0; f < F.size(); f++)
@@ -1329,8 +1637,6 @@ int hec_decode_verify_device(hec_coder_t* c, int checksum_type, const uint8_t* c
     });
 }
 
-// Tuning knobs for the measurement harness: see include/hdfs_ec_amd.h and
-// csrc/tuning.hpp (atomics, snapshotted per launch).
 // ---- multi-GPU coder group -----------------------------------
 
 }  // extern "C"
@@ -1565,12 +1871,16 @@ int hec_host_free(void* ptr) {
     });
 }
 
+#ifdef HEC_EXPERIMENTAL
+// Measurement knobs (include/hdfs_ec_amd_exp.h): the HEC_EXPERIMENTAL build
+// only.  The product library has no knobs and does not export this symbol.
 int hec_tune_set(int key, int value) {
     const int rc = hec::tune_store(key, value);
     if (rc != HEC_OK)
-        std::snprintf(g_last_error, sizeof(g_last_error),
-                      "hec_tune_set: key %d value %d unknown, out of range or experimental-build only", key, value);
+        std::snprintf(g_last_error, sizeof(g_last_error), "hec_tune_set: key %d value %d unknown or out of range", key,
+                      value);
     return rc;
 }
+#endif
 
 }  // extern "C"

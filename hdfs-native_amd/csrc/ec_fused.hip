@@ -568,10 +568,20 @@ const void* verify_kind(int kind, bool pair = false) {
                                 : reinterpret_cast<const void*>(&gf_fused_crc<K, R, SL, SCHEME, crc::kCksum, true, WPE>);
 }
 
-// scheme 11 (default) = 11-bit slicing, 1 = slicing-by-8 (tune key 11 = 1)
+// scheme 12 (default) = the fold + 11-bit slicing of the tail; the
+// measurement build adds 11 = 11-bit slicing (tune key 11 = 5), 1 =
+// slicing-by-8 (key 11 = 1), the rejected schemes and shapes.  The product
+// library compiles the default slab count / pairing of each (K, R) only.
 template <int K, int R>
 const void* encode_fn(int slabs, int scheme, int wpe, bool pair) {
-#ifdef HEC_EXPERIMENTAL
+#ifndef HEC_EXPERIMENTAL
+    (void)slabs;
+    (void)scheme;
+    (void)wpe;
+    (void)pair;
+    constexpr int SL = fused_slabs(K, R);
+    return reinterpret_cast<const void*>(&gf_fused_crc<K, R, SL, 12, crc::kCrc32c, false, 2, SL == 4>);
+#else
     // rejected (same-box A/B, profiles/r01_probe_fused_scheme.log,
     // r02_probe_fused_rep2.log, r02_probe_fused_wpe3_*.log):
     // bank-replicated slicing-by-1 (4 chains) and slicing-by-2 (tune key 11
@@ -579,21 +589,27 @@ const void* encode_fn(int slabs, int scheme, int wpe, bool pair) {
     if (scheme == 4) return encode_sl<K, R, 4>(slabs);
     if (scheme == 22) return encode_sl<K, R, 22>(slabs);
     if (wpe == 3) return scheme == 11 ? encode_sl<K, R, 11, 3>(slabs) : encode_sl<K, R, 1, 3>(slabs);
-#endif
-    (void)wpe;
     if (scheme == 12) return encode_sl<K, R, 12>(slabs, pair);
     return scheme == 11 ? encode_sl<K, R, 11>(slabs, pair) : encode_sl<K, R, 1>(slabs, pair);
+#endif
 }
 
 template <int K, int R>
 const void* verify_fn(int kind, int scheme, int wpe, bool pair) {
-#ifdef HEC_EXPERIMENTAL
+#ifndef HEC_EXPERIMENTAL
+    (void)scheme;
+    (void)wpe;
+    (void)pair;
+    constexpr int SL = fused_slabs(K, R);
+    return kind == crc::kCrc32c
+               ? reinterpret_cast<const void*>(&gf_fused_crc<K, R, SL, 12, crc::kCrc32c, true, 2, SL == 4>)
+               : reinterpret_cast<const void*>(&gf_fused_crc<K, R, SL, 12, crc::kCksum, true, 2, SL == 4>);
+#else
     if (scheme == 22) return verify_kind<K, R, 22>(kind);
     if (wpe == 3) return scheme == 11 ? verify_kind<K, R, 11, 3>(kind) : verify_kind<K, R, 1, 3>(kind);
-#endif
-    (void)wpe;
     if (scheme == 12) return verify_kind<K, R, 12>(kind, pair);
     return scheme == 11 ? verify_kind<K, R, 11>(kind, pair) : verify_kind<K, R, 1>(kind, pair);
+#endif
 }
 
 #ifdef HEC_EXPERIMENTAL

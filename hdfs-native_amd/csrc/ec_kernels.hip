@@ -630,15 +630,37 @@ const void* pick_r(int k, int r) {
     }
 }
 
-// Shapes compiled: (chunks per lane U, block size BS) in
-// {(1,256),(2,256),(4,256),(1,512),(2,512)}, each with and without
-// non-temporal access.
+#ifdef HEC_EXPERIMENTAL
+// Measurement build: every shape a knob can ask for, (chunks per lane U,
+// block size BS) in {(1,256),(2,256),(4,256),(1,512),(2,512)} plus (8,256)
+// for k <= 3, each with and without non-temporal access.
 template <bool NT>
 const void* pick_shape(int k, int r, int unroll, int bs) {
     if (bs == 512) return unroll >= 2 ? pick_r<2, NT, 512>(k, r) : pick_r<1, NT, 512>(k, r);
-    if (unroll == 4) return pick_r<4, NT, 256>(k, r);
+    if (unroll == 8 && (k == 2 || k == 3)) {
+        switch (r) {
+            case 1: return k == 2 ? vec_fn<2, 1, 8, NT, 256>() : vec_fn<3, 1, 8, NT, 256>();
+            case 2: return k == 2 ? vec_fn<2, 2, 8, NT, 256>() : vec_fn<3, 2, 8, NT, 256>();
+            case 3: return k == 2 ? vec_fn<2, 3, 8, NT, 256>() : vec_fn<3, 3, 8, NT, 256>();
+            default: return k == 2 ? vec_fn<2, 4, 8, NT, 256>() : vec_fn<3, 4, 8, NT, 256>();
+        }
+    }
+    if (unroll >= 4) return pick_r<4, NT, 256>(k, r);
     if (unroll == 2) return pick_r<2, NT, 256>(k, r);
     return pick_r<1, NT, 256>(k, r);
+}
+#endif
+
+// The register kernel for a launch shape.  The product library compiles only
+// the default shapes (default_shape below): (4, 256) for k <= 6 and (2, 512)
+// above, non-temporal.
+template <typename Sh>
+const void* pick_vec(int k, int r, const Sh& sh) {
+#ifdef HEC_EXPERIMENTAL
+    return sh.nt ? pick_shape<true>(k, r, sh.unroll, sh.block) : pick_shape<false>(k, r, sh.unroll, sh.block);
+#else
+    return sh.block == 512 ? pick_r<2, true, 512>(k, r) : pick_r<4, true, 256>(k, r);
+#endif
 }
 
 template <int R, int U, int BS>
@@ -661,9 +683,15 @@ const void* dma_pick(int k, int r) {
     }
 }
 
-// LDS-DMA pipelined kernel: (U, BS) in {(4,256), (2,256), (2,512)} for k <= 6;
-// k = 10 only at (2,256) (10 x 2 x 4 waves x 1 KiB = 80 KiB of LDS).
+// LDS-DMA pipelined kernel: the product default is (4, 256) for k in {2, 3,
+// 6}; the measurement build adds (2,256), (2,512) and k = 10 at (2,256)
+// (10 x 2 x 4 waves x 1 KiB = 80 KiB of LDS).
 const void* pick_dma(int k, int r, int unroll, int bs) {
+#ifndef HEC_EXPERIMENTAL
+    (void)unroll;
+    (void)bs;
+    return dma_pick<4, 256>(k, r);
+#else
     if (k == 10) {
         switch (r) {
             case 1: return reinterpret_cast<const void*>(&gf_matmul_dma<10, 1, 2, 256>);
@@ -675,6 +703,7 @@ const void* pick_dma(int k, int r, int unroll, int bs) {
     if (bs == 512) return dma_pick<2, 512>(k, r);
     if (unroll == 4) return dma_pick<4, 256>(k, r);
     return dma_pick<2, 256>(k, r);
+#endif
 }
 
 // Launch shape chosen from the MI355X sweeps in DESIGN.md ("Tuning"): long
@@ -750,10 +779,8 @@ int launch_gf_matmul(const MatmulArgs& in, int device, hipStream_t stream) {
             tile_mult = ek.tile_mult;
         }
 #endif
-        if (!fn)
-            fn = sh.dma  ? pick_dma(a.k, a.r, sh.unroll, sh.block)
-                 : sh.nt ? pick_shape<true>(a.k, a.r, sh.unroll, sh.block)
-                         : pick_shape<false>(a.k, a.r, sh.unroll, sh.block);
+        if (!fn) fn = sh.dma ? pick_dma(a.k, a.r, sh.unroll, sh.block) : pick_vec(a.k, a.r, sh);
+        if (!fn) return -1;
         const uint64_t tile = uint64_t(sh.block) * sh.unroll * tile_mult;
         const uint64_t tps = (chunks + tile - 1) / tile;
         const uint64_t total = tps * a.stripes;
@@ -817,10 +844,19 @@ const void* mixed_fn() {
         return reinterpret_cast<const void*>(&gf_decode_mixed<K, R, 4, 256, RES, SKIP>);
 }
 
+// The product library compiles the default row policy only (rows past a
+// stripe's e skipped for k <= 6, computed and dropped above); the
+// measurement build both (tune key 20).
 template <int K, int R>
 const void* mixed_sel(bool res, bool skip) {
+#ifdef HEC_EXPERIMENTAL
     return res ? (skip ? mixed_fn<K, R, true, true>() : mixed_fn<K, R, true, false>())
                : (skip ? mixed_fn<K, R, false, true>() : mixed_fn<K, R, false, false>());
+#else
+    (void)skip;
+    constexpr bool SKIP = K <= 6;
+    return res ? mixed_fn<K, R, true, SKIP>() : mixed_fn<K, R, false, SKIP>();
+#endif
 }
 
 template <int K>

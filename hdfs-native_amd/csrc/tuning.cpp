@@ -1,5 +1,5 @@
-// tuning.cpp -- hec_tune_set's knobs as atomics, and the CU-count cache
-// (see tuning.hpp).
+// tuning.cpp -- the CU-count cache and, in the HEC_EXPERIMENTAL measurement
+// build only, hec_tune_set's knobs as atomics (see tuning.hpp).
 #include "tuning.hpp"
 
 #include <hip/hip_runtime.h>
@@ -12,23 +12,19 @@ namespace hec {
 
 namespace {
 
+std::atomic<int> g_cus[64];
+
+#ifdef HEC_EXPERIMENTAL
 constexpr int kKeys = 21;
 std::atomic<int> g_knob[kKeys + 1];  // index = key; zero-initialised (static storage)
 std::atomic<int> g_nt{-1};           // key 2 defaults to -1 (non-temporal on)
 
-constexpr bool kExperimental =
-#ifdef HEC_EXPERIMENTAL
-    true;
-#else
-    false;
-#endif
-
 int load(int key) { return g_knob[key].load(std::memory_order_relaxed); }
-
-std::atomic<int> g_cus[64];
+#endif
 
 }  // namespace
 
+#ifdef HEC_EXPERIMENTAL
 Tune tune_snapshot() {
     Tune t;
     t.unroll = load(1);
@@ -58,38 +54,38 @@ Tune tune_snapshot() {
 int tune_store(int key, int value) {
     bool ok = false;
     switch (key) {
-        case 1: ok = value == 0 || value == 1 || value == 2 || value == 4 || (kExperimental && value == 3); break;
+        case 1: ok = value == 0 || value == 1 || value == 2 || value == 3 || value == 4 || value == 8; break;
         case 2:
             g_nt.store(value < 0 ? -1 : (value ? 1 : 0), std::memory_order_relaxed);
             return HEC_OK;
         case 3: ok = value >= 0 && value <= 16; break;
         case 4: ok = value == 0 || value == 256 || value == 512; break;
-        case 5: ok = (value >= 0 && value <= 2) || (kExperimental && value >= 3 && value <= 5); break;
+        case 5: ok = value >= 0 && value <= 5; break;
         case 6: ok = value >= 0 && value <= 2; break;
         case 7: ok = value >= 0 && value <= 65536; break;
         case 8: ok = value >= 0 && value <= 65536; break;
         case 9: value = value ? 1 : 0; ok = true; break;
         case 10: ok = value == 0 || value == 4 || value == 8; break;
-        case 11:
-            ok = value == 0 || value == 1 || value == 5 || value == 7 ||
-                 (kExperimental && (value == 2 || value == 3 || value == 4 || value == 6 || value == 9));
+        case 11: ok = value == 0 || value == 1 || value == 2 || value == 3 || value == 4 || value == 5 || value == 6 ||
+                      value == 7 || value == 9;
             break;
         case 12: ok = value >= 0 && value <= 2; break;
-        case 13: ok = kExperimental && value >= 0 && value <= 4; break;
+        case 13: ok = value >= 0 && value <= 4; break;
         case 14: ok = value >= 0 && value <= 64; break;
-        case 15: ok = kExperimental && (value == 0 || value == 2 || value == 3); break;
-        case 16: ok = value == 0 || value == 2 || (kExperimental && value == 3); break;
+        case 15: ok = value == 0 || value == 2 || value == 3; break;
+        case 16: ok = value == 0 || value == 2 || value == 3; break;
         case 17: ok = value >= 0 && value <= 65536 && (value & 3) == 0; break;
         case 18: ok = value == 0 || value == 1; break;
         case 19: ok = value >= 0 && value <= 2; break;
         case 20: ok = value >= 0 && value <= 2; break;
-        case 21: ok = value == 0 || value == 1 || (kExperimental && (value == 2 || value == 3)); break;
+        case 21: ok = value >= 0 && value <= 3; break;
         default: ok = false;
     }
     if (!ok) return HEC_ERR_INVALID_ARG;
     g_knob[key].store(value, std::memory_order_relaxed);
     return HEC_OK;
 }
+#endif
 
 int num_cus(int dev) {
     if (dev < 0 || dev >= 64) return 256;

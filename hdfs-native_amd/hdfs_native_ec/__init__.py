@@ -43,12 +43,15 @@ EXPORTS = [
     "hec_decode_plan", "hec_coder_create", "hec_coder_destroy", "hec_coder_data_units",
     "hec_coder_parity_units", "hec_coder_device", "hec_encode", "hec_decode",
     "hec_encode_device", "hec_decode_device", "hec_gf_matmul_device",
-    "hec_encode_host_batch", "hec_tune_set", "hec_decode_mixed_workspace_size",
+    "hec_encode_host_batch", "hec_decode_mixed_workspace_size",
     "hec_decode_device_mixed", "hec_coder_create_codec", "hec_decode_host_batch",
     "hec_crc32c_device", "hec_encode_crc_device", "hec_checksum_device", "hec_checksum_verify_device",
     "hec_decode_verify_device", "hec_group_create", "hec_group_destroy", "hec_group_size", "hec_group_coder",
     "hec_group_range", "hec_group_encode_host_batch", "hec_group_decode_host_batch",
     "hec_device_alloc", "hec_device_free", "hec_device_numa_node", "hec_host_alloc", "hec_host_free",
+    "hec_coder_acquire", "hec_coder_release", "hec_coder_pool_trim", "hec_coder_set_host_limit",
+    "hec_coder_host_limit", "hec_gf_matmul_host", "hec_host_isa", "hec_encode_rows_host",
+    "hec_encode_rows_workspace_size", "hec_encode_rows_device", "hec_decode_rows_host",
 ]
 
 
@@ -128,7 +131,6 @@ def _load(path: str = LIB_PATH) -> ctypes.CDLL:
         "hec_checksum_device": ([P, I, PP, SP, S, S, S, S, P, P], I),
         "hec_checksum_verify_device": ([P, I, PP, SP, S, S, S, S, P, P, P], I),
         "hec_decode_verify_device": ([P, I, PP, SP, PP, SP, S, S, S, P, P, P], I),
-        "hec_tune_set": ([I, I], I),
         "hec_decode_mixed_workspace_size": ([P, S], S),
         "hec_decode_device_mixed": ([P, PP, SP, PP, SP, ctypes.POINTER(ctypes.c_uint64), S, S, P, S, P], I),
         "hec_group_create": ([ctypes.c_char_p, S, S, ctypes.POINTER(I), S, ctypes.POINTER(P)], I),
@@ -143,7 +145,20 @@ def _load(path: str = LIB_PATH) -> ctypes.CDLL:
         "hec_device_numa_node": ([I], I),
         "hec_host_alloc": ([I, S, I, ctypes.POINTER(P)], I),
         "hec_host_free": ([P], I),
+        "hec_coder_acquire": ([ctypes.c_char_p, S, S, I, ctypes.POINTER(P)], I),
+        "hec_coder_release": ([P], None),
+        "hec_coder_pool_trim": ([], S),
+        "hec_coder_set_host_limit": ([P, S], I),
+        "hec_coder_host_limit": ([P], S),
+        "hec_gf_matmul_host": ([P, S, S, PP, PP, S], I),
+        "hec_host_isa": ([], ctypes.c_char_p),
+        "hec_encode_rows_host": ([P, P, S, P, S, S], I),
+        "hec_encode_rows_workspace_size": ([P, S], S),
+        "hec_encode_rows_device": ([P, P, S, P, S, P, S, P], I),
+        "hec_decode_rows_host": ([P, PP, SP, S, P, S, S], I),
     }
+    if hasattr(lib, "hec_tune_set"):  # the measurement build only (include/hdfs_ec_amd_exp.h)
+        sig["hec_tune_set"] = ([I, I], I)
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)
         fn.argtypes = args
@@ -155,13 +170,20 @@ lib = _load()
 _exp_lib = None
 
 
+def experimental_available() -> bool:
+    return os.path.exists(EXP_LIB_PATH)
+
+
 def experimental_lib() -> ctypes.CDLL:
-    """The HEC_EXPERIMENTAL build (lib/libhdfs_ec_amd_exp.so: the default
-    kernels plus the measured-and-rejected variants, selected by tune keys).
-    Pass it as Coder(..., lib=experimental_lib()); its knobs are its own
-    (set them with tune_set(..., lib=experimental_lib()))."""
+    """The HEC_EXPERIMENTAL measurement build (lib/libhdfs_ec_amd_exp.so,
+    `make -C hdfs-native_amd exp`: the default kernels plus every shape a knob
+    can select and the measured-and-rejected variants).  Pass it as
+    Coder(..., lib=experimental_lib()); its knobs (include/hdfs_ec_amd_exp.h)
+    are its own.  The product library has no knobs."""
     global _exp_lib
     if _exp_lib is None:
+        if not experimental_available():
+            raise ImportError(f"{EXP_LIB_PATH} not built: run `make -C hdfs-native_amd exp` (measurement build)")
         _exp_lib = _load(EXP_LIB_PATH)
     return _exp_lib
 
@@ -215,6 +237,31 @@ def matrix_invert(mat: List[List[int]]) -> List[List[int]]:
     buf = (ctypes.c_uint8 * (n * n))(*[v for row in mat for v in row])
     _check(lib.hec_matrix_invert(buf, n))
     return [list(buf[r * n:(r + 1) * n]) for r in range(n)]
+
+
+def host_isa() -> str:
+    """The host routine's ISA (hec_host_isa): avx512bw+gfni, avx2 or scalar."""
+    return lib.hec_host_isa().decode()
+
+
+def gf_matmul_host(matrix: List[List[int]], shards: Sequence) -> List[bytes]:
+    """hec_gf_matmul_host: the hot loop Mul<&[&[u8]]> (matrix.rs:204-231) on
+    the host -- out[j] = sum_i matrix[j][i] * shards[i] over GF(2^8)."""
+    import numpy as np
+    rows, cols = len(matrix), len(matrix[0])
+    ins = [np.ascontiguousarray(np.frombuffer(bytes(x) if not isinstance(x, np.ndarray) else x, dtype=np.uint8))
+           for x in shards]
+    n = len(ins[0])
+    outs = [np.empty(n, dtype=np.uint8) for _ in range(rows)]
+    mat = (ctypes.c_uint8 * (rows * cols))(*[v for r in matrix for v in r])
+    _check(lib.hec_gf_matmul_host(mat, rows, cols, _pp([a.ctypes.data for a in ins]),
+                                  _pp([a.ctypes.data for a in outs]), n))
+    return [o.tobytes() for o in outs]
+
+
+def pool_trim() -> int:
+    """hec_coder_pool_trim: destroys the idle pooled coders."""
+    return lib.hec_coder_pool_trim()
 
 
 def decode_plan(data_units: int, parity_units: int, present: Sequence[bool]):
@@ -289,7 +336,8 @@ def device_numa_node(device: int = 0) -> int:
 
 
 def tune_set(key: int, value: int, lib_=None) -> None:
-    _check((lib_ or lib).hec_tune_set(key, value))
+    """hec_tune_set on the measurement build (default: experimental_lib())."""
+    _check((lib_ or experimental_lib()).hec_tune_set(key, value))
 
 
 def _addr(buf) -> int:
@@ -304,12 +352,21 @@ def _addr(buf) -> int:
 
 
 class Coder:
-    """Drop-in for hdfs_native::ec::gf256::Coder on one MI355X."""
+    """Drop-in for hdfs_native::ec::gf256::Coder on one MI355X.  pooled=True
+    takes the coder from the process-wide pool (hec_coder_acquire; device -1
+    = any) and close() returns it (hec_coder_release)."""
 
-    def __init__(self, data_units: int, parity_units: int, device: int = 0, codec: str = "rs", lib=None):
+    def __init__(self, data_units: int, parity_units: int, device: int = 0, codec: str = "rs", lib=None,
+                 pooled: bool = False):
         self._lib = lib or globals()["lib"]
         h = ctypes.c_void_p()
-        _check(self._lib.hec_coder_create_codec(codec.encode(), data_units, parity_units, device, ctypes.byref(h)))
+        if pooled:
+            _check(self._lib.hec_coder_acquire(codec.encode(), data_units, parity_units, device, ctypes.byref(h)))
+            device = self._lib.hec_coder_device(h)
+        else:
+            _check(self._lib.hec_coder_create_codec(codec.encode(), data_units, parity_units, device,
+                                                    ctypes.byref(h)))
+        self.pooled = pooled
         self.codec = codec
         self._h = h
         self.data_units = data_units
@@ -318,8 +375,18 @@ class Coder:
 
     def close(self) -> None:
         if getattr(self, "_h", None):
-            self._lib.hec_coder_destroy(self._h)
+            (self._lib.hec_coder_release if self.pooled else self._lib.hec_coder_destroy)(self._h)
             self._h = None
+
+    @property
+    def host_limit(self) -> int:
+        """Rows of at most this many bytes per shard are coded on the host
+        (hec_coder_host_limit); 0 = always the device."""
+        return self._lib.hec_coder_host_limit(self._h)
+
+    @host_limit.setter
+    def host_limit(self, max_shard_len: int) -> None:
+        _check(self._lib.hec_coder_set_host_limit(self._h, max_shard_len))
 
     def __del__(self):
         try:
@@ -437,6 +504,26 @@ class Coder:
                           chunk_stripes: int) -> None:
         _check(self._lib.hec_encode_host_batch(self._h, ctypes.c_void_p(h_data_addr), ctypes.c_void_p(h_parity_addr),
                                          cell_len, stripes, chunk_stripes))
+
+    # -- whole files: the last row may be short (CellBuffer semantics) --------
+    def encode_rows_host(self, h_data_addr: int, data_len: int, h_parity_addr: int, cell_len: int,
+                         chunk_stripes: int = 16) -> None:
+        _check(self._lib.hec_encode_rows_host(self._h, ctypes.c_void_p(h_data_addr), data_len,
+                                              ctypes.c_void_p(h_parity_addr), cell_len, chunk_stripes))
+
+    def encode_rows_workspace_size(self, cell_len: int) -> int:
+        return self._lib.hec_encode_rows_workspace_size(self._h, cell_len)
+
+    def encode_rows_device(self, d_data: int, data_len: int, d_parity: int, cell_len: int, workspace: int,
+                           workspace_bytes: int, stream: int = 0) -> None:
+        _check(self._lib.hec_encode_rows_device(self._h, ctypes.c_void_p(d_data), data_len, ctypes.c_void_p(d_parity),
+                                                cell_len, ctypes.c_void_p(workspace), workspace_bytes,
+                                                ctypes.c_void_p(stream)))
+
+    def decode_rows_host(self, vertical_addrs, vertical_lens, cell_len: int, h_file_addr: int, file_len: int,
+                         chunk_rows: int = 16) -> None:
+        _check(self._lib.hec_decode_rows_host(self._h, _pp([a or 0 for a in vertical_addrs]), _sp(vertical_lens),
+                                              cell_len, ctypes.c_void_p(h_file_addr), file_len, chunk_rows))
 
 
 # ---- torch helpers (device memory comes from torch; plumbing only) --------

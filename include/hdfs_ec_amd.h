@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define HEC_ABI_VERSION 3
+#define HEC_ABI_VERSION 4
 
 /* Status codes */
 #define HEC_OK 0
@@ -110,6 +110,29 @@ size_t hec_coder_data_units(const hec_coder_t *coder);
 size_t hec_coder_parity_units(const hec_coder_t *coder);
 int hec_coder_device(const hec_coder_t *coder);
 
+/* Pooled coders for callers that build a Coder per row: the reference
+ * constructs one per decoded row (ec/mod.rs:71-72, Coder::new gf256.rs:32-38)
+ * and one per block writer (block_writer.rs:787).  hec_coder_acquire hands
+ * out an idle coder of the same (codec, data_units, parity_units, device)
+ * from a process-wide pool, or creates one; hec_coder_release returns it (at
+ * most 64 idle per key are kept, the rest destroyed).  An acquired coder is
+ * the caller's alone until released; steady state costs a mutex and a
+ * vector pop -- no stream, event or buffer creation.  device -1 = any device
+ * (round-robin over the visible ones).  hec_coder_release on a coder from
+ * hec_coder_create destroys it.  hec_coder_pool_trim destroys every idle
+ * pooled coder and returns how many. */
+int hec_coder_acquire(const char *codec, size_t data_units, size_t parity_units, int device, hec_coder_t **out);
+void hec_coder_release(hec_coder_t *coder);
+size_t hec_coder_pool_trim(void);
+
+/* Small-row policy of the host-buffer drop-ins below: rows of at most
+ * `max_shard_len` bytes per shard are coded on the calling thread by the
+ * engine's host routine (hec_gf_matmul_host), where a PCIe round trip would
+ * cost more than the row (measured per size); larger rows go
+ * through the device.  Per coder (default 256 KiB); 0 = always the device. */
+int hec_coder_set_host_limit(hec_coder_t *coder, size_t max_shard_len);
+size_t hec_coder_host_limit(const hec_coder_t *coder);
+
 /* ---- Host-buffer drop-ins (synchronous) -------------------------------- */
 
 /* Coder::encode (gf256.rs:61-80).  data[k] host buffers of shard_len bytes
@@ -130,6 +153,16 @@ int hec_encode(hec_coder_t *coder, const uint8_t *const *data, size_t shard_len,
  * shards are present. */
 int hec_decode(hec_coder_t *coder, const uint8_t *const *shards, size_t shard_len,
                uint8_t *const *out);
+
+/* The hot loop Mul<&[&[u8]]> (matrix.rs:204-231) on the host, for rows too
+ * small for the device: out[j] = sum_i matrix[j*cols + i] * in[i], len bytes
+ * each, any length and alignment; AVX-512BW+GFNI affine transforms (one
+ * vgf2p8affineqb per 64 bytes per coefficient), else AVX2 split-nibble
+ * shuffles, else scalar tables (hec_host_isa names the one in use).
+ * 1 <= cols <= HEC_MAX_DATA_UNITS.  Synchronous, thread-safe, no device. */
+int hec_gf_matmul_host(const uint8_t *matrix, size_t rows, size_t cols, const uint8_t *const *in, uint8_t *const *out,
+                       size_t len);
+const char *hec_host_isa(void);
 
 /* ---- Device-resident batched API (asynchronous, on hip_stream) --------- *
  * A batch is `stripes` independent stripes of cell_len-byte cells.  Shard i
@@ -269,6 +302,38 @@ int hec_encode_host_batch(hec_coder_t *coder, const uint8_t *h_data, uint8_t *h_
 int hec_decode_host_batch(hec_coder_t *coder, const uint8_t *const *h_vertical, size_t cell_len, size_t rows,
                           uint8_t *h_file, size_t chunk_rows);
 
+/* ---- Whole files: the last row may be short ------------------------------ *
+ * A file of data_len bytes is rows of k cells in file order (CellBuffer::write,
+ * block_writer.rs:791-805); the last row may hold L < k*cell_len bytes: cell
+ * i of it has min(cell_len, max(0, L - i*cell_len)) bytes.  As
+ * CellBuffer::encode (block_writer.rs:817-851) every cell of that row is
+ * zero-padded to n0 = min(cell_len, L) and its m parity cells are n0 bytes
+ * long; the engine writes them at their [row][m][cell_len] slots and zeroes
+ * the slot bytes past n0.  Full rows run exactly as hec_encode_host_batch /
+ * hec_encode_device. */
+int hec_encode_rows_host(hec_coder_t *coder, const uint8_t *h_data, size_t data_len, uint8_t *h_parity,
+                         size_t cell_len, size_t chunk_stripes);
+
+/* The same on device memory (asynchronous on hip_stream): d_parity holds
+ * ceil(data_len / (k*cell_len)) rows.  The short row's short cells are
+ * zero-padded into d_workspace (hec_encode_rows_workspace_size bytes, untouched
+ * until the stream reaches the work), so nothing is read past d_data +
+ * data_len. */
+size_t hec_encode_rows_workspace_size(const hec_coder_t *coder, size_t cell_len);
+int hec_encode_rows_device(hec_coder_t *coder, const uint8_t *d_data, size_t data_len, uint8_t *d_parity,
+                           size_t cell_len, void *d_workspace, size_t workspace_bytes, void *hip_stream);
+
+/* hec_decode_host_batch over a whole file: h_vertical[i] holds vertical_len[i]
+ * bytes of shard i (its block: max_offset(i), ec/mod.rs:40-60; NULL =
+ * missing), and the file is file_len bytes.  Every cell shorter than cell_len
+ * (or absent past the end of its shard) reads as zeros, as
+ * CellReader::next_cell pads it (block_reader.rs:343-378); the short last row
+ * is decoded like the others and trimmed to file_len (block_reader.rs:
+ * 524-549).  HEC_ERR_INVALID_ARG if a present shard holds fewer than
+ * full_rows * cell_len bytes. */
+int hec_decode_rows_host(hec_coder_t *coder, const uint8_t *const *h_vertical, const size_t *vertical_len,
+                         size_t cell_len, uint8_t *h_file, size_t file_len, size_t chunk_rows);
+
 /* ---- Multi-GPU coder group --------------------------------- *
  * Stripes are independent, so a batch is split into contiguous stripe ranges,
  * one per device, and each range runs on its own device's coder from its own
@@ -325,53 +390,6 @@ int hec_device_numa_node(int device);
 int hec_host_alloc(int device, size_t bytes, int numa_node, void **out);
 int hec_host_free(void *ptr);
 
-/* ---- Measurement knobs (not part of the reference interface) ---------- *
- * Process-wide atomics; every launch reads one consistent snapshot at its
- * start, so a concurrent hec_tune_set only affects launches made after it.
- * "exp" values exist only in the HEC_EXPERIMENTAL build
- * (lib/libhdfs_ec_amd_exp.so, the measured-and-rejected kernel variants);
- * the default library answers them with HEC_ERR_INVALID_ARG.
- * key 1: 16-B column chunks per lane per tile (1, 2 or 4; exp 3; 0 = default)
- * key 2: non-temporal global loads/stores (0 or 1; -1 = default on)
- * key 3: blocks per CU for the grid (1..16; 0 = default)
- * key 4: threads per block (256 or 512; 0 = default)
- * key 5: kernel pipeline: 1 = register, 2 = LDS-DMA prefetch; exp 3 = register
- *        double-buffered (pipe), 4 = output bursts, 5 = double-buffered tiles;
- *        0 = default
- * key 6: store drain per tile in the register kernels: 1 = no drain,
- *        0 / 2 = drain (default)
- * key 7: absolute grid size in blocks (0 = default)
- * key 8: tile order, stripes interleaved per group (1 = stripe-major; 0 = default 4)
- * key 9: 1 = hec_encode_crc_device as encode + separate CRC pass (0 = fused)
- * key 10: fused encode+CRC slabs per wave: 0 = default, 4 or 8
- * key 11: CRC lookups: 0 = default (CRC32C: each 128-B quarter folded by the
- *         sparse multiple x^209+x^144+x^54+x^39+x^14+1 of the polynomial, then
- *         11-bit slicing over its last 32 B; CRC32: 11-bit slicing), 7 = the
- *         same, 1 = slice-by-8, 5 = 11-bit slicing everywhere; exp 2 / 3 = bank-replicated slice-by-1 with 4 / 8
- *         chains, 4 = slice-by-8 at 4 waves per SIMD (checksum kernel), 6 =
- *         bank-replicated slice-by-2, 9 = memory side only (WRONG sums)
- * key 12: CRC register prefetch depth in 8-KiB tasks: 0 = default (1 with the
- *         fold, else 2), 1 or 2
- * key 13: exp: store cache policy of the pipe kernel (0 = nt, 1 = sc1, 2 = sc0 sc1,
- *         3 = nt sc1, 4 = plain)
- * key 14: host threads that copy the present data cells in hec_decode_host_batch
- *         (0 = default 4)
- * key 15: exp: column tiles per store burst of the output-burst kernel (2 or 3)
- * key 16: fused kernels' waves per SIMD: 0 / 2 = default; exp 3
- * key 17: per-call drop-in (hec_encode / hec_decode) pipeline piece in KiB per
- *         shard, a multiple of 4 (0 = default 256)
- * key 18: unaligned layouts: 0 = default (dword-realigning kernel + byte tail),
- *         1 = the byte kernel alone
- * key 19: fused kernels at 4 slabs per wave: 0 / 2 = inputs two at a time
- *         (default), 1 = one at a time
- * key 20: mixed-pattern decode, rows past a stripe's erasure count: 0 = default
- *         (skipped for k <= 6, computed and dropped for larger k), 1 = computed,
- *         2 = skipped
- * key 21: fused kernels' wave roles: 0 / 1 = every wave alternates GF math
- *         and CRC rounds (default); exp 2 = role-split GF / CRC waves (one
- *         512-thread block per CU, RS(6,3) and RS(10,4) only), 3 = role-split
- *         with the CRC waves at raised priority */
-int hec_tune_set(int key, int value);
 
 #ifdef __cplusplus
 }

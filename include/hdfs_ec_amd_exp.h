@@ -1,0 +1,70 @@
+/*
+ * hdfs_ec_amd_exp.h -- measurement knobs of the HEC_EXPERIMENTAL build
+ * (hdfs-native_amd/lib/libhdfs_ec_amd_exp.so, `make -C hdfs-native_amd exp`).
+ *
+ * NOT part of the drop-in interface (include/hdfs_ec_amd.h) and not exported
+ * by the product library: lib/libhdfs_ec_amd.so always runs the measured
+ * default launch shapes and compiles only their kernels.  The measurement
+ * build adds the measured-and-rejected kernel variants and lets a harness
+ * (bench.py --tune, scripts/, tests/test_gpu_experimental.py) pick shapes and
+ * variants for same-box A/B runs.  Knobs are process-wide atomics; every
+ * launch reads one consistent snapshot at its start, so a concurrent
+ * hec_tune_set only affects launches made after it.
+ *
+ * key 1: 16-B column chunks per lane per tile (1, 2, 3, 4; 8 for k <= 3; 0 = default)
+ * key 2: non-temporal global loads/stores (0 or 1; -1 = default on)
+ * key 3: blocks per CU for the grid (1..16; 0 = default)
+ * key 4: threads per block (256 or 512; 0 = default)
+ * key 5: kernel pipeline: 1 = register, 2 = LDS-DMA prefetch, 3 = register
+ *        double-buffered (pipe), 4 = output bursts, 5 = double-buffered tiles;
+ *        0 = default
+ * key 6: store drain per tile in the register kernels: 1 = no drain,
+ *        0 / 2 = drain (default)
+ * key 7: absolute grid size in blocks (0 = default)
+ * key 8: tile order, stripes interleaved per group (1 = stripe-major; 0 = default 4)
+ * key 9: 1 = hec_encode_crc_device as encode + separate CRC pass (0 = fused)
+ * key 10: fused encode+CRC slabs per wave: 0 = default, 4 or 8
+ * key 11: CRC lookups: 0 = default (CRC32C: each 128-B quarter folded by a
+ *         sparse multiple of the polynomial, then 11-bit slicing over its
+ *         tail; CRC32: 11-bit slicing), 7 = the same, 1 = slice-by-8, 5 =
+ *         11-bit slicing everywhere, 2 / 3 = bank-replicated slice-by-1 with
+ *         4 / 8 chains, 4 = slice-by-8 at 4 waves per SIMD (checksum
+ *         kernel), 6 = bank-replicated slice-by-2, 9 = memory side only
+ *         (WRONG sums)
+ * key 12: CRC register prefetch depth in 8-KiB tasks: 0 = default (1 for the
+ *         CRC32C fold, else 2), 1 or 2
+ * key 13: store cache policy of the pipe kernel (0 = nt, 1 = sc1, 2 = sc0 sc1,
+ *         3 = nt sc1, 4 = plain)
+ * key 14: host threads that copy the present data cells in hec_decode_host_batch
+ *         (0 = default 4)
+ * key 15: column tiles per store burst of the output-burst kernel (2 or 3)
+ * key 16: fused kernels' waves per SIMD: 0 / 2 = default; 3
+ * key 17: per-call drop-in (hec_encode / hec_decode) pipeline piece in KiB per
+ *         shard, a multiple of 4 (0 = default 256)
+ * key 18: unaligned layouts: 0 = default (dword-realigning kernel + byte tail),
+ *         1 = the byte kernel alone
+ * key 19: fused kernels at 4 slabs per wave: 0 / 2 = inputs two at a time
+ *         (default), 1 = one at a time
+ * key 20: mixed-pattern decode, rows past a stripe's erasure count: 0 = default
+ *         (skipped for k <= 6, computed and dropped for larger k), 1 = computed,
+ *         2 = skipped
+ * key 21: fused kernels' wave roles: 0 / 1 = every wave alternates GF math
+ *         and CRC rounds (default); 2 = role-split GF / CRC waves (one
+ *         512-thread block per CU, RS(6,3) and RS(10,4) only), 3 = role-split
+ *         with the CRC waves at raised priority
+ * Returns HEC_OK, or HEC_ERR_INVALID_ARG for an unknown key / value.
+ */
+#ifndef HDFS_EC_AMD_EXP_H
+#define HDFS_EC_AMD_EXP_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+int hec_tune_set(int key, int value);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* HDFS_EC_AMD_EXP_H */

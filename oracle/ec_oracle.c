@@ -266,6 +266,30 @@ int orc_encode_batch(size_t k, size_t m, const uint8_t *data, size_t n, size_t s
     return ORC_OK;
 }
 
+/* Stripe-batched decode over [stripe][k][cell] data and [stripe][m][cell]
+ * parity (the bench layout): per stripe one Coder::decode (gf256.rs:84-137)
+ * with shard i present iff bit i of `present` is set; the rebuilt data
+ * shards (ascending missing index) go to out[stripe][e][cell].  Returns the
+ * first non-OK status.  Test infrastructure: the full-batch parity checks. */
+int orc_decode_batch(size_t k, size_t m, const uint8_t *data, const uint8_t *parity, size_t n, size_t stripes,
+                     uint64_t present, uint8_t *out) {
+    const uint8_t *sh[256];
+    uint8_t *o[256];
+    size_t e = 0;
+    for (size_t i = 0; i < k; i++) e += !((present >> i) & 1);
+    for (size_t s = 0; s < stripes; s++) {
+        for (size_t i = 0; i < k + m; i++) {
+            const uint8_t *base = i < k ? data + (s * k + i) * n : parity + (s * m + i - k) * n;
+            sh[i] = ((present >> i) & 1) ? base : NULL;
+        }
+        size_t r = 0;
+        for (size_t i = 0; i < k; i++) o[i] = ((present >> i) & 1) ? NULL : out + (s * e + r++) * n;
+        int rc = orc_decode(k, m, sh, n, o);
+        if (rc != ORC_OK) return rc;
+    }
+    return ORC_OK;
+}
+
 /* ---- CRC32C per checksum chunk --------------------- *
  * rust/src/hdfs/connection.rs:37-38 declares CRC32C = crc 3.4's
  * CRC_32_ISCSI (Castagnoli, reflected poly 0x82F63B78, init and xorout

@@ -320,6 +320,49 @@ def cell_buffer_encode(k: int, m: int, cells: Sequence[bytes]) -> List[bytes]:
     return [bytes(c) for c in cells] + [p.tobytes() for p in parity]
 
 
+def cell_buffer_rows(data: bytes, k: int, cell: int) -> List[List[bytes]]:
+    """block_writer.rs:791-805 + StripedBlockWriter's close: the file bytes
+    split into rows of k cell buffers, buffer i of a row filled to `cell`
+    before buffer i+1; the last row may be partial (short or empty buffers)."""
+    rows, row = [], k * cell
+    for start in range(0, len(data), row):
+        chunk = data[start:start + row]
+        rows.append([chunk[i * cell:(i + 1) * cell] for i in range(k)])
+    return rows
+
+
+def striped_write(data: bytes, k: int, m: int, cell: int) -> List[List[bytes]]:
+    """What the striped writer emits per row: CellBuffer::encode's k data
+    cells (unpadded) + m parity cells of len(buffers[0]) bytes."""
+    return [cell_buffer_encode(k, m, r) for r in cell_buffer_rows(data, k, cell)]
+
+
+def vertical_buffers(rows: List[List[bytes]], k: int, m: int) -> List[bytes]:
+    """Per shard: its cells in row order, i.e. the block each of the k+m
+    single-replica writers stores (its length is max_offset, mod.rs:40-60)."""
+    return [b"".join(r[i] for r in rows) for i in range(k + m)]
+
+
+def striped_read(vertical: List[Optional[bytes]], k: int, m: int, cell: int, file_len: int) -> bytes:
+    """The read side over whole rows (block_reader.rs:480-554): every cell a
+    CellReader returns is zero-padded to cell_size (:343-378; a missing tail
+    is all zeros), ec_decode per row (mod.rs:62-89), cells concatenated in
+    file order, trimmed to the file length."""
+    rows = -(-file_len // (k * cell))
+    out = []
+    for r in range(rows):
+        cells = []
+        for i in range(k + m):
+            v = vertical[i]
+            if v is None:
+                cells.append(None)
+            else:
+                c = v[r * cell:(r + 1) * cell]
+                cells.append(c + b"\0" * (cell - len(c)))
+        out.extend(ec_decode(k, m, cell, "rs", cells))
+    return b"".join(out)[:file_len]
+
+
 def ec_decode(k: int, m: int, cell_size: int, codec: str,
               vertical: List[Optional[bytes]]) -> List[bytes]:
     """mod.rs:62-89: decode when a data shard is missing, then split each data
@@ -463,6 +506,7 @@ def load_c_oracle() -> ctypes.CDLL:
     lib.orc_encode.argtypes = [S, S, P, S, P]
     lib.orc_decode.argtypes = [S, S, P, S, P]
     lib.orc_encode_batch.argtypes = [S, S, P, S, S, P]
+    lib.orc_decode_batch.argtypes = [S, S, P, P, S, S, ctypes.c_uint64, P]
     lib.orc_matmul_shards.argtypes = [P, S, S, P, S, P]
     lib.orc_decode_matrix.argtypes = [S, S, P, P, P, P]
     lib.orc_crc32c.argtypes = [P, S]
@@ -476,6 +520,49 @@ def load_c_oracle() -> ctypes.CDLL:
 
 def _ptrs(arrs):
     return (ctypes.c_void_p * len(arrs))(*[0 if a is None else a.ctypes.data for a in arrs])
+
+
+def c_check_batch(lib, k: int, m: int, data: np.ndarray, parity: np.ndarray, present: int = None,
+                  rebuilt: np.ndarray = None, threads: int = 16) -> None:
+    """Full-batch checker (test infrastructure): every stripe of an engine
+    batch against the C restatement, stripe-parallel on `threads` host
+    threads (ctypes releases the GIL).  data [S,k,cell], parity [S,m,cell]
+    (the engine's); with `present` (bit i = shard i available) and rebuilt
+    [S,e,cell] (the engine's decode, ascending missing data index) the C
+    decode of the same survivors is compared too.  Raises AssertionError
+    naming the first mismatching stripe."""
+    import threading
+    S, _, n = data.shape
+    data = np.ascontiguousarray(data)
+    parity = np.ascontiguousarray(parity)
+    threads = max(1, min(threads, S))
+    errors = []
+
+    def work(t):
+        a, b = S * t // threads, S * (t + 1) // threads
+        if a == b:
+            return
+        want = np.empty((b - a, m, n), dtype=np.uint8)
+        rc = lib.orc_encode_batch(k, m, data[a:b].ctypes.data, n, b - a, want.ctypes.data)
+        if rc != 0 or not np.array_equal(want, parity[a:b]):
+            bad = [s for s in range(a, b) if not np.array_equal(want[s - a], parity[s])][:1]
+            errors.append(f"parity != oracle at stripe {bad}")
+            return
+        if present is not None and rebuilt is not None:
+            e = rebuilt.shape[1]
+            got = np.empty((b - a, e, n), dtype=np.uint8)
+            rc = lib.orc_decode_batch(k, m, data[a:b].ctypes.data, parity[a:b].ctypes.data, n, b - a,
+                                      ctypes.c_uint64(present), got.ctypes.data)
+            if rc != 0 or not np.array_equal(got, rebuilt[a:b]):
+                bad = [s for s in range(a, b) if not np.array_equal(got[s - a], rebuilt[s])][:1]
+                errors.append(f"rebuilt != oracle decode at stripe {bad}")
+
+    ths = [threading.Thread(target=work, args=(t,)) for t in range(threads)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    assert not errors, errors
 
 
 def c_encode(lib, k: int, m: int, data: Sequence[np.ndarray]) -> List[np.ndarray]:

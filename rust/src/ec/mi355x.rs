@@ -17,7 +17,11 @@
 //!     shards"))` when fewer than k are present; parity slots are never
 //!     touched.
 //! and adds the batched forms the striped writer/reader can use instead of
-//! one call per 1 MiB row.
+//! one call per 1 MiB row.  `PooledCoder` is what `Coder::new` holds when the
+//! `mi355x` feature forwards the reference's `Coder` (rust/patches/
+//! ec_mi355x.patch): the reference builds a Coder per decoded row
+//! (`ec/mod.rs:71`), so it takes an idle engine coder from the process-wide
+//! pool (`hec_coder_acquire`) and gives it back on drop.
 
 use std::ffi::{c_char, c_int, c_void, CStr};
 
@@ -48,6 +52,12 @@ unsafe extern "C" {
     fn hec_coder_create_codec(codec: *const c_char, k: usize, m: usize, device: c_int,
                               out: *mut *mut HecCoder) -> c_int;
     fn hec_coder_destroy(c: *mut HecCoder);
+    fn hec_coder_acquire(codec: *const c_char, k: usize, m: usize, device: c_int, out: *mut *mut HecCoder) -> c_int;
+    fn hec_coder_release(c: *mut HecCoder);
+    fn hec_encode_rows_host(c: *mut HecCoder, h_data: *const u8, data_len: usize, h_parity: *mut u8,
+                            cell_len: usize, chunk_stripes: usize) -> c_int;
+    fn hec_decode_rows_host(c: *mut HecCoder, h_vertical: *const *const u8, vertical_len: *const usize,
+                            cell_len: usize, h_file: *mut u8, file_len: usize, chunk_rows: usize) -> c_int;
     fn hec_encode(c: *mut HecCoder, data: *const *const u8, n: usize, parity: *const *mut u8) -> c_int;
     fn hec_decode(c: *mut HecCoder, shards: *const *const u8, n: usize, out: *const *mut u8) -> c_int;
     fn hec_encode_host_batch(c: *mut HecCoder, h_data: *const u8, h_parity: *mut u8, cell_len: usize,
@@ -68,7 +78,7 @@ unsafe extern "C" {
 }
 
 /// The ABI revision this shim is written against (include/hdfs_ec_amd.h).
-const ABI_VERSION: c_int = 3;
+const ABI_VERSION: c_int = 4;
 
 /// Status -> the reference's error kinds (rust/src/error.rs:32-39).
 fn err(rc: c_int) -> HdfsError {
@@ -116,48 +126,39 @@ impl GpuCoder {
 
     /// `Coder::encode` (gf256.rs:61-80): m freshly allocated parity shards.
     pub fn encode(&self, data: &[Bytes]) -> Vec<Bytes> {
-        assert_eq!(data.len(), self.data_units, "data.len() == data_units (gf256.rs:62)");
-        let n = data[0].len();
-        assert!(n > 0, "shards must not be empty (matrix.rs:57)");
-        assert!(data.iter().all(|s| s.len() == n), "equal shard lengths (gf256.rs:65)");
-        let mut parity: Vec<BytesMut> = (0..self.parity_units).map(|_| BytesMut::zeroed(n)).collect();
-        let ins: Vec<*const u8> = data.iter().map(|d| d.as_ptr()).collect();
-        let outs: Vec<*mut u8> = parity.iter_mut().map(|p| p.as_mut_ptr()).collect();
-        let rc = unsafe { hec_encode(self.raw, ins.as_ptr(), n, outs.as_ptr()) };
-        // the reference encode cannot fail; a device error here is a bug or a lost GPU
-        assert_eq!(rc, HEC_OK, "hec_encode: {}", err(rc));
-        parity.into_iter().map(BytesMut::freeze).collect()
+        encode_raw(self.raw, self.data_units, self.parity_units, data)
     }
 
     /// `Coder::decode` (gf256.rs:84-137): rebuilds every missing data slot.
     pub fn decode(&self, data: &mut [Option<Bytes>]) -> Result<()> {
+        decode_raw(self.raw, self.data_units, self.parity_units, data)
+    }
+
+    /// A whole file in file order (rows of k cells, the last one possibly
+    /// short: `CellBuffer::write` / `encode`, block_writer.rs:791-851) ->
+    /// `parity` = ceil(len / (k*cell)) rows of m cells; the short row's parity
+    /// cells hold len(cell 0) bytes, zero past them.
+    pub fn encode_file(&self, data: &[u8], cell: usize, parity: &mut [u8]) -> Result<()> {
         let (k, m) = (self.data_units, self.parity_units);
-        assert_eq!(data.len(), k + m, "data.len() == data_units + parity_units");
-        if data.iter().take(k).all(Option::is_some) {
-            return Ok(()); // gf256.rs:102-105
-        }
-        let n = match data.iter().flatten().next() {
-            Some(b) => b.len(),
-            None => return Err(err(HEC_ERR_NOT_ENOUGH_SHARDS)),
-        };
-        // the engine reads n bytes from every present shard: hold the
-        // reference's equal-length precondition here, before the FFI call
-        assert!(n > 0, "shards must not be empty (matrix.rs:57)");
-        assert!(data.iter().flatten().all(|b| b.len() == n), "equal shard lengths (matrix.rs:215)");
-        let ins: Vec<*const u8> =
-            data.iter().map(|d| d.as_ref().map_or(std::ptr::null(), |b| b.as_ptr())).collect();
-        let mut rec: Vec<Option<BytesMut>> =
-            (0..k + m).map(|i| (i < k && data[i].is_none()).then(|| BytesMut::zeroed(n))).collect();
-        // parity slots (and present data slots) pass null: never written
-        let outs: Vec<*mut u8> =
-            rec.iter_mut().map(|r| r.as_mut().map_or(std::ptr::null_mut(), |b| b.as_mut_ptr())).collect();
-        check(unsafe { hec_decode(self.raw, ins.as_ptr(), n, outs.as_ptr()) })?;
-        for (i, r) in rec.into_iter().enumerate() {
-            if let Some(b) = r {
-                data[i] = Some(b.freeze());
-            }
-        }
-        Ok(())
+        assert!(cell > 0, "cell_len > 0");
+        let rows = data.len().div_ceil(k * cell);
+        assert!(parity.len() >= rows * m * cell, "parity holds ceil(len / row) * m cells");
+        check(unsafe { hec_encode_rows_host(self.raw, data.as_ptr(), data.len(), parity.as_mut_ptr(), cell, 16) })
+    }
+
+    /// The blocks of one block group (`vertical[i]` = shard i's block, any
+    /// length up to its `max_offset`; `None` = failed reader) -> the file's
+    /// `file.len()` bytes, short and absent cells read as zeros
+    /// (`CellReader::next_cell`, block_reader.rs:343-378).
+    pub fn decode_file(&self, vertical: &[Option<&[u8]>], cell: usize, file: &mut [u8]) -> Result<()> {
+        let (k, m) = (self.data_units, self.parity_units);
+        assert_eq!(vertical.len(), k + m, "one slot per shard");
+        assert!(cell > 0, "cell_len > 0");
+        let ptrs: Vec<*const u8> = vertical.iter().map(|v| v.map_or(std::ptr::null(), |b| b.as_ptr())).collect();
+        let lens: Vec<usize> = vertical.iter().map(|v| v.map_or(0, <[u8]>::len)).collect();
+        check(unsafe {
+            hec_decode_rows_host(self.raw, ptrs.as_ptr(), lens.as_ptr(), cell, file.as_mut_ptr(), file.len(), 16)
+        })
     }
 
     /// N full rows in file order (row r = `rows[r*k*cell ..]`) -> N x m
@@ -212,6 +213,91 @@ impl GpuCoder {
 impl Drop for GpuCoder {
     fn drop(&mut self) {
         unsafe { hec_coder_destroy(self.raw) }
+    }
+}
+
+fn encode_raw(raw: *mut HecCoder, k: usize, m: usize, data: &[Bytes]) -> Vec<Bytes> {
+    assert_eq!(data.len(), k, "data.len() == data_units (gf256.rs:62)");
+    let n = data[0].len();
+    assert!(n > 0, "shards must not be empty (matrix.rs:57)");
+    assert!(data.iter().all(|s| s.len() == n), "equal shard lengths (gf256.rs:65)");
+    let mut parity: Vec<BytesMut> = (0..m).map(|_| BytesMut::zeroed(n)).collect();
+    let ins: Vec<*const u8> = data.iter().map(|d| d.as_ptr()).collect();
+    let outs: Vec<*mut u8> = parity.iter_mut().map(|p| p.as_mut_ptr()).collect();
+    let rc = unsafe { hec_encode(raw, ins.as_ptr(), n, outs.as_ptr()) };
+    // the reference encode cannot fail; a device error here is a bug or a lost GPU
+    assert_eq!(rc, HEC_OK, "hec_encode: {}", err(rc));
+    parity.into_iter().map(BytesMut::freeze).collect()
+}
+
+fn decode_raw(raw: *mut HecCoder, k: usize, m: usize, data: &mut [Option<Bytes>]) -> Result<()> {
+    assert_eq!(data.len(), k + m, "data.len() == data_units + parity_units");
+    if data.iter().take(k).all(Option::is_some) {
+        return Ok(()); // gf256.rs:102-105
+    }
+    let n = match data.iter().flatten().next() {
+        Some(b) => b.len(),
+        None => return Err(err(HEC_ERR_NOT_ENOUGH_SHARDS)),
+    };
+    // the engine reads n bytes from every present shard: hold the
+    // reference's equal-length precondition here, before the FFI call
+    assert!(n > 0, "shards must not be empty (matrix.rs:57)");
+    assert!(data.iter().flatten().all(|b| b.len() == n), "equal shard lengths (matrix.rs:215)");
+    let ins: Vec<*const u8> = data.iter().map(|d| d.as_ref().map_or(std::ptr::null(), |b| b.as_ptr())).collect();
+    let mut rec: Vec<Option<BytesMut>> =
+        (0..k + m).map(|i| (i < k && data[i].is_none()).then(|| BytesMut::zeroed(n))).collect();
+    // parity slots (and present data slots) pass null: never written
+    let outs: Vec<*mut u8> =
+        rec.iter_mut().map(|r| r.as_mut().map_or(std::ptr::null_mut(), |b| b.as_mut_ptr())).collect();
+    check(unsafe { hec_decode(raw, ins.as_ptr(), n, outs.as_ptr()) })?;
+    for (i, r) in rec.into_iter().enumerate() {
+        if let Some(b) = r {
+            data[i] = Some(b.freeze());
+        }
+    }
+    Ok(())
+}
+
+/// The engine coder behind the reference's `Coder` when the `mi355x` feature
+/// forwards it (rust/patches/ec_mi355x.patch): `Coder::new` acquires one from
+/// the process-wide pool, drop releases it.  `Coder::new` runs per decoded
+/// row (ec/mod.rs:71) and per block writer (block_writer.rs:787), so a pool
+/// hit costs a mutex and a vector pop -- no streams, events or buffers are
+/// created (`tests/cpp/shim_replay.c` times 10,000 cycles).  The device is
+/// `HDFS_EC_AMD_DEVICE` if set, else any (round-robin over the visible GPUs).
+/// Rows below the coder's host limit are coded on the calling thread.
+pub struct PooledCoder {
+    raw: *mut HecCoder,
+    data_units: usize,
+    parity_units: usize,
+}
+
+unsafe impl Send for PooledCoder {}
+unsafe impl Sync for PooledCoder {}
+
+impl PooledCoder {
+    pub fn acquire(codec: &str, data_units: usize, parity_units: usize) -> Result<Self> {
+        assert_eq!(unsafe { hec_abi_version() }, ABI_VERSION, "libhdfs_ec_amd ABI mismatch");
+        let device: i32 =
+            std::env::var("HDFS_EC_AMD_DEVICE").ok().and_then(|v| v.parse().ok()).unwrap_or(-1);
+        let name = std::ffi::CString::new(codec).map_err(|_| HdfsError::InvalidArgument(codec.to_string()))?;
+        let mut raw = std::ptr::null_mut();
+        check(unsafe { hec_coder_acquire(name.as_ptr(), data_units, parity_units, device, &mut raw) })?;
+        Ok(Self { raw, data_units, parity_units })
+    }
+
+    pub fn encode(&self, data: &[Bytes]) -> Vec<Bytes> {
+        encode_raw(self.raw, self.data_units, self.parity_units, data)
+    }
+
+    pub fn decode(&self, data: &mut [Option<Bytes>]) -> Result<()> {
+        decode_raw(self.raw, self.data_units, self.parity_units, data)
+    }
+}
+
+impl Drop for PooledCoder {
+    fn drop(&mut self) {
+        unsafe { hec_coder_release(self.raw) }
     }
 }
 

@@ -42,10 +42,44 @@ KERNEL_RE = "gf_matmul"
 # kernel name, bytes per launch = the line's TB/s x ms for that leg
 CRC_CONFIGS = {"crc63": (["--crc", "--corrupt", ""], 6, 3, 1 << 20, 1024)}
 CRC_RE = "gf_fused_crc|checksum_chunks512"
-CRC_LEGS = [  # kernel-name test, leg ms key, leg TB/s key (bytes = TB/s x ms)
-    (lambda n, k, m: f"gf_fused_crc<{k}, {m}, " in n and "false" in n, "encode_crc_ms", "encode_crc_hbm_TBps"),
-    (lambda n, k, m: f"gf_fused_crc<{k}, {m}, " in n and "true" in n, "decode_verify_ms", "decode_verify_hbm_TBps"),
-    (lambda n, k, m: "checksum_chunks512" in n, "crc_only_ms", None),
+
+
+def fused_template_args(name):
+    """Template arguments of a gf_fused_crc<K, R, SLABS, SCHEME, KIND, VERIFY,
+    WPE, PAIR> dispatch name, as strings ([] for other kernels).  The legs are
+    told apart by VERIFY (the 6th argument): matching "false" anywhere in the
+    name also caught the decode+verify kernel through its PAIR argument."""
+    i = name.find("gf_fused_crc<")
+    if i < 0:
+        return []
+    j = name.index(">", i)
+    return [t.strip() for t in name[i + len("gf_fused_crc<"):j].split(",")]
+
+
+def is_fused(name, k, m, verify):
+    t = fused_template_args(name)
+    return len(t) >= 6 and t[0] == str(k) and t[1] == str(m) and t[5] == ("true" if verify else "false")
+
+
+def crc_leg_bytes(leg, k, m, cell, stripes, e=None):
+    """Algorithmic HBM bytes of one launch of a checksum leg, the 4-B chunk
+    sums included: encode + CRC reads k cells, writes m parity cells and
+    (k+m) x nchunks sums; decode + verify reads the k survivors and their
+    k x nchunks expected sums and writes the e rebuilt cells (the flags are
+    written only on a mismatch); the CRC pass reads k+m cells, writes the sums."""
+    nck = (cell + 511) // 512
+    e = m if e is None else e
+    if leg == "encode_crc":
+        return ((k + m) * cell + 4 * nck * (k + m)) * stripes
+    if leg == "decode_verify":
+        return ((k + e) * cell + 4 * nck * k) * stripes
+    return ((k + m) * cell + 4 * nck * (k + m)) * stripes
+
+
+CRC_LEGS = [  # kernel-name test, leg ms key, leg name for crc_leg_bytes
+    (lambda n, k, m: is_fused(n, k, m, verify=False), "encode_crc_ms", "encode_crc"),
+    (lambda n, k, m: is_fused(n, k, m, verify=True), "decode_verify_ms", "decode_verify"),
+    (lambda n, k, m: "checksum_chunks512" in n, "crc_only_ms", "crc_only"),
 ]
 
 
@@ -151,11 +185,11 @@ def profile_crc(out, name):
                os.path.join(d, cnt.lower()), "-o", "run", "--output-format", "csv", "--"]
         run(pmc + bench, os.path.join(d, f"bench_{cnt.lower()}.log"), 400)
     trace = [r for r in rows(os.path.join(d, "trace"), "*kernel_trace.csv")]
-    for match, ms_key, tb_key in CRC_LEGS:
+    for match, ms_key, leg in CRC_LEGS:
         mine = sorted((r for r in trace if match(r.get("Kernel_Name", ""), k, m)), key=lambda r: int(r["Dispatch_Id"]))
         if not mine:
             raise SystemExit(f"{name}: no dispatch for {ms_key}")
-        algo = (k + m) * cell * stripes if tb_key is None else round(crc[tb_key] * 1e12 * crc[ms_key] * 1e-3)
+        algo = crc_leg_bytes(leg, k, m, cell, stripes)
 
         def per_dispatch(cnt):  # counter value per dispatch, in dispatch order
             got = {}

@@ -6,6 +6,7 @@
  * scripts/asan_host.sh (tests/test_capi.py).  Device code is not sanitized
  * (no GPU ASan on this pool). */
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 #include "hdfs_ec_amd.h"
 int main(void) {
@@ -34,6 +35,26 @@ int main(void) {
     hec_coder_t* c = 0;
     (void)hec_coder_create(6, 3, 0, &c);
     hec_coder_destroy(c);
-    printf("invert rc=%d bad=%d last_error=%s\n", rc, bad, hec_last_error());
+    /* pool: no device -> a status; release / trim of nothing */
+    if (hec_coder_acquire("rs", 6, 3, -1, &c) == HEC_OK) bad++;
+    hec_coder_release(c);
+    (void)hec_coder_pool_trim();
+    /* the host small-row routine over exact-size heap buffers (every tail
+     * length up to 200 and a 64 KiB + 5 row): no access past the shards */
+    for (size_t n = 1; n < 200 || n == 65541; n = n < 199 ? n + 1 : (n == 199 ? 65541 : 0)) {
+        const uint8_t* in[10];
+        uint8_t* out[4];
+        for (int i = 0; i < 10; i++) {
+            uint8_t* p = (uint8_t*)malloc(n);
+            for (size_t b = 0; b < n; b++) p[b] = (uint8_t)(b * 7 + i);
+            in[i] = p;
+        }
+        for (int j = 0; j < 4; j++) out[j] = (uint8_t*)malloc(n);
+        if (hec_gf_matmul_host(m + 100, 4, 10, in, out, n) != HEC_OK) bad++;
+        for (int i = 0; i < 10; i++) free((void*)in[i]);
+        for (int j = 0; j < 4; j++) free(out[j]);
+        if (n == 65541) break;
+    }
+    printf("invert rc=%d bad=%d host_isa=%s last_error=%s\n", rc, bad, hec_host_isa(), hec_last_error());
     return bad != 0;
 }

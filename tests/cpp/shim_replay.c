@@ -10,11 +10,17 @@
  *                        untouched); HEC_ERR_NOT_ENOUGH_SHARDS -> the shim's
  *                        ErasureCodingError("Not enough valid shards")
  *   encode_rows / decode_rows / GpuGroup -> the batched calls
+ *   Coder::new per row (rust/patches/gf256_mi355x.patch: PooledCoder) ->
+ *                        hec_coder_acquire / hec_coder_release: 10,000
+ *                        acquire / encode / release cycles, timed against
+ *                        create / destroy and against one device-routed call
  * Built by __graft_entry__.build(); run by tests/test_shim_replay.py (GPU). */
+#define _POSIX_C_SOURCE 199309L
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "../../include/hdfs_ec_amd.h"
 
@@ -32,6 +38,12 @@ static int failures = 0;
         }                                                 \
     } while (0)
 
+static double now_us(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec * 1e6 + ts.tv_nsec * 1e-3;
+}
+
 static uint64_t rng = 0x5EEDEC00u;
 static uint8_t next_byte(void) {
     rng ^= rng << 13;
@@ -43,7 +55,7 @@ static uint8_t next_byte(void) {
 enum { K = 6, M = 3 };
 
 int main(void) {
-    CHECK(hec_abi_version() == 3, "ABI %d", hec_abi_version());
+    CHECK(hec_abi_version() == 4, "ABI %d", hec_abi_version());
     hec_coder_t *c = NULL;
     int rc = hec_coder_create_codec("rs", K, M, 0, &c);
     if (rc != HEC_OK) {
@@ -156,6 +168,73 @@ int main(void) {
         CHECK(memcmp(file, rows, R * K * cell) == 0, "group file order");
         free(gpar);
         hec_group_destroy(g);
+    }
+
+    /* Coder::new per row (ec/mod.rs:71, block_writer.rs:787) through the pool:
+     * 10,000 acquire / encode / release cycles of a 4 KiB row (the host
+     * small-row path), each checked against the oracle every 1000th cycle;
+     * then the same cost with create / destroy instead, and one
+     * device-routed call of the same row (host limit 0) for scale */
+    {
+        enum { CYCLES = 10000, SMALL = 4096 };
+        const uint8_t *sin[K];
+        uint8_t *sout[M], *swant[M];
+        for (int i = 0; i < K; i++) sin[i] = data[i];
+        for (int j = 0; j < M; j++) {
+            sout[j] = malloc(SMALL);
+            swant[j] = malloc(SMALL);
+        }
+        orc_encode(K, M, sin, SMALL, swant);
+        hec_coder_t *first = NULL;
+        double t0 = now_us();
+        for (int it = 0; it < CYCLES; it++) {
+            hec_coder_t *pc = NULL;
+            rc = hec_coder_acquire("rs", K, M, 0, &pc);
+            if (rc != HEC_OK) {
+                CHECK(0, "acquire %s", hec_strerror(rc));
+                break;
+            }
+            if (it == 0) first = pc;
+            rc = hec_encode(pc, sin, SMALL, sout);
+            if (rc != HEC_OK || it % 1000 == 0)
+                for (int j = 0; j < M; j++) CHECK(rc == HEC_OK && memcmp(sout[j], swant[j], SMALL) == 0, "pooled encode %d", it);
+            hec_coder_release(pc);
+        }
+        const double pooled_us = (now_us() - t0) / CYCLES;
+        hec_coder_t *again = NULL;
+        CHECK(hec_coder_acquire("rs", K, M, 0, &again) == HEC_OK && again == first, "the pool hands the idle coder back");
+        hec_coder_release(again);
+        t0 = now_us();
+        for (int it = 0; it < CYCLES; it++) {
+            hec_coder_t *pc = NULL;
+            hec_coder_acquire("rs", K, M, 0, &pc);
+            hec_coder_release(pc);
+        }
+        const double cycle_us = (now_us() - t0) / CYCLES;
+        enum { FRESH = 50 };
+        t0 = now_us();
+        for (int it = 0; it < FRESH; it++) {
+            hec_coder_t *fc = NULL;
+            CHECK(hec_coder_create_codec("rs", K, M, 0, &fc) == HEC_OK, "create");
+            hec_encode(fc, sin, SMALL, sout);
+            hec_coder_destroy(fc);
+        }
+        const double fresh_us = (now_us() - t0) / FRESH;
+        hec_coder_set_host_limit(c, 0); /* this row through the device, for scale */
+        hec_encode(c, sin, SMALL, sout);
+        t0 = now_us();
+        for (int it = 0; it < 100; it++) hec_encode(c, sin, SMALL, sout);
+        const double device_us = (now_us() - t0) / 100;
+        for (int j = 0; j < M; j++) CHECK(memcmp(sout[j], swant[j], SMALL) == 0, "device-routed encode");
+        printf("pool: acquire+encode(4 KiB)+release %.2f us/cycle, acquire+release %.3f us, "
+               "create+encode+destroy %.1f us, device-routed encode %.1f us, host isa %s\n",
+               pooled_us, cycle_us, fresh_us, device_us, hec_host_isa());
+        CHECK(pooled_us <= device_us, "a pooled cycle must cost less than one device-routed call");
+        CHECK(hec_coder_pool_trim() >= 1, "trim");
+        for (int j = 0; j < M; j++) {
+            free(sout[j]);
+            free(swant[j]);
+        }
     }
 
     hec_coder_destroy(c);

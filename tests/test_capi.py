@@ -32,7 +32,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version_and_strerror():
-    assert H.lib.hec_abi_version() == 3
+    assert H.lib.hec_abi_version() == 4
     assert "Not enough valid shards" in H.strerror(H.HEC_ERR_NOT_ENOUGH_SHARDS)
     assert H.strerror(H.HEC_ERR_CHECKSUM) == "checksum error"
     assert H.strerror(12345) == "unknown status"
@@ -174,11 +174,74 @@ def test_host_paths_under_address_sanitizer(tmp_path):
     assert "bad=0" in r.stdout
 
 
+def test_product_library_has_no_knobs():
+    # measurement knobs live only in the HEC_EXPERIMENTAL build
+    # (include/hdfs_ec_amd_exp.h); the product library neither declares nor
+    # exports them
+    lib = ctypes.CDLL(H.LIB_PATH)
+    assert not hasattr(lib, "hec_tune_set")
+    assert "hec_tune_set" not in header_functions()
+
+
+@pytest.mark.skipif(not H.experimental_available(), reason="measurement build not built")
 def test_tune_set_validates_without_device():
-    # knobs are host-side atomics: no device needed; removed and
-    # experimental-only keys are rejected by the default library
-    assert H.lib.hec_tune_set(3, 2) == H.HEC_OK
-    assert H.lib.hec_tune_set(3, 0) == H.HEC_OK
-    for key, value in [(5, 3), (5, 4), (5, 5), (6, 3), (13, 1), (15, 2), (16, 1), (16, 3), (11, 2), (11, 6), (11, 9), (3, 99),
-                       (18, 2), (17, 6), (19, 3), (20, 3), (21, 2), (21, 4), (22, 0), (0, 0)]:
-        assert H.lib.hec_tune_set(key, value) == H.HEC_ERR_INVALID_ARG, (key, value)
+    # knobs are host-side atomics of the measurement build: no device needed
+    xlib = H.experimental_lib()
+    assert xlib.hec_tune_set(3, 2) == H.HEC_OK
+    assert xlib.hec_tune_set(3, 0) == H.HEC_OK
+    for key, value in [(6, 3), (16, 1), (3, 99), (18, 2), (17, 6), (19, 3), (20, 3), (21, 4), (22, 0), (0, 0)]:
+        assert xlib.hec_tune_set(key, value) == H.HEC_ERR_INVALID_ARG, (key, value)
+
+
+# ---- the host small-row path (hec_gf_matmul_host) on the CPU ---------------
+# rust/tests/test_ec.rs:77-87 sizes_to_test: 16 B, cell +- 4, 5 rows +- 4 (a
+# 64 KiB cell keeps it quick; the GPU suite runs the 1 MiB cells)
+
+def _sizes_to_test(k, cell):
+    return [16, cell - 4, cell, cell + 4, 5 * k * cell - 4, 5 * k * cell, 5 * k * cell + 4]
+
+
+@pytest.mark.parametrize("k,m", [(3, 2), (6, 3), (10, 4)])
+def test_gf_matmul_host_vs_oracle_reference_sizes(k, m):
+    import numpy as np
+    from hdfs_native_ec.synth import splitmix64_bytes
+    enc = O.gen_rs_matrix(k, m)
+    for total in _sizes_to_test(k, 65536):
+        # the writer's row split of a file of `total` bytes: the last row's
+        # cells zero-padded to buffers[0].len() (block_writer.rs:817-851)
+        n = min(65536, total)
+        data = [splitmix64_bytes(total * 10 + i, n) for i in range(k)]
+        got = H.gf_matmul_host(enc[k:], data)
+        want = O.c_encode(O.load_c_oracle(), k, m, data)
+        assert all(g == w.tobytes() for g, w in zip(got, want)), (k, m, total)
+        # decode matrix of the worst case (data 0..m-1 lost)
+        surv, miss, dm = O.decode_plan(k, m, [i >= m for i in range(k + m)])
+        shards = data + [np.frombuffer(g, dtype=np.uint8) for g in got]
+        rec = H.gf_matmul_host(dm, [shards[i] for i in surv])
+        for r, i in enumerate(miss):
+            assert rec[r] == data[i].tobytes()
+
+
+def test_gf_matmul_host_args():
+    buf = (ctypes.c_uint8 * 4)()
+    ptrs = (ctypes.c_void_p * 2)()
+    assert H.lib.hec_gf_matmul_host(None, 1, 1, ptrs, ptrs, 16) == H.HEC_ERR_INVALID_ARG
+    assert H.lib.hec_gf_matmul_host(buf, 1, 33, ptrs, ptrs, 16) == H.HEC_ERR_INVALID_ARG
+    assert H.lib.hec_gf_matmul_host(buf, 1, 1, ptrs, ptrs, 0) == H.HEC_ERR_INVALID_ARG
+    assert H.lib.hec_gf_matmul_host(buf, 1, 1, ptrs, ptrs, 16) == H.HEC_ERR_INVALID_ARG  # null shard pointers
+    assert H.host_isa() in ("avx512bw+gfni", "avx2", "scalar")
+
+
+def test_coder_pool_args_need_no_device():
+    h = ctypes.c_void_p()
+    assert H.lib.hec_coder_acquire(b"rs", 6, 3, 0, None) == H.HEC_ERR_INVALID_ARG
+    assert H.lib.hec_coder_acquire(b"rs", 6, 3, -2, ctypes.byref(h)) == H.HEC_ERR_INVALID_ARG
+    assert H.lib.hec_coder_acquire(b"lrc", 6, 3, 0, ctypes.byref(h)) in (H.HEC_ERR_UNSUPPORTED_CODEC,
+                                                                         H.HEC_ERR_DEVICE)
+    assert not h.value
+    H.lib.hec_coder_release(None)
+    assert H.lib.hec_coder_set_host_limit(None, 5) == H.HEC_ERR_INVALID_ARG
+    assert H.lib.hec_coder_host_limit(None) == 0
+    if not gpu_available():
+        assert H.lib.hec_coder_acquire(b"rs", 6, 3, -1, ctypes.byref(h)) == H.HEC_ERR_DEVICE
+        assert H.pool_trim() == 0

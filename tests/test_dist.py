@@ -1,6 +1,9 @@
-"""Multi-rank path on CPU: world_size-2 gloo process groups exercising the
-stripe sharding and max-over-ranks timing used by bench.py (the data path
-itself has no collective; each rank codes its own stripe range)."""
+"""Multi-rank path: world_size-2 gloo process groups exercising the stripe
+sharding and max-over-ranks timing used by bench.py (the data path itself
+has no collective; each rank codes its own stripe range).  On the CPU every
+rank codes its share with the ENGINE's host routine (hec_gf_matmul_host);
+the GPU variant runs the device engine on both ranks (one card, two
+processes); both are checked against the oracle."""
 import hashlib
 import json
 import os
@@ -41,19 +44,30 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, total, k, m, cell, out_path, root):
+def _worker(rank, world, port, total, k, m, cell, out_path, root, device=False):
     sys.path[:0] = [os.path.join(root, "hdfs-native_amd"), os.path.join(root, "oracle")]
-    import ec_oracle as O
+    import hdfs_native_ec as H
     from hdfs_native_ec.dist import max_over_ranks, shard_range, sum_over_ranks
     from hdfs_native_ec.synth import batch_data
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
-        lib = O.load_c_oracle()
         first, count = shard_range(total, world, rank)
         data = batch_data(count, k, cell, first=first)
         digests = []
-        for s in range(count):
-            par = O.c_encode(lib, k, m, list(data[s]))
+        if device:  # the device engine on this rank's share (ranks share card 0)
+            coder = H.Coder(k, m, 0)
+            d = torch.from_numpy(data).to("cuda:0")
+            p = torch.empty((count, m, cell), dtype=torch.uint8, device="cuda:0")
+            if count:
+                H.encode_batch(coder, d, p)
+            torch.cuda.synchronize()
+            pars = [list(p[s].cpu().numpy()) for s in range(count)]
+            coder.close()
+        else:  # the engine's host routine, no device
+            enc = H.gen_rs_matrix(k, m)[k:]
+            pars = [[np.frombuffer(x, dtype=np.uint8) for x in H.gf_matmul_host(enc, list(data[s]))]
+                    for s in range(count)]
+        for par in pars:
             digests.append(hashlib.sha256(b"".join(p.tobytes() for p in par)).hexdigest())
         gathered = [None] * world
         dist.all_gather_object(gathered, (first, digests))
@@ -68,13 +82,14 @@ def _worker(rank, world, port, total, k, m, cell, out_path, root):
 
 
 @pytest.mark.parametrize("world", [2])
-def test_gloo_sharded_encode_matches_single_process(tmp_path, world):
+@pytest.mark.parametrize("device", [False, pytest.param(True, marks=pytest.mark.gpu)])
+def test_gloo_sharded_encode_matches_single_process(tmp_path, world, device):
     import ec_oracle as O
     from hdfs_native_ec.synth import batch_data
     from conftest import ROOT
     total, k, m, cell = 7, 6, 3, 4096
     out = tmp_path / "res.json"
-    mp.spawn(_worker, args=(world, _free_port(), total, k, m, cell, str(out), ROOT), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), total, k, m, cell, str(out), ROOT, device), nprocs=world, join=True)
     res = json.loads(out.read_text())
     assert res["tmax"] == float(world)
     assert res["bytes"] == float(total * k * cell)
@@ -112,3 +127,12 @@ def test_bench_gpus_flag_spawns_ranks(args, want_S, want_global, scaling):
     assert d["config"]["global_stripes"] == want_global
     assert d["config"]["stripes_summed_over_ranks"] == want_global
     assert d["config"]["stripes_per_gpu"] == want_S  # rank 0's share
+    # the other multi-GPU BASELINE configs are timed by the same invocation,
+    # each split over the ranks (bench.py --extra-configs)
+    ex = d["extra_configs"]
+    assert set(ex) == {"rs104_1MiB_x2048", "rs63_64KiB_x65536"}
+    assert ex["rs104_1MiB_x2048"]["stripes_per_gpu_rank0"] == 1024
+    assert ex["rs104_1MiB_x2048"]["stripes_summed_over_ranks"] == 2048
+    assert ex["rs63_64KiB_x65536"]["stripes_per_gpu_rank0"] == 32768
+    assert ex["rs63_64KiB_x65536"]["stripes_summed_over_ranks"] == 65536
+    assert all(v["scaling"] == "strong" and v["value_GiBps"] is None for v in ex.values())

@@ -1,16 +1,26 @@
-"""Parity of the measured-and-rejected kernel variants, which exist only in
-the HEC_EXPERIMENTAL build (hdfs-native_amd/lib/libhdfs_ec_amd_exp.so, `make
-exp`; ec_experimental.hip and the #ifdef'd CRC schemes).  Same oracle and
-same bit-exact bar as the default library; every coder here is bound to the
-experimental library and its knobs are that library's own."""
+"""Parity of every knob-selected shape and of the measured-and-rejected
+kernel variants, which exist only in the HEC_EXPERIMENTAL measurement build
+(hdfs-native_amd/lib/libhdfs_ec_amd_exp.so, `make -C hdfs-native_amd exp`;
+ec_experimental.hip and the #ifdef'd shapes and CRC schemes; knobs in
+include/hdfs_ec_amd_exp.h).  Same oracle and same bit-exact bar as the
+product library; every coder here is bound to the measurement build and its
+knobs are that library's own.  The product library has no knobs: its
+default paths are covered by tests/test_gpu_parity.py, whose test bodies are
+reused here with knobs set.  Skipped when the measurement build is absent
+(it is not built or shipped by default)."""
+import threading
+
 import numpy as np
 import pytest
 
 import ec_oracle as O
 import hdfs_native_ec as H
+import test_gpu_parity as P
 from hdfs_native_ec.synth import batch_data
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif(not H.experimental_available(),
+                                 reason="measurement build not built (make -C hdfs-native_amd exp)")]
 
 torch = pytest.importorskip("torch")
 
@@ -198,3 +208,168 @@ def test_fused_variants_verify_vs_oracle(xlib, dev, c_oracle, ctype, k, m, cell,
     assert np.array_equal(b, want_bad)
     assert np.array_equal(o[:, 0], data[:, 0])
     assert np.array_equal(o[1, 2], data[1, 2])
+
+
+# ---- knob-selected shapes of the product kernels -------------------------
+
+@pytest.mark.parametrize("knob", [((1, 1),), ((1, 2),), ((1, 4),), ((2, 0),), ((3, 2),), ((4, 512), (1, 1)),
+                                  ((4, 512), (1, 2)), ((1, 4), (2, 0), (3, 3)), ((5, 2),), ((5, 2), (1, 2)),
+                                  ((5, 2), (4, 512)), ((5, 2), (3, 2)), ((5, 1),), ((6, 1),), ((6, 2),),
+                                  ((6, 2), (4, 512)), ((7, 100),), ((7, 3),), ((8, 2),), ((8, 3),), ((8, 4), (5, 2)),
+                                  ((8, 64),), ((7, 16),), ((7, 12),)])
+def test_tuning_variants_bit_identical(xlib, dev, c_oracle, knob):
+    run_variant(xlib, c_oracle, dev, 6, 3, 5, 8192 + 16, list(knob), 21)
+
+
+@pytest.mark.parametrize("knob", [((1, 8),), ((1, 8), (3, 2)), ((1, 8), (7, 5))])
+@pytest.mark.parametrize("k,m", [(2, 1), (3, 2)])
+@pytest.mark.parametrize("cell", [8192 + 16, 3 * 65536 + 48, (1 << 20) + 16])
+def test_eight_chunks_per_lane_small_k(xlib, dev, c_oracle, knob, k, m, cell):
+    # 8 x 16-B chunks per lane (k <= 3): full and partial tiles, small grids
+    run_variant(xlib, c_oracle, dev, k, m, 3, cell, list(knob) + [(5, 1)], cell + k)
+
+
+@pytest.mark.parametrize("pipeline", [1, 2])
+@pytest.mark.parametrize("k,m", [(2, 1), (3, 2), (6, 3), (10, 4)])
+@pytest.mark.parametrize("cell", [4096, 4096 + 16, 3 * 65536 + 48])
+@pytest.mark.parametrize("S", [3, 6])
+def test_pipelines_forced_vs_oracle(xlib, dev, c_oracle, pipeline, k, m, cell, S):
+    # tune key 5: the register (1) or LDS-DMA (2) kernel whatever the cell size
+    with P.knobs([(5, pipeline)], xlib):
+        P.pipelines_body(dev, c_oracle, k, m, cell, S, P.coder(k, m, xlib))
+
+
+def test_tune_set_concurrent_with_launches(xlib, dev, c_oracle):
+    # hec_tune_set while other threads launch: the knobs are atomics read once
+    # per launch, and every value toggled here is result-neutral
+    k, m, S, cell = 6, 3, 4, 65536 + 16
+    data = batch_data(S, k, cell, first=5)
+    want = oracle_batch_encode(c_oracle, k, m, data)
+    stop = threading.Event()
+    errors = []
+
+    def toggler():
+        i = 0
+        while not stop.is_set():
+            H.tune_set(3, 1 + i % 2, xlib)
+            H.tune_set(8, 1 + 3 * (i % 2), xlib)
+            H.tune_set(7, (i % 3) * 64, xlib)
+            i += 1
+
+    def launcher(seed):
+        try:
+            cod = H.Coder(k, m, 0, lib=xlib)
+            st = torch.cuda.Stream(dev)
+            d = torch.from_numpy(data).to(dev)
+            for _ in range(40):
+                p = torch.zeros((S, m, cell), dtype=torch.uint8, device=dev)
+                with torch.cuda.stream(st):
+                    H.encode_batch(cod, d, p, st)
+                st.synchronize()
+                if not np.array_equal(p.cpu().numpy(), want):
+                    errors.append(seed)
+            cod.close()
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(repr(e))
+
+    t = threading.Thread(target=toggler)
+    ls = [threading.Thread(target=launcher, args=(i,)) for i in range(4)]
+    t.start()
+    for th in ls:
+        th.start()
+    for th in ls:
+        th.join()
+    stop.set()
+    t.join()
+    for key in (3, 7, 8):
+        H.tune_set(key, 0, xlib)
+    assert not errors, errors
+
+
+def test_tune_set_rejects_unknown_values(xlib):
+    for key, value in [(3, 99), (1, 5), (5, 6), (11, 8), (16, 1), (17, 6), (19, 3), (20, 3), (21, 4), (22, 0), (0, 0)]:
+        with pytest.raises(ValueError):
+            H.tune_set(key, value, xlib)
+
+
+@pytest.mark.parametrize("case", P.UNALIGNED_CASES)
+def test_unaligned_byte_kernel_alone(xlib, dev, c_oracle, case):
+    # tune key 18 = 1: unaligned layouts through the byte kernel alone
+    with P.knobs([(18, 1)], xlib):
+        P.unaligned_layouts_body(dev, c_oracle, *case, P.coder(case[0], case[1], xlib))
+
+
+@pytest.mark.parametrize("k,m,cell", [(6, 3, 4096), (10, 4, 8192), (3, 2, 4096 + 16), (4, 2, 4096)])
+@pytest.mark.parametrize("skip", [1, 2])
+def test_mixed_row_policies(xlib, dev, c_oracle, k, m, cell, skip):
+    # tune key 20: rows past a stripe's erasure count computed (1) or skipped (2)
+    P.mixed_patterns_body(dev, c_oracle, k, m, cell, P.coder(k, m, xlib), [(20, skip)], xlib)
+
+
+def test_mixed_many_plans_skipped_rows(xlib, dev):
+    P.mixed_many_plans_body(dev, P.coder(10, 4, xlib), [(20, 2)], xlib)
+
+
+@pytest.mark.parametrize("cell,bpc,n", P.CRC32C_CASES)
+@pytest.mark.parametrize("variant,pf", [(0, 2), (1, 1), (1, 2), (5, 0), (5, 1), (5, 2), (7, 1)])
+def test_crc32c_lookup_schemes(xlib, dev, cell, bpc, n, variant, pf):
+    # tune key 11: slicing-by-8 (1), 11-bit slicing (5), the fold (0 / 7); key 12: prefetch
+    P.crc32c_body(dev, cell, bpc, n, P.coder(6, 3, xlib), [(11, variant), (12, pf)], xlib)
+
+
+@pytest.mark.parametrize("ctype", P.CKSUM_TYPES)
+@pytest.mark.parametrize("cell,bpc,n", P.CHECKSUM_CASES)
+@pytest.mark.parametrize("variant", [1, 5])
+def test_checksum_lookup_schemes(xlib, dev, ctype, cell, bpc, n, variant):
+    P.checksum_body(dev, ctype, cell, bpc, n, P.coder(6, 3, xlib), [(11, variant)], xlib)
+
+
+@pytest.mark.parametrize("case", P.ENCODE_CRC_CASES)
+@pytest.mark.parametrize("fused,scheme", [(4, 0), (8, 0), (None, 0), (0, 1), (0, 5), (4, 5), (8, 1)])
+def test_encode_crc_knobs(xlib, dev, c_oracle, case, fused, scheme):
+    # key 9 = 1: two passes; key 10: slabs per wave; key 11: lookup scheme
+    pairs = [(9, 1 if fused is None else 0), (10, fused or 0), (11, scheme)]
+    P.encode_crc_body(dev, c_oracle, *case, xlib, pairs)
+
+
+@pytest.mark.parametrize("k,m,cell,S,slabs", [(10, 4, 1 << 15, 3, 0), (3, 2, 8192 + 512, 4, 4), (6, 3, 1 << 14, 2, 4)])
+@pytest.mark.parametrize("pair", [1, 2])
+def test_fused_input_pairing(xlib, dev, c_oracle, k, m, cell, S, slabs, pair):
+    """Fused encode + CRC32C and decode + verify at 4 slabs per wave with the
+    inputs two at a time (tune key 19 = 2, the default) and one at a time (1),
+    an odd k included, against the oracle."""
+    bpc = 512
+    data = batch_data(S, k, cell, first=57 + cell + pair)
+    par = oracle_batch_encode(c_oracle, k, m, data)
+    d = torch.from_numpy(data).to(dev)
+    p = torch.zeros((S, m, cell), dtype=torch.uint8, device=dev)
+    nch = cell // bpc
+    sums = torch.zeros((S, k + m, nch, 4), dtype=torch.uint8, device=dev)
+    dp, ds = H.stripe_layout_ptrs(d, k)
+    pp, ps = H.stripe_layout_ptrs(p, m)
+    sp = torch.cuda.current_stream().cuda_stream
+    cod = P.coder(k, m, xlib)
+    with P.knobs([(19, pair), (10, slabs)], xlib):
+        cod.encode_crc_device(dp, ds, pp, ps, cell, S, bpc, sums.data_ptr(), sp)
+        torch.cuda.synchronize()
+        assert np.array_equal(p.cpu().numpy(), par)
+        want = _oracle_sums(np.concatenate([data, par], axis=1), bpc)
+        assert np.array_equal(sums.cpu().numpy(), want)
+        out = torch.zeros_like(d)
+        bad = torch.zeros((S, k + m), dtype=torch.uint8, device=dev)
+        op, os_ = H.stripe_layout_ptrs(out, k)
+        miss = list(range(min(m, k)))
+        cod.decode_verify_device(H.CHECKSUM_CRC32C, [None if i in miss else dp[i] for i in range(k)] + pp, ds + ps,
+                                 op, os_, cell, S, bpc, sums.data_ptr(), bad.data_ptr(), sp)
+        torch.cuda.synchronize()
+    assert not bad.cpu().numpy().any()
+    o = out.cpu().numpy()
+    for i in miss:
+        assert np.array_equal(o[:, i], data[:, i])
+
+
+@pytest.mark.parametrize("ctype", P.CKSUM_TYPES)
+@pytest.mark.parametrize("case", P.VERIFY_CASES)
+@pytest.mark.parametrize("scheme", [1, 5])
+def test_decode_verify_lookup_schemes(xlib, dev, c_oracle, ctype, case, scheme):
+    P.decode_verify_body(dev, c_oracle, ctype, *case, P.coder(case[0], case[1], xlib), [(11, scheme)], xlib)

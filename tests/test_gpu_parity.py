@@ -4,6 +4,7 @@ and the committed golden vectors, bit-exact.  Full-size configs
 encode -> erase -> decode round trips, linearity, sampled-stripe oracle
 checks.  Edge cases follow the reference tests (rust/tests/test_ec.rs:77-87
 sizes 16 B .. +-4 B around cell boundaries; 0..m failures; m+1 fails)."""
+import contextlib
 import itertools
 
 import numpy as np
@@ -27,10 +28,27 @@ def dev():
 _coders = {}
 
 
-def coder(k, m):
-    if (k, m) not in _coders:
-        _coders[(k, m)] = H.Coder(k, m, 0)
-    return _coders[(k, m)]
+def coder(k, m, lib=None):
+    """A cached coder on the product library (lib=None) or on another build
+    (tests/test_gpu_experimental.py passes the measurement build)."""
+    key = (k, m, id(lib))
+    if key not in _coders:
+        _coders[key] = H.Coder(k, m, 0, lib=lib)
+    return _coders[key]
+
+
+@contextlib.contextmanager
+def knobs(pairs, xlib=None):
+    """hec_tune_set pairs on the measurement build for the duration of a
+    block (the product library has no knobs: pairs must be empty there)."""
+    assert not pairs or xlib is not None, "knobs exist only in the measurement build"
+    try:
+        for key, val in pairs:
+            H.tune_set(key, val, xlib)
+        yield
+    finally:
+        for key, _ in pairs:
+            H.tune_set(key, -1 if key == 2 else 0, xlib)
 
 
 def oracle_batch_encode(c_oracle, k, m, data: np.ndarray) -> np.ndarray:
@@ -201,12 +219,22 @@ def test_device_unaligned_layout(dev, c_oracle):
     (6, 3, 3, 1000, 1, 3, 0, False), (6, 3, 2, 4096 + 7, 5, 0, 12, False), (6, 3, 2, 65536 + 5, 0, 2, 4, False),
     (10, 4, 2, 8192 + 5, 3, 1, 0, True), (3, 2, 4, 4096, 2, 6, 2, True), (3, 2, 3, 7, 1, 1, 0, False),
     (2, 1, 3, 24, 7, 5, 1, True)])
-@pytest.mark.parametrize("byte_only", [False, True])
-def test_device_unaligned_layouts(dev, c_oracle, k, m, S, cell, in_off, out_off, pitch_extra, per_shard, byte_only):
+def test_device_unaligned_layouts(dev, c_oracle, k, m, S, cell, in_off, out_off, pitch_extra, per_shard):
     """Bases and strides off the 16-B grid: the dword-realigning kernel (8 B
     per lane, aligned dword loads + v_alignbyte, dword / short / byte stores
-    by output alignment) plus the byte tail, or the byte kernel alone (tune
-    key 18 = 1); encode and a decode with m data shards missing vs the oracle."""
+    by output alignment) plus the byte tail; encode and a decode with m data
+    shards missing vs the oracle (the measurement build also runs the byte
+    kernel alone, tests/test_gpu_experimental.py)."""
+    unaligned_layouts_body(dev, c_oracle, k, m, S, cell, in_off, out_off, pitch_extra, per_shard, coder(k, m))
+
+
+UNALIGNED_CASES = [
+    (6, 3, 3, 1000, 1, 3, 0, False), (6, 3, 2, 4096 + 7, 5, 0, 12, False), (6, 3, 2, 65536 + 5, 0, 2, 4, False),
+    (10, 4, 2, 8192 + 5, 3, 1, 0, True), (3, 2, 4, 4096, 2, 6, 2, True), (3, 2, 3, 7, 1, 1, 0, False),
+    (2, 1, 3, 24, 7, 5, 1, True)]
+
+
+def unaligned_layouts_body(dev, c_oracle, k, m, S, cell, in_off, out_off, pitch_extra, per_shard, cod):
     data = batch_data(S, k, cell, first=13 + cell + in_off)
     want = oracle_batch_encode(c_oracle, k, m, data)
     pitch = cell + pitch_extra
@@ -224,9 +252,7 @@ def test_device_unaligned_layouts(dev, c_oracle, k, m, S, cell, in_off, out_off,
     pbuf = torch.zeros(S * m * pitch + out_off + 16, dtype=torch.uint8, device=dev)
     op = [pbuf.data_ptr() + out_off + j * pitch for j in range(m)]
     sp = torch.cuda.current_stream().cuda_stream
-    cod = coder(k, m)
-    H.tune_set(18, 1 if byte_only else 0)
-    try:
+    if True:
         cod.encode_device(ip, [in_stride] * k, op, [m * pitch] * m, cell, S, sp)
         torch.cuda.synchronize()
         hp = pbuf.cpu().numpy()
@@ -243,8 +269,6 @@ def test_device_unaligned_layouts(dev, c_oracle, k, m, S, cell, in_off, out_off,
         for s_ in range(S):
             for i in miss:
                 assert np.array_equal(hr[out_off + (s_ * k + i) * pitch:][:cell], data[s_, i]), (s_, i)
-    finally:
-        H.tune_set(18, 0)
 
 
 def test_gf_matmul_device_arbitrary_matrix(dev):
@@ -266,114 +290,28 @@ def test_gf_matmul_device_arbitrary_matrix(dev):
             assert np.array_equal(o[s, j], want[j])
 
 
-@pytest.mark.parametrize("knob", [((1, 1),), ((1, 2),), ((1, 4),), ((2, 0),), ((3, 2),), ((4, 512), (1, 1)),
-                                  ((4, 512), (1, 2)), ((1, 4), (2, 0), (3, 3)), ((5, 2),), ((5, 2), (1, 2)),
-                                  ((5, 2), (4, 512)), ((5, 2), (3, 2)), ((5, 1),), ((6, 1),), ((6, 2),), ((6, 2), (4, 512)), ((7, 100),), ((7, 3),), ((8, 2),),
-                                  ((8, 3),), ((8, 4), (5, 2)), ((8, 64),), ((7, 16),), ((7, 12),)])
-def test_tuning_variants_bit_identical(dev, c_oracle, knob):
-    k, m, S, cell = 6, 3, 5, 8192 + 16
-    data = batch_data(S, k, cell, first=21)
-    want = oracle_batch_encode(c_oracle, k, m, data)
-    d = torch.from_numpy(data).to(dev)
-    p = torch.zeros((S, m, cell), dtype=torch.uint8, device=dev)
-    try:
-        for kv in knob:
-            H.tune_set(*kv)
-        H.encode_batch(coder(k, m), d, p)
-        out = torch.zeros_like(d)
-        H.decode_batch(coder(k, m), d, p, [0, 2, 4], out)
-        torch.cuda.synchronize()
-    finally:
-        H.tune_set(1, 0)
-        H.tune_set(2, -1)
-        H.tune_set(3, 0)
-        H.tune_set(4, 0)
-        H.tune_set(5, 0)
-        H.tune_set(6, 0)
-        H.tune_set(7, 0)
-        H.tune_set(8, 0)
-    assert np.array_equal(p.cpu().numpy(), want)
-    for i in (0, 2, 4):
-        assert torch.equal(out[:, i], d[:, i])
-
-
-@pytest.mark.parametrize("pipeline", [1, 2])
 @pytest.mark.parametrize("k,m", [(2, 1), (3, 2), (6, 3), (10, 4)])
-@pytest.mark.parametrize("cell", [4096, 4096 + 16, 3 * 65536 + 48])
-@pytest.mark.parametrize("S", [3, 6])
-def test_pipelines_vs_oracle(dev, c_oracle, pipeline, k, m, cell, S):
-    # register kernel and LDS-DMA kernel, full and partial tiles; S = 3 and 6
-    # stripes: tile-order groups of 3 and of 2 (groups divide the batch)
+@pytest.mark.parametrize("cell", [4096, 4096 + 16, 3 * 65536 + 48, (1 << 18) + 48, 5 * 65536 + 16])
+@pytest.mark.parametrize("S", [3, 6, 7])
+def test_pipelines_vs_oracle(dev, c_oracle, k, m, cell, S):
+    """The default kernels by cell size: the LDS-DMA kernel (cells <= 256 KiB,
+    k in {2, 3, 6}) and the register kernel (larger cells, and k = 10), full
+    and partial tiles; S = 3, 6 and 7 stripes: tile-order groups of 3 and 2,
+    and 7 = a group of 4 plus a stripe-major remainder of 3."""
+    pipelines_body(dev, c_oracle, k, m, cell, S, coder(k, m))
+
+
+def pipelines_body(dev, c_oracle, k, m, cell, S, cod):
     data = batch_data(S, k, cell, first=cell + k)
     want = oracle_batch_encode(c_oracle, k, m, data)
     d = torch.from_numpy(data).to(dev)
     p = torch.zeros((S, m, cell), dtype=torch.uint8, device=dev)
-    try:
-        H.tune_set(5, pipeline)
-        H.encode_batch(coder(k, m), d, p)
-        out = torch.zeros_like(d)
-        H.decode_batch(coder(k, m), d, p, list(range(m)), out)
-        torch.cuda.synchronize()
-    finally:
-        H.tune_set(5, 0)
+    H.encode_batch(cod, d, p)
+    out = torch.zeros_like(d)
+    H.decode_batch(cod, d, p, list(range(m)), out)
+    torch.cuda.synchronize()
     assert np.array_equal(p.cpu().numpy(), want)
     assert torch.equal(out[:, :m], d[:, :m])
-
-
-def test_tune_set_concurrent_with_launches(dev, c_oracle):
-    # hec_tune_set while other threads launch: the knobs are atomics read once
-    # per launch, and every value toggled here is result-neutral
-    import threading
-    k, m, S, cell = 6, 3, 4, 65536 + 16
-    data = batch_data(S, k, cell, first=5)
-    want = oracle_batch_encode(c_oracle, k, m, data)
-    stop = threading.Event()
-    errors = []
-
-    def toggler():
-        i = 0
-        while not stop.is_set():
-            H.tune_set(3, 1 + i % 2)
-            H.tune_set(8, 1 + 3 * (i % 2))
-            H.tune_set(7, (i % 3) * 64)
-            i += 1
-
-    def launcher(seed):
-        try:
-            cod = H.Coder(k, m, 0)
-            st = torch.cuda.Stream(dev)
-            d = torch.from_numpy(data).to(dev)
-            for _ in range(40):
-                p = torch.zeros((S, m, cell), dtype=torch.uint8, device=dev)
-                with torch.cuda.stream(st):
-                    H.encode_batch(cod, d, p, st)
-                st.synchronize()
-                if not np.array_equal(p.cpu().numpy(), want):
-                    errors.append(seed)
-            cod.close()
-        except Exception as e:  # pragma: no cover - reported below
-            errors.append(repr(e))
-
-    t = threading.Thread(target=toggler)
-    ls = [threading.Thread(target=launcher, args=(i,)) for i in range(4)]
-    t.start()
-    for th in ls:
-        th.start()
-    for th in ls:
-        th.join()
-    stop.set()
-    t.join()
-    for key in (3, 7, 8):
-        H.tune_set(key, 0)
-    assert not errors, errors
-
-
-def test_experimental_keys_rejected_by_default_library():
-    # the rejected variants exist only in lib/libhdfs_ec_amd_exp.so
-    for key, value in [(5, 3), (5, 4), (5, 5), (13, 1), (15, 2), (11, 2), (11, 6), (11, 9), (6, 3), (16, 1), (16, 3),
-                       (18, 2), (17, 6), (19, 3), (20, 3)]:
-        with pytest.raises(ValueError):
-            H.tune_set(key, value)
 
 
 @pytest.mark.parametrize("S,chunk,cell", [(9, 4, 65536), (23, 2, 65536), (7, 7, 4096 + 16), (5, 1, 1000)])
@@ -457,10 +395,14 @@ def _random_masks(k, m, S, seed, allow_fail=False):
 
 @pytest.mark.parametrize("k,m,cell", [(6, 3, 4096), (6, 3, 65536 + 64), (10, 4, 8192), (3, 2, 4096 + 16),
                                       (2, 1, 1024), (4, 2, 4096), (6, 3, 1000)])
-@pytest.mark.parametrize("skip", [0, 1, 2])
-def test_device_decode_mixed_patterns(dev, c_oracle, k, m, cell, skip):
-    """Random per-stripe patterns; tune key 20: rows past a stripe's erasure
-    count skipped (2), computed and dropped (1), or the per-k default (0)."""
+def test_device_decode_mixed_patterns(dev, c_oracle, k, m, cell):
+    """Random per-stripe patterns (rows past a stripe's erasure count skipped
+    for k <= 6, computed and dropped above; the measurement build forces
+    either, tests/test_gpu_experimental.py)."""
+    mixed_patterns_body(dev, c_oracle, k, m, cell, coder(k, m))
+
+
+def mixed_patterns_body(dev, c_oracle, k, m, cell, cod, knob_pairs=(), xlib=None):
     S = 40
     data = batch_data(S, k, cell, first=900 + k)
     par = oracle_batch_encode(c_oracle, k, m, data)
@@ -476,12 +418,9 @@ def test_device_decode_mixed_patterns(dev, c_oracle, k, m, cell, skip):
             if not (mask >> i) & 1:
                 (d[s, i] if i < k else p[s, i - k]).fill_(0xEE)
     out = torch.full_like(d, 0x5A)
-    H.tune_set(20, skip)
-    try:
-        H.decode_batch_mixed(coder(k, m), d, p, masks, out)
+    with knobs(knob_pairs, xlib):
+        H.decode_batch_mixed(cod, d, p, masks, out)
         torch.cuda.synchronize()
-    finally:
-        H.tune_set(20, 0)
     o = out.cpu().numpy()
     for s, mask in enumerate(masks):
         for i in range(k):
@@ -491,17 +430,20 @@ def test_device_decode_mixed_patterns(dev, c_oracle, k, m, cell, skip):
                 assert np.array_equal(o[s, i], data[s, i]), (s, i, bin(mask))
 
 
-@pytest.mark.parametrize("skip", [0, 2])
-def test_device_decode_mixed_many_plans(dev, skip):
+def test_device_decode_mixed_many_plans(dev):
     """RS(10,4), 512 stripes with random 1..4 erased shards: a few hundred
     distinct plans, more than the kernel keeps resident in LDS (the per-stripe
-    restaging path), rows past a stripe's e computed (0) or skipped (2)."""
+    restaging path)."""
+    mixed_many_plans_body(dev, coder(10, 4))
+
+
+def mixed_many_plans_body(dev, cod, knob_pairs=(), xlib=None):
     k, m, S, cell = 10, 4, 512, 4096
     rng = np.random.default_rng(1234)
     data = rng.integers(0, 256, size=(S, k, cell), dtype=np.uint8)
     d = torch.from_numpy(data).to(dev)
     p = torch.empty((S, m, cell), dtype=torch.uint8, device=dev)
-    H.encode_batch(coder(k, m), d, p)
+    H.encode_batch(cod, d, p)
     full = (1 << (k + m)) - 1
     masks = []
     for s in range(S):
@@ -514,12 +456,9 @@ def test_device_decode_mixed_many_plans(dev, skip):
             if not (mask >> i) & 1:
                 (dm[s, i] if i < k else pm[s, i - k]).fill_(0xEE)
     out = torch.full_like(d, 0x5A)
-    H.tune_set(20, skip)
-    try:
-        H.decode_batch_mixed(coder(k, m), dm, pm, masks, out)
+    with knobs(knob_pairs, xlib):
+        H.decode_batch_mixed(cod, dm, pm, masks, out)
         torch.cuda.synchronize()
-    finally:
-        H.tune_set(20, 0)
     for s, mask in enumerate(masks):
         for i in range(k):
             if (mask >> i) & 1:
@@ -701,22 +640,24 @@ def _oracle_sums(cells: np.ndarray, bpc: int) -> np.ndarray:
     return out
 
 
-@pytest.mark.parametrize("cell,bpc,n", [(512 * 64, 512, 3), (512 * 70 + 256, 512, 2), (1 << 16, 512, 9),
-                                        (4096, 4096, 2), (1000, 512, 3), (3 * 512 + 16, 512, 1), (2048, 100, 2)])
-@pytest.mark.parametrize("variant,pf", [(0, 0), (0, 1), (0, 2), (1, 1), (1, 2), (5, 0), (5, 1), (5, 2), (7, 1)])
-def test_crc32c_device_vs_oracle(dev, cell, bpc, n, variant, pf):
-    """The default library's CRC lookup schemes (tune key 11: 11-bit slicing,
-    slicing-by-8; 0 / 7 = the fold + 11-bit tail, 5 = 11-bit slicing) and prefetch depths (key 12) against the oracle."""
+CRC32C_CASES = [(512 * 64, 512, 3), (512 * 70 + 256, 512, 2), (1 << 16, 512, 9), (4096, 4096, 2), (1000, 512, 3),
+                (3 * 512 + 16, 512, 1), (2048, 100, 2)]
+
+
+@pytest.mark.parametrize("cell,bpc,n", CRC32C_CASES)
+def test_crc32c_device_vs_oracle(dev, cell, bpc, n):
+    """The default CRC32C kernel (each 128-B quarter folded by a sparse
+    multiple of the polynomial, 11-bit slicing of the tail) and the generic
+    byte kernel (other chunk sizes, unaligned cells) against the oracle."""
+    crc32c_body(dev, cell, bpc, n, coder(6, 3))
+
+
+def crc32c_body(dev, cell, bpc, n, cod, knob_pairs=(), xlib=None):
     S = 3
     cells = batch_data(S, n, cell, first=cell + bpc)
-    H.tune_set(11, variant)
-    H.tune_set(12, pf)
-    try:
-        got = H.crc32c_batch(coder(6, 3), torch.from_numpy(cells).to(dev), bpc)
+    with knobs(knob_pairs, xlib):
+        got = H.crc32c_batch(cod, torch.from_numpy(cells).to(dev), bpc)
         torch.cuda.synchronize()
-    finally:
-        H.tune_set(11, 0)
-        H.tune_set(12, 0)
     assert np.array_equal(got.cpu().numpy(), _oracle_sums(cells, bpc))
 
 
@@ -727,85 +668,42 @@ def test_crc32c_device_published_vector(dev):
     assert got.cpu().numpy().ravel().tobytes() == (0xE3069283).to_bytes(4, "big")
 
 
-@pytest.mark.parametrize("codec,k,m,cell,S", [
+ENCODE_CRC_CASES = [
     ("rs", 6, 3, 1 << 16, 4), ("rs", 6, 3, 3 * 512 + 16, 5), ("rs", 6, 3, (1 << 16) + 48, 3),
     ("rs", 10, 4, 1 << 15, 3), ("rs", 10, 4, 70 * 512 + 256, 2), ("rs", 3, 2, 1 << 17, 3),
-    ("rs", 2, 1, 8192 + 512, 4), ("rs", 12, 4, 1 << 14, 2), ("rs", 6, 3, 1000, 2), ("xor", 2, 1, 1 << 14, 3)])
-@pytest.mark.parametrize("fused", [0, 4, 8, None])
-@pytest.mark.parametrize("scheme", [0, 1, 5])
-def test_encode_crc_device(dev, c_oracle, codec, k, m, cell, S, fused, scheme):
-    """Fused encode+CRC (k in {2,3,6,10}) and the two-pass fallback (other k,
-    unaligned cell_len, or tune key 9) against oracle parity + oracle CRCs;
-    scheme = tune key 11 (0: the fold, 1: slicing-by-8, 5: 11-bit slicing)."""
+    ("rs", 2, 1, 8192 + 512, 4), ("rs", 12, 4, 1 << 14, 2), ("rs", 6, 3, 1000, 2), ("xor", 2, 1, 1 << 14, 3),
+    ("rs", 3, 2, 8192 + 512, 4), ("rs", 6, 3, 1 << 14, 7), ("rs", 2, 1, 1 << 15, 2), ("rs", 10, 4, 1 << 14, 5)]
+
+
+@pytest.mark.parametrize("codec,k,m,cell,S", ENCODE_CRC_CASES)
+def test_encode_crc_device(dev, c_oracle, codec, k, m, cell, S):
+    """Fused encode+CRC (k in {2,3,6,10}: 8 slabs per wave for k <= 6 and
+    r <= 3, else 4 with the inputs two at a time) and the two-pass fallback
+    (other k, unaligned cell_len) against oracle parity + oracle CRCs."""
+    encode_crc_body(dev, c_oracle, codec, k, m, cell, S, None)
+
+
+def encode_crc_body(dev, c_oracle, codec, k, m, cell, S, xlib, knob_pairs=()):
     bpc = 512
     data = batch_data(S, k, cell, first=31 + cell)
     if codec == "xor":
         par = np.bitwise_xor.reduce(data, axis=1, keepdims=True)
-        cod = H.Coder(k, m, 0, "xor")
+        cod = H.Coder(k, m, 0, "xor", lib=xlib)
     else:
         par = oracle_batch_encode(c_oracle, k, m, data)
-        cod = coder(k, m)
+        cod = coder(k, m, xlib)
     d = torch.from_numpy(data).to(dev)
     p = torch.zeros((S, m, cell), dtype=torch.uint8, device=dev)
     nch = (cell + bpc - 1) // bpc
     sums = torch.zeros((S, k + m, nch, 4), dtype=torch.uint8, device=dev)
     dp, ds = H.stripe_layout_ptrs(d, k)
     pp, ps = H.stripe_layout_ptrs(p, m)
-    # fused: 0 = default slabs/wave, 4 / 8 forced; None = two-pass fallback
-    H.tune_set(9, 1 if fused is None else 0)
-    H.tune_set(10, fused or 0)
-    H.tune_set(11, scheme)
-    try:
+    with knobs(knob_pairs, xlib):
         cod.encode_crc_device(dp, ds, pp, ps, cell, S, bpc, sums.data_ptr(), torch.cuda.current_stream().cuda_stream)
         torch.cuda.synchronize()
-    finally:
-        H.tune_set(9, 0)
-        H.tune_set(10, 0)
-        H.tune_set(11, 0)
     assert np.array_equal(p.cpu().numpy(), par)
     want = _oracle_sums(np.concatenate([data, par], axis=1), bpc)
     assert np.array_equal(sums.cpu().numpy(), want)
-
-
-@pytest.mark.parametrize("k,m,cell,S,slabs", [(10, 4, 1 << 15, 3, 0), (3, 2, 8192 + 512, 4, 4), (6, 3, 1 << 14, 2, 4)])
-@pytest.mark.parametrize("pair", [1, 2])
-def test_fused_input_pairing(dev, c_oracle, k, m, cell, S, slabs, pair):
-    """Fused encode + CRC32C and decode + verify at 4 slabs per wave with the
-    inputs two at a time (tune key 19 = 2, the default) and one at a time (1),
-    an odd k included, against the oracle."""
-    bpc = 512
-    data = batch_data(S, k, cell, first=57 + cell + pair)
-    par = oracle_batch_encode(c_oracle, k, m, data)
-    d = torch.from_numpy(data).to(dev)
-    p = torch.zeros((S, m, cell), dtype=torch.uint8, device=dev)
-    nch = cell // bpc
-    sums = torch.zeros((S, k + m, nch, 4), dtype=torch.uint8, device=dev)
-    dp, ds = H.stripe_layout_ptrs(d, k)
-    pp, ps = H.stripe_layout_ptrs(p, m)
-    sp = torch.cuda.current_stream().cuda_stream
-    cod = coder(k, m)
-    H.tune_set(19, pair)
-    H.tune_set(10, slabs)
-    try:
-        cod.encode_crc_device(dp, ds, pp, ps, cell, S, bpc, sums.data_ptr(), sp)
-        torch.cuda.synchronize()
-        assert np.array_equal(p.cpu().numpy(), par)
-        want = _oracle_sums(np.concatenate([data, par], axis=1), bpc)
-        assert np.array_equal(sums.cpu().numpy(), want)
-        out = torch.zeros_like(d)
-        bad = torch.zeros((S, k + m), dtype=torch.uint8, device=dev)
-        op, os_ = H.stripe_layout_ptrs(out, k)
-        miss = list(range(min(m, k)))
-        cod.decode_verify_device(H.CHECKSUM_CRC32C, [None if i in miss else dp[i] for i in range(k)] + pp, ds + ps,
-                                 op, os_, cell, S, bpc, sums.data_ptr(), bad.data_ptr(), sp)
-        torch.cuda.synchronize()
-        assert not bad.cpu().numpy().any()
-        o = out.cpu().numpy()
-        for i in miss:
-            assert np.array_equal(o[:, i], data[:, i])
-    finally:
-        H.tune_set(19, 0)
-        H.tune_set(10, 0)
 
 
 def test_encode_crc_full_size_properties(dev):
@@ -846,19 +744,21 @@ def _oracle_checksums(cells: np.ndarray, bpc: int, ctype: int) -> np.ndarray:
     return out
 
 
+CHECKSUM_CASES = [(512 * 64, 512, 3), (512 * 70 + 256, 512, 2), (1000, 512, 3), (4096, 4096, 2), (2048, 100, 2)]
+
+
 @pytest.mark.parametrize("ctype", CKSUM_TYPES)
-@pytest.mark.parametrize("cell,bpc,n", [(512 * 64, 512, 3), (512 * 70 + 256, 512, 2), (1000, 512, 3),
-                                        (4096, 4096, 2), (2048, 100, 2)])
-@pytest.mark.parametrize("variant", [0, 1, 5, 7])
-def test_checksum_device_vs_oracle(dev, ctype, cell, bpc, n, variant):
+@pytest.mark.parametrize("cell,bpc,n", CHECKSUM_CASES)
+def test_checksum_device_vs_oracle(dev, ctype, cell, bpc, n):
+    checksum_body(dev, ctype, cell, bpc, n, coder(6, 3))
+
+
+def checksum_body(dev, ctype, cell, bpc, n, cod, knob_pairs=(), xlib=None):
     S = 3
     cells = batch_data(S, n, cell, first=cell + bpc + ctype)
-    H.tune_set(11, variant)
-    try:
-        got = H.checksum_batch(coder(6, 3), torch.from_numpy(cells).to(dev), ctype, bpc)
+    with knobs(knob_pairs, xlib):
+        got = H.checksum_batch(cod, torch.from_numpy(cells).to(dev), ctype, bpc)
         torch.cuda.synchronize()
-    finally:
-        H.tune_set(11, 0)
     assert np.array_equal(got.cpu().numpy(), _oracle_checksums(cells, bpc, ctype))
 
 
@@ -915,19 +815,25 @@ def _verified_read_expect(k, m, data, parity, missing, missing_parity, sums_np, 
     return outs, bads, oks
 
 
-@pytest.mark.parametrize("ctype", CKSUM_TYPES)
-@pytest.mark.parametrize("k,m,cell,bpc,missing,missing_parity", [
+VERIFY_CASES = [
     (6, 3, 1 << 15, 512, [0, 1, 2], []), (6, 3, 512 * 9 + 48, 512, [4], [1]), (6, 3, 1 << 14, 512, [], []),
     (10, 4, 1 << 14, 512, [0, 1, 2, 3], []), (10, 4, 1 << 13, 512, [7], [0]), (3, 2, 1 << 14, 512, [1], []),
     (2, 1, 8192, 512, [0], []), (12, 4, 1 << 13, 512, [2, 5], []), (6, 3, 3000, 100, [0, 5], []),
-    (6, 3, 4096 + 16, 4096, [3], [])])
-@pytest.mark.parametrize("scheme", [0, 1, 5])
-def test_decode_verify_vs_oracle(dev, c_oracle, ctype, k, m, cell, bpc, missing, missing_parity, scheme):
+    (6, 3, 4096 + 16, 4096, [3], [])]
+
+
+@pytest.mark.parametrize("ctype", CKSUM_TYPES)
+@pytest.mark.parametrize("k,m,cell,bpc,missing,missing_parity", VERIFY_CASES)
+def test_decode_verify_vs_oracle(dev, c_oracle, ctype, k, m, cell, bpc, missing, missing_parity):
     """Fused (k in {2,3,6,10}, 512-B chunks) and two-pass decode+verify: clean
     stripes, corrupt survivors (data and parity), a stripe that runs out of
     verified shards; rebuilt data, bad flags and the error all as the
-    oracle's read_slice restatement.  scheme = tune key 11 (0: 11-bit
-    slicing, 1: slicing-by-8)."""
+    oracle's read_slice restatement."""
+    decode_verify_body(dev, c_oracle, ctype, k, m, cell, bpc, missing, missing_parity, coder(k, m))
+
+
+def decode_verify_body(dev, c_oracle, ctype, k, m, cell, bpc, missing, missing_parity, cod, knob_pairs=(),
+                       xlib=None):
     S = 6
     data = batch_data(S, k, cell, first=5 + cell + k)
     parity = oracle_batch_encode(c_oracle, k, m, data)
@@ -949,7 +855,6 @@ def test_decode_verify_vs_oracle(dev, c_oracle, ctype, k, m, cell, bpc, missing,
     want_data, want_bad, oks = _verified_read_expect(k, m, bd, bp, set(missing), set(missing_parity), sums_np,
                                                      bpc, ctype)
     assert not oks[5] and oks[0] and oks[4]
-    cod = coder(k, m)
     d, p = torch.from_numpy(bd).to(dev), torch.from_numpy(bp).to(dev)
     out = torch.zeros_like(d)
     sums = torch.from_numpy(sums_np).to(dev)
@@ -959,14 +864,11 @@ def test_decode_verify_vs_oracle(dev, c_oracle, ctype, k, m, cell, bpc, missing,
     op, os_ = H.stripe_layout_ptrs(out, k)
     ptrs = [None if i in missing else dp[i] for i in range(k)] + \
         [None if j in missing_parity else pp[j] for j in range(m)]
-    H.tune_set(11, scheme)
-    try:
+    with knobs(knob_pairs, xlib):
         with pytest.raises(H.ErasureCodingError):
             cod.decode_verify_device(ctype, ptrs, ds + ps, op, os_, cell, S, bpc, sums.data_ptr(), bad.data_ptr(),
                                      torch.cuda.current_stream().cuda_stream)
         torch.cuda.synchronize()
-    finally:
-        H.tune_set(11, 0)
     o, b = out.cpu().numpy(), bad.cpu().numpy()
     for s in range(S):
         if not oks[s]:
@@ -1165,3 +1067,230 @@ def test_numa_host_buffers_feed_the_host_batch(c_oracle):
     assert node >= -1
     import ctypes
     assert H.lib.hec_host_free(ctypes.c_void_p(12345)) == H.HEC_ERR_INVALID_ARG  # not ours: refused, not freed
+
+
+# ---- full-batch oracle parity at the BASELINE sizes -------------------------
+# Every byte of every stripe of the benchmark batches against the C
+# restatement (oracle/ec_oracle.c), stripe-parallel on the box's CPU share:
+# the engine's parity, and its decode of the worst-case erasure set against
+# the oracle's decode of the same survivors (gf256.rs:61-137).
+
+def _cpu_share():
+    import os
+    return max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 8)))
+
+
+@pytest.mark.parametrize("k,m,cell,S,lost", [(6, 3, 1 << 20, 1024, (0, 1, 2)), (6, 3, 1 << 16, 65536, (0, 1, 2)),
+                                             (10, 4, 1 << 20, 256, (0, 1, 2, 3))])
+def test_full_batch_vs_oracle(dev, c_oracle, k, m, cell, S, lost):
+    cod = coder(k, m)
+    d = _device_random((S, k, cell), dev, seed=0x5EED_EC00 + k * 7 + S)
+    p = torch.empty((S, m, cell), dtype=torch.uint8, device=dev)
+    H.encode_batch(cod, d, p)
+    e = len(lost)
+    rec = torch.empty((S, e, cell), dtype=torch.uint8, device=dev)
+    dp, ds = H.stripe_layout_ptrs(d, k)
+    pp, ps = H.stripe_layout_ptrs(p, m)
+    shard_ptrs = [None if i in lost else dp[i] for i in range(k)] + pp
+    out = [rec.data_ptr() + lost.index(i) * cell if i in lost else 0 for i in range(k)]
+    cod.decode_device(shard_ptrs, ds + ps, out, [e * cell] * k, cell, S, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert torch.equal(rec, d[:, list(lost)])  # the round trip, on the device
+    present = ((1 << (k + m)) - 1) & ~sum(1 << i for i in lost)
+    step = max(1, (1 << 31) // (k * cell))  # <= 2 GiB of data per slice on the host
+    for a in range(0, S, step):
+        b = min(S, a + step)
+        O.c_check_batch(c_oracle, k, m, d[a:b].cpu().numpy(), p[a:b].cpu().numpy(), present,
+                        rec[a:b].cpu().numpy(), threads=_cpu_share())
+
+
+# ---- whole files: the last row short (CellBuffer / CellReader semantics) ----
+
+def _file_sizes(k, cell):
+    # rust/tests/test_ec.rs:77-87 sizes_to_test around this cell size, plus a
+    # 1-byte file and one row +- 4
+    return [1, 16, cell - 4, cell, cell + 4, k * cell - 4, k * cell, k * cell + 4, 5 * k * cell - 4, 5 * k * cell,
+            5 * k * cell + 4]
+
+
+def _want_parity(rows, k, m, cell):
+    want = np.zeros((len(rows), m, cell), dtype=np.uint8)
+    for r, row in enumerate(rows):
+        for j in range(m):
+            par = np.frombuffer(row[k + j], dtype=np.uint8)
+            want[r, j, :len(par)] = par
+    return want
+
+
+@pytest.mark.parametrize("k,m", [(3, 2), (6, 3), (10, 4)])
+def test_encode_rows_partial_last_row(dev, k, m):
+    """hec_encode_rows_host / _device over whole files: full rows batched, the
+    short last row padded as CellBuffer::encode (block_writer.rs:817-851),
+    parity cells of len(cell 0) bytes, the slot past them zeroed."""
+    cell = 1 << 16
+    cod = coder(k, m)
+    ws = torch.empty(cod.encode_rows_workspace_size(cell), dtype=torch.uint8, device=dev)
+    for L in _file_sizes(k, cell):
+        data = splitmix64_bytes(L * 3 + k, L)
+        rows = O.striped_write(data.tobytes(), k, m, cell)
+        want = _want_parity(rows, k, m, cell)
+        hp = np.full((len(rows), m, cell), 0xA5, dtype=np.uint8)
+        cod.encode_rows_host(data.ctypes.data, L, hp.ctypes.data, cell, 2)
+        assert np.array_equal(hp, want), L
+        dd = torch.from_numpy(data.copy()).to(dev)
+        dpar = torch.full((len(rows), m, cell), 0xA5, dtype=torch.uint8, device=dev)
+        cod.encode_rows_device(dd.data_ptr(), L, dpar.data_ptr(), cell, ws.data_ptr(), ws.numel(),
+                               torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        assert np.array_equal(dpar.cpu().numpy(), want), L
+
+
+@pytest.mark.parametrize("k,m", [(3, 2), (6, 3), (10, 4)])
+def test_decode_rows_partial_last_row(c_oracle, k, m):
+    """hec_decode_rows_host over the blocks a striped write leaves (shard i =
+    max_offset(i) bytes, ec/mod.rs:40-60): short and absent cells read as
+    zeros (CellReader::next_cell), the file trimmed to its length; every lost
+    set the reader can meet, against the oracle's striped read."""
+    cell = 1 << 16
+    cod = coder(k, m)
+    lost_sets = [(), (0,), (k - 1,), (0, k), tuple(range(m)), tuple(range(k - m, k))]
+    for L in _file_sizes(k, cell):
+        data = splitmix64_bytes(L * 5 + k, L).tobytes()
+        vert = O.vertical_buffers(O.striped_write(data, k, m, cell), k, m)
+        for i in range(k + m):
+            assert len(vert[i]) == O.max_offset(k, cell, i, L)
+        arrs = [np.frombuffer(v, dtype=np.uint8) for v in vert]
+        for lost in lost_sets:
+            want = O.striped_read([None if i in lost else vert[i] for i in range(k + m)], k, m, cell, L)
+            assert want == data
+            out = np.full(L + 64, 0x3C, dtype=np.uint8)  # 64 guard bytes past the file
+            addrs = [0 if i in lost else arrs[i].ctypes.data for i in range(k + m)]
+            lens = [0 if i in lost else len(vert[i]) for i in range(k + m)]
+            cod.decode_rows_host(addrs, lens, cell, out.ctypes.data, L, 2)
+            assert out[:L].tobytes() == data, (L, lost)
+            assert (out[L:] == 0x3C).all(), (L, lost)
+
+
+@pytest.mark.parametrize("k,m", [(3, 2), (6, 3)])
+@pytest.mark.parametrize("route", ["default", "device", "host"])
+def test_per_call_reference_sizes(c_oracle, k, m, route):
+    """The per-call drop-in (hec_encode / hec_decode) on every row a striped
+    write of the reference's sizes_to_test files (test_ec.rs:77-87, 1 MiB
+    cells) produces, through the default size routing, the device forced
+    (host limit 0) and the host routine forced; bit-exact vs the oracle."""
+    cell = 1 << 20
+    cod = H.Coder(k, m, 0)
+    cod.host_limit = {"default": cod.host_limit, "device": 0, "host": 1 << 30}[route]
+    for L in [16, cell - 4, cell, cell + 4, 5 * k * cell - 4, 5 * k * cell + 4]:
+        data = splitmix64_bytes(L + 17 * k, L).tobytes()
+        rows = O.cell_buffer_rows(data, k, cell)
+        for r in (rows[0], rows[-1]):  # a full row (when there is one) and the last row
+            n0 = len(r[0])
+            padded = [c + b"\0" * (n0 - len(c)) for c in r]
+            want = O.cell_buffer_encode(k, m, r)[k:]
+            got = cod.encode(padded)
+            assert got == want, (L, n0)
+            shards = [None if i < m else (padded + got)[i] for i in range(k + m)]  # worst case
+            cod.decode(shards)
+            assert shards[:k] == padded, (L, n0)
+    cod.close()
+
+
+# ---- pooled coders (Coder::new per row) -------------------------------------
+
+def test_coder_pool_reuses_and_isolates(dev, c_oracle):
+    H.pool_trim()
+    a = H.Coder(6, 3, 0, pooled=True)
+    ha = a.handle.value
+    a.close()
+    b = H.Coder(6, 3, 0, pooled=True)
+    assert b.handle.value == ha  # the idle coder comes back
+    c = H.Coder(6, 3, 0, pooled=True)
+    assert c.handle.value != ha  # b is still out: a second coder
+    x = H.Coder(3, 2, -1, pooled=True)  # another key; any device
+    assert x.device == 0 and x.handle.value not in (ha, c.handle.value)
+    data = [splitmix64_bytes(40 + i, 4096) for i in range(6)]
+    want = [w.tobytes() for w in O.c_encode(c_oracle, 6, 3, data)]
+    assert b.encode(data) == want and c.encode(data) == want
+    for cc in (b, c, x):
+        cc.close()
+    assert H.pool_trim() == 3
+
+
+def test_coder_pool_threads(dev, c_oracle):
+    # 8 threads x 300 acquire / encode / decode / release cycles of small rows
+    import threading
+    errors = []
+    k, m = 6, 3
+
+    def worker(t):
+        rng = np.random.default_rng(t)
+        try:
+            for it in range(300):
+                n = int(rng.integers(1, 5000))
+                data = [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(k)]
+                c = H.Coder(k, m, 0, pooled=True)
+                par = c.encode(data)
+                shards = [None, None] + [d.tobytes() for d in data[2:]] + par
+                c.decode(shards)
+                c.close()
+                if par != [w.tobytes() for w in O.c_encode(c_oracle, k, m, data)] or shards[0] != data[0].tobytes():
+                    errors.append((t, it))
+        except Exception as e:  # surfaced below
+            errors.append(repr(e))
+
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join(timeout=100)
+    assert not errors, errors[:5]
+    assert H.pool_trim() <= 8  # at most one idle coder per concurrent user
+
+
+# ---- verified reads sharing one coder (the phase-2 scratch is serialised) ---
+
+def test_decode_verify_two_threads_share_a_coder(dev, c_oracle):
+    import threading
+    k, m, cell, S = 6, 3, 1 << 14, 24
+    cod = H.Coder(k, m, 0)
+    data = batch_data(S, k, cell, first=4242)
+    par = oracle_batch_encode(c_oracle, k, m, data)
+    sums_np = np.concatenate([data, par], axis=1)
+    sums = torch.from_numpy(np.stack([np.stack([np.frombuffer(O.chunk_crc32c(sums_np[s, i].tobytes(), 512),
+                                                              dtype=np.uint8).reshape(-1, 4)
+                                                for i in range(k + m)]) for s in range(S)])).to(dev)
+    errors = []
+
+    def worker(t):
+        try:
+            st = torch.cuda.Stream(dev)
+            for it in range(15):
+                bent = data.copy()
+                bad_stripes = list(range(t, S, 2 + it % 3))  # different patterns per thread / round
+                for s in bad_stripes:
+                    bent[s, 1 + t, (it * 97 + s) % cell] ^= 0x41
+                with torch.cuda.stream(st):
+                    d = torch.from_numpy(bent).to(dev)
+                    p = torch.from_numpy(par).to(dev)
+                    out = torch.zeros_like(d)
+                    bad = H.decode_verify_batch(cod, d, p, [0], sums, out, stream=st)
+                st.synchronize()
+                b = bad.cpu().numpy()
+                want = np.zeros((S, k + m), dtype=np.uint8)
+                want[bad_stripes, 1 + t] = 1
+                o = out.cpu().numpy()
+                if not np.array_equal(b, want) or not np.array_equal(o[:, 0], data[:, 0]):
+                    errors.append((t, it, "flags/rebuilt"))
+                if not all(np.array_equal(o[s, 1 + t], data[s, 1 + t]) for s in bad_stripes):
+                    errors.append((t, it, "repair"))
+        except Exception as e:  # surfaced below
+            errors.append(repr(e))
+
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(2)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join(timeout=100)
+    cod.close()
+    assert not errors, errors[:5]

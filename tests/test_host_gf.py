@@ -1,0 +1,19 @@
+"""The engine's host-side GF(2^8) multiply (hdfs-native_amd/csrc/host_gf.cpp:
+AVX-512BW+GFNI, AVX2, scalar), the per-call drop-in's small-row path, against
+the oracle on the CPU: tests/cpp/host_gf_check.cpp runs every ISA this CPU
+supports over RS encode/decode matrices and random matrices at every tail
+length, and checks the affine bit matrix of every coefficient."""
+import os
+import subprocess
+
+from conftest import PKG_DIR
+
+BIN = os.path.join(PKG_DIR, "build", "host_gf_check")
+
+
+def test_host_gf_every_isa_vs_oracle():
+    if not os.path.exists(BIN):
+        subprocess.check_call(["make", "-s", "-C", PKG_DIR, "build/host_gf_check"])
+    out = subprocess.run([BIN], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-4000:]
+    assert "host gf ok" in out.stdout

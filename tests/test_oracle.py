@@ -355,3 +355,23 @@ def test_legacy_decode_plan_round_trip():
         rec = O.matmul_shards(dm, [shards[i] for i in surv])
         for idx, arr in zip(miss, rec):
             assert np.array_equal(arr, data[idx])
+
+
+def test_striped_write_matches_reference_block_lengths():
+    # the oracle's striped writer (CellBuffer::write / encode restated) leaves
+    # every shard exactly max_offset(i) bytes (ec/mod.rs:40-60, the
+    # reference's own block-length rule), and its striped read (CellReader
+    # zero-padding + ec_decode + trim) returns the file for every lost set
+    # of up to m shards
+    import itertools
+
+    import ec_oracle as O
+    for k, m, cell in [(3, 2, 4096), (6, 3, 1024), (10, 4, 512)]:
+        for L in [1, 16, cell - 4, cell, cell + 4, k * cell - 4, k * cell, 5 * k * cell - 4, 5 * k * cell + 4]:
+            data = bytes((i * 131 + L) & 0xFF for i in range(L))
+            vert = O.vertical_buffers(O.striped_write(data, k, m, cell), k, m)
+            assert [len(v) for v in vert] == [O.max_offset(k, cell, i, L) for i in range(k + m)]
+            for e in range(m + 1):
+                for lost in list(itertools.combinations(range(k + m), e))[:6]:
+                    v = [None if i in lost else vert[i] for i in range(k + m)]
+                    assert O.striped_read(v, k, m, cell, L) == data, (k, m, L, lost)

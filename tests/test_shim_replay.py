@@ -23,6 +23,7 @@ def test_shim_call_sequence_on_device():
     out = subprocess.run([BIN], capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stderr[-4000:]
     assert "shim replay ok" in out.stdout
+    print(out.stdout)
 
 
 def test_shim_without_device_is_clean_error():
