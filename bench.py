@@ -46,6 +46,11 @@ GIB = float(1 << 30)
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic_configs.json")
 
 
+def log(msg):
+    """Progress on stderr (the JSON line stays the only stdout line)."""
+    print(f"bench[{os.environ.get('RANK', '0')}] {time.strftime('%H:%M:%S')} {msg}", file=sys.stderr, flush=True)
+
+
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -569,6 +574,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = max_over_ranks(t1 - t0, dev)
+    log(f"timed {args.steps} steps: {elapsed / args.steps * 1e3:.3f} ms/step")
 
     # correctness gate (after the timed region): decode reconstructs the
     # erased shards of every stripe (on the device), and every stripe's parity
@@ -582,6 +588,7 @@ def main():
     import ec_oracle
     clib = ec_oracle.load_c_oracle()
     verified = verify_batch(args, ec_oracle, clib, data, parity, None if (args.encode_only or mixed) else rec, k, m)
+    log(f"verified: {verified}")
 
 
     enc_ms = [evs[i][0].elapsed_time(evs[i][1]) for i in range(args.steps)]
@@ -655,9 +662,12 @@ def main():
     if host_path and rank == 0 and not mixed:
         result["host_path"] = pinned_leg(coder, data, parity, k, m, cell, S, torch)
         result["host_path"]["per_call"] = per_call_leg(H, k, m, cell, 64, clib)
+        log("host path legs")
         result["host_path"]["per_call_by_size"] = per_call_sizes(H, k, m, clib)
+        log("per-call table")
 
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        log("cpu baseline")
         result["cpu_baseline"] = cpu_baseline(k, m, cell, args.cpu_seconds, 1)
         if args.cpu_threads > 1:
             result["cpu_baseline_parallel"] = cpu_baseline(k, m, cell, args.cpu_seconds, args.cpu_threads)
@@ -764,6 +774,7 @@ def extra_configs(args, H, dist, world, rank, dev, max_over_ranks, shard_range):
         if world > 1:
             dist.barrier()
         elapsed = max_over_ranks(t1 - t0, dev)
+        log(f"extra config {cfg['name']}: {elapsed / steps * 1e3:.3f} ms/step")
         assert torch.equal(rec, data[:, :m]), f"{cfg['name']}: decode != original"
         launch = [evs[i][0].elapsed_time(evs[i][1]) for i in range(steps)] + \
                  [evs[i][1].elapsed_time(evs[i][2]) for i in range(steps)]
