@@ -22,8 +22,10 @@
 #include "checksum.hpp"
 #include "checksum_device.hpp"
 #include "checksum_tables.hpp"
+#include "bitslice.hpp"
 #include "ec_kernels.hpp"
 #include "gf_device.hpp"
+#include "xor_networks.hpp"
 
 namespace hec {
 
@@ -55,10 +57,19 @@ __device__ __forceinline__ const crc::Tables<KIND>& fused_tables() {
 //   VERIFY: checksummed shards 0..K-1 = the survivors; their expected sums
 //     sit at the same index (shard_id = survivor shard numbers), a mismatch
 //     sets bad[stripe * n_total + shard_id[s]].
-template <int K, int R, int SLABS, int SCHEME, int KIND, bool VERIFY, int WPE = 2, bool PAIR = false>
+// BSL (encode with the RS coding matrix, K in {3, 6, 10}): the parity is
+// computed bit-sliced -- each input's 8-dword groups transposed into bit
+// planes (bitslice.hpp) and folded into the accumulator planes by the
+// generated XOR network of the RS parity rows (xor_networks.hpp), the planes
+// transposed back at the end -- instead of through the v_perm product
+// tables: RS(6,3) 650 instead of 960 VALU per 8 dwords of every shard,
+// RS(10,4) 1155 instead of 2000.  The kernel is VALU-issue bound.
+template <int K, int R, int SLABS, int SCHEME, int KIND, bool VERIFY, int WPE = 2, bool PAIR = false,
+          bool BSL = false>
 __global__ __launch_bounds__(crcdev::sliced(SCHEME) ? 128 * WPE * (WPE - 1) : 512)
     __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void gf_fused_crc(
     MatmulArgs a, FusedCrcArgs cs) {
+    static_assert(!BSL || (!VERIFY && bitslice::rs_net_available<K, R>() && SLABS % 2 == 0), "bit-sliced encode");
     using TL = crcdev::TableLayout<SCHEME>;
     using Spec = crc::Spec<KIND>;
     constexpr bool REFL = Spec::kReflected;
@@ -160,11 +171,50 @@ __global__ __launch_bounds__(crcdev::sliced(SCHEME) ? 128 * WPE * (WPE - 1) : 51
             if (shard % SPR == SPR - 1 || shard == NSUM - 1) crc_round(shard - shard % SPR, shard % SPR + 1);
         };
 
-        u32x4 acc[SLABS][R];
+        u32x4 acc[BSL ? 1 : SLABS][R];
+        if constexpr (!BSL) {
 #pragma unroll
-        for (int u = 0; u < SLABS; u++)
+            for (int u = 0; u < SLABS; u++)
 #pragma unroll
-            for (int j = 0; j < R; j++) acc[u][j] = u32x4{0, 0, 0, 0};
+                for (int j = 0; j < R; j++) acc[u][j] = u32x4{0, 0, 0, 0};
+        }
+        // BSL: group g = slabs 2g, 2g+1 (8 dwords) as R*8 bit planes
+        uint32_t accp[BSL ? SLABS / 2 : 1][BSL ? R * 8 : 1];
+        // input i's share of the parity, bit-sliced (input 0 initialises accp)
+        auto bsl_absorb = [&](int i, const u32x4 (&xi)[SLABS]) {
+            if constexpr (BSL) {
+#pragma unroll
+                for (int g = 0; g < SLABS / 2; g++) {
+                    uint32_t pl[8] = {xi[2 * g][0],     xi[2 * g][1],     xi[2 * g][2],     xi[2 * g][3],
+                                      xi[2 * g + 1][0], xi[2 * g + 1][1], xi[2 * g + 1][2], xi[2 * g + 1][3]};
+                    if (i > 0) {
+                        // opaque per input: keeps the XOR chains of the
+                        // accumulators from being reassociated across inputs
+#pragma unroll
+                        for (int t = 0; t < R * 8; t++) asm volatile("" : "+v"(accp[g][t]));
+                    }
+                    bitslice::transpose8(pl);
+                    bitslice::rs_absorb_at<K, R>(i, pl, accp[g]);
+                    // one group's planes and network temporaries live at a time
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+        };
+        // parity row j's slabs back from the planes (the transpose is its own inverse)
+        auto bsl_output = [&](int j, u32x4 (&o)[SLABS]) {
+            if constexpr (BSL) {
+#pragma unroll
+                for (int g = 0; g < SLABS / 2; g++) {
+                    uint32_t q[8];
+#pragma unroll
+                    for (int t = 0; t < 8; t++) q[t] = accp[g][8 * j + t];
+                    bitslice::transpose8(q);
+                    o[2 * g] = u32x4{q[0], q[1], q[2], q[3]};
+                    o[2 * g + 1] = u32x4{q[4], q[5], q[6], q[7]};
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+        };
         u32x4 x[SLABS], xn[SLABS];
 #pragma unroll
         for (int u = 0; u < SLABS; u++) x[u] = load16<true>(a.in[0] + (uint64_t(stripe) * a.in_stride[0] + wbyte) + voff[u]);
@@ -187,6 +237,10 @@ __global__ __launch_bounds__(crcdev::sliced(SCHEME) ? 128 * WPE * (WPE - 1) : 51
                     stage_piece(0, u, x[u]);
                     if (two) stage_piece(1, u, xn[u]);
                 }
+                if constexpr (BSL) {
+                    bsl_absorb(i, x);
+                    if (two) bsl_absorb(i + 1, xn);
+                } else {
                 uint32_t toff = uint32_t(i) * uint32_t(sizeof(PermTable));
                 asm volatile("" : "+v"(toff));
 #pragma unroll
@@ -238,6 +292,7 @@ __global__ __launch_bounds__(crcdev::sliced(SCHEME) ? 128 * WPE * (WPE - 1) : 51
                                                         sa.s1, sa.s2);
                         }
                     }
+                }  // !BSL
                 __builtin_amdgcn_sched_barrier(0);
                 if (i + 2 < K) {
 #pragma unroll
@@ -256,7 +311,7 @@ __global__ __launch_bounds__(crcdev::sliced(SCHEME) ? 128 * WPE * (WPE - 1) : 51
         } else {
 #pragma unroll
             for (int i = 0; i < K; i++) {
-                if (PF && i + 1 < K) {
+                if (PF && !BSL && i + 1 < K) {
     #pragma unroll
                     for (int u = 0; u < SLABS; u++)
                         xn[u] = load16<true>(a.in[i + 1] + (uint64_t(stripe) * a.in_stride[i + 1] + wbyte) + voff[u]);
@@ -264,6 +319,9 @@ __global__ __launch_bounds__(crcdev::sliced(SCHEME) ? 128 * WPE * (WPE - 1) : 51
                 __builtin_amdgcn_sched_barrier(0);
     #pragma unroll
                 for (int u = 0; u < SLABS; u++) stage_piece(i % SPR, u, x[u]);
+                if constexpr (BSL) {
+                    bsl_absorb(i, x);
+                } else {
                 // opaque per-input table offset threaded through the
                 // accumulators: keeps the table reads (and the GF math) of input
                 // i from being hoisted next to those of the other inputs
@@ -295,10 +353,19 @@ __global__ __launch_bounds__(crcdev::sliced(SCHEME) ? 128 * WPE * (WPE - 1) : 51
                         for (int j = 0; j < R; j++)
                             acc[u][j][d] ^= gf_mul4(tb[j][0], tb[j][1], tb[j][2], tb[j][3], tb[j][4], sl.s0, sl.s1, sl.s2);
                     }
+                }  // !BSL
+                __builtin_amdgcn_sched_barrier(0);
+                // BSL: the next shard's loads go out after this shard's GF
+                // math (x is dead by then), in flight across the CRC round
+                if (BSL && i + 1 < K) {
+    #pragma unroll
+                    for (int u = 0; u < SLABS; u++)
+                        x[u] = load16<true>(a.in[i + 1] + (uint64_t(stripe) * a.in_stride[i + 1] + wbyte) + voff[u]);
+                }
                 __builtin_amdgcn_sched_barrier(0);
                 after_stage(i);
                 __builtin_amdgcn_sched_barrier(0);
-                if (i + 1 < K) {
+                if (!BSL && i + 1 < K) {
     #pragma unroll
                     for (int u = 0; u < SLABS; u++)
                         x[u] = PF ? xn[u]
@@ -308,10 +375,17 @@ __global__ __launch_bounds__(crcdev::sliced(SCHEME) ? 128 * WPE * (WPE - 1) : 51
         }
 #pragma unroll
         for (int j = 0; j < R; j++) {
+            u32x4 o[SLABS];
+            if constexpr (BSL) {
+                bsl_output(j, o);
+            } else {
+#pragma unroll
+                for (int u = 0; u < SLABS; u++) o[u] = acc[u][j];
+            }
 #pragma unroll
             for (int u = 0; u < SLABS; u++) {
-                if (live[u]) store16<true>(a.out[j] + (uint64_t(stripe) * a.out_stride[j] + wbyte) + voff[u], acc[u][j]);
-                if constexpr (!VERIFY) stage_piece((K + j) % SPR, u, acc[u][j]);
+                if (live[u]) store16<true>(a.out[j] + (uint64_t(stripe) * a.out_stride[j] + wbyte) + voff[u], o[u]);
+                if constexpr (!VERIFY) stage_piece((K + j) % SPR, u, o[u]);
             }
             if constexpr (!VERIFY) after_stage(K + j);
         }
@@ -572,16 +646,34 @@ const void* verify_kind(int kind, bool pair = false) {
 // measurement build adds 11 = 11-bit slicing (tune key 11 = 5), 1 =
 // slicing-by-8 (key 11 = 1), the rejected schemes and shapes.  The product
 // library compiles the default slab count / pairing of each (K, R) only.
+// the bit-sliced parity (BSL) for the RS coding matrix of (K, R) with a
+// generated network; RS(2,1) keeps the v_perm tables (no gain: 162 vs 160 VALU)
 template <int K, int R>
-const void* encode_fn(int slabs, int scheme, int wpe, bool pair) {
+constexpr bool bsl_shape() {
+    return bitslice::rs_net_available<K, R>() && K > 2;
+}
+
+template <int K, int R, int SCHEME, bool PAIR>
+const void* encode_bsl(bool bsl) {
+    constexpr int SL = fused_slabs(K, R);
+    if constexpr (bsl_shape<K, R>())
+        if (bsl) return reinterpret_cast<const void*>(&gf_fused_crc<K, R, SL, SCHEME, crc::kCrc32c, false, 2, PAIR, true>);
+    return reinterpret_cast<const void*>(&gf_fused_crc<K, R, SL, SCHEME, crc::kCrc32c, false, 2, PAIR>);
+}
+
+template <int K, int R>
+const void* encode_fn(int slabs, int scheme, int wpe, bool pair, bool bsl) {
 #ifndef HEC_EXPERIMENTAL
     (void)slabs;
     (void)scheme;
     (void)wpe;
     (void)pair;
     constexpr int SL = fused_slabs(K, R);
-    return reinterpret_cast<const void*>(&gf_fused_crc<K, R, SL, 12, crc::kCrc32c, false, 2, SL == 4>);
+    return encode_bsl<K, R, 12, SL == 4>(bsl);
 #else
+    // bit-sliced parity at the default slab count (tune key 22 = 1: off)
+    if (bsl && scheme == 12 && wpe != 3 && slabs == fused_slabs(K, R) && (slabs == 8 || pair))
+        return encode_bsl<K, R, 12, fused_slabs(K, R) == 4>(true);
     // rejected (same-box A/B, profiles/r01_probe_fused_scheme.log,
     // r02_probe_fused_rep2.log, r02_probe_fused_wpe3_*.log):
     // bank-replicated slicing-by-1 (4 chains) and slicing-by-2 (tune key 11
@@ -636,13 +728,25 @@ const void* pick_split(bool verify, int r, int kind, bool prio) {
 #endif
 
 template <int K>
-const void* pick_r(bool verify, int r, int slabs, int scheme, int kind, int wpe, bool pair) {
+const void* pick_r(bool verify, int r, int slabs, int scheme, int kind, int wpe, bool pair, bool bsl) {
     switch (r) {
-        case 1: return verify ? verify_fn<K, 1>(kind, scheme, wpe, pair) : encode_fn<K, 1>(slabs, scheme, wpe, pair);
-        case 2: return verify ? verify_fn<K, 2>(kind, scheme, wpe, pair) : encode_fn<K, 2>(slabs, scheme, wpe, pair);
-        case 3: return verify ? verify_fn<K, 3>(kind, scheme, wpe, pair) : encode_fn<K, 3>(slabs, scheme, wpe, pair);
-        default: return verify ? verify_fn<K, 4>(kind, scheme, wpe, pair) : encode_fn<K, 4>(slabs, scheme, wpe, pair);
+        case 1: return verify ? verify_fn<K, 1>(kind, scheme, wpe, pair) : encode_fn<K, 1>(slabs, scheme, wpe, pair, bsl);
+        case 2: return verify ? verify_fn<K, 2>(kind, scheme, wpe, pair) : encode_fn<K, 2>(slabs, scheme, wpe, pair, bsl);
+        case 3: return verify ? verify_fn<K, 3>(kind, scheme, wpe, pair) : encode_fn<K, 3>(slabs, scheme, wpe, pair, bsl);
+        default: return verify ? verify_fn<K, 4>(kind, scheme, wpe, pair) : encode_fn<K, 4>(slabs, scheme, wpe, pair, bsl);
     }
+}
+
+// The launch's coefficients are the RS coding matrix's parity rows
+// (gen_rs_matrix, gf256.rs:40-57): the bit-sliced network applies.
+bool rs_parity_matrix(const MatmulArgs& a) {
+    if (a.k < 1 || a.k > kMaxK || a.r < 1 || a.r > kMaxR) return false;
+    for (int j = 0; j < a.r; j++)
+        for (int i = 0; i < a.k; i++) {
+            const uint8_t s = uint8_t(a.k + j) ^ uint8_t(i);
+            if (a.coef[j * kMaxK + i] != (s == 0 ? 0 : gf_div(1, s))) return false;
+        }
+    return true;
 }
 
 int launch_fused(const MatmulArgs& in, const FusedCrcArgs& cs, bool verify, int device, hipStream_t stream) {
@@ -702,11 +806,14 @@ int launch_fused(const MatmulArgs& in, const FusedCrcArgs& cs, bool verify, int 
         if (!fn) return -1;
 #endif
     } else {
+        // encode with the RS matrix: the bit-sliced parity (tune key 22 = 1: the
+        // v_perm tables, measurement build)
+        const bool bsl = !verify && tn.fused_bsl != 1 && rs_parity_matrix(a);
         switch (a.k) {
-            case 2: fn = pick_r<2>(verify, a.r, slabs, scheme, cs.kind, wpe, pair); break;
-            case 3: fn = pick_r<3>(verify, a.r, slabs, scheme, cs.kind, wpe, pair); break;
-            case 6: fn = pick_r<6>(verify, a.r, slabs, scheme, cs.kind, wpe, pair); break;
-            case 10: fn = pick_r<10>(verify, a.r, slabs, scheme, cs.kind, wpe, pair); break;
+            case 2: fn = pick_r<2>(verify, a.r, slabs, scheme, cs.kind, wpe, pair, bsl); break;
+            case 3: fn = pick_r<3>(verify, a.r, slabs, scheme, cs.kind, wpe, pair, bsl); break;
+            case 6: fn = pick_r<6>(verify, a.r, slabs, scheme, cs.kind, wpe, pair, bsl); break;
+            case 10: fn = pick_r<10>(verify, a.r, slabs, scheme, cs.kind, wpe, pair, bsl); break;
             default: return -1;
         }
     }
@@ -721,7 +828,7 @@ int launch_fused(const MatmulArgs& in, const FusedCrcArgs& cs, bool verify, int 
     a.chunks = uint32_t(chunks);
     a.tiles_per_stripe = uint32_t(tps);
     a.total_tiles = uint32_t(total);
-    a.group = group_for(a.stripes, tn.group > 0 ? uint32_t(tn.group) : 4u);
+    tile_order(a.stripes, a.tiles_per_stripe, tn.group > 0 ? uint32_t(tn.group) : 4u, a.group, a.grouped_tiles);
     // LDS: ~61 KiB per 256-thread block (two per CU) / ~131 KiB per 512-thread block (one)
     // a grid of 8 blocks per CU (2 or 1 resident): finer-grained dynamic
     // scheduling beats exactly the resident blocks by 3 % (RS(6,3)) to 5 %

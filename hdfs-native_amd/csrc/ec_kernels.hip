@@ -367,6 +367,7 @@ __global__ __launch_bounds__(BS) void gf_decode_mixed(MixedArgs a) {
     MatmulArgs order;  // tile_coords reads tiles_per_stripe / group only
     order.tiles_per_stripe = a.tiles_per_stripe;
     order.group = a.group;
+    order.grouped_tiles = a.grouped_tiles;
     order.stripes = a.stripes;
 
     // RESIDENT: grouped interleaved order (best DRAM locality).  Otherwise
@@ -790,7 +791,7 @@ int launch_gf_matmul(const MatmulArgs& in, int device, hipStream_t stream) {
         a.total_tiles = uint32_t(total);
         // 4 stripes column-interleaved: +1-4 % over stripe-major at 1 MiB
         // cells (profiles/r01_probe_tile_order.log)
-        a.group = group_for(a.stripes, tn.group > 0 ? uint32_t(tn.group) : 4u);
+        tile_order(a.stripes, a.tiles_per_stripe, tn.group > 0 ? uint32_t(tn.group) : 4u, a.group, a.grouped_tiles);
         // stores drained before the next tile's loads unless key 6 = 1: same-box
         // bench A/B (profiles/r02_drain_ab.txt): RS(6,3) 1 MiB 3702 vs 3514
         // GiB/s, RS(10,4) 3926 vs 3906, RS(3,2) 3089 vs 3075 -- DRAM prefers a
@@ -907,7 +908,7 @@ int launch_decode_mixed(const MixedArgs& in, int rows, int device, hipStream_t s
     a.chunks = uint32_t(chunks);
     a.tiles_per_stripe = uint32_t(tps);
     a.total_tiles = uint32_t(total);
-    a.group = group_for(a.stripes, tn.group > 0 ? uint32_t(tn.group) : 4u);
+    tile_order(a.stripes, a.tiles_per_stripe, tn.group > 0 ? uint32_t(tn.group) : 4u, a.group, a.grouped_tiles);
     a.drain = tn.drain == 1 ? 0u : 1u;
     uint64_t grid = uint64_t(num_cus(device)) * bpc;
     if (grid > total) grid = total;

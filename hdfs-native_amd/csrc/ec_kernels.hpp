@@ -29,7 +29,8 @@ struct MatmulArgs {
     uint32_t chunks;              // vec kernel: 16-B chunks per cell
     uint32_t tiles_per_stripe;
     uint32_t total_tiles;
-    uint32_t group;               // tile order: G stripes column-interleaved (1 = stripe-major); divides stripes
+    uint32_t group;               // tile order: G stripes column-interleaved (1 = stripe-major)
+    uint32_t grouped_tiles;       // tiles of the whole G-stripe groups; the remainder stripes go stripe-major
     uint32_t drain;               // register kernel: 1 = wait for the tile's stores before the next tile's loads
 };
 
@@ -67,7 +68,7 @@ struct MixedArgs {
     int32_t row0;                     // first missing row handled by this launch
     uint64_t cell_len;
     uint64_t stripes;
-    uint32_t chunks, tiles_per_stripe, total_tiles, group;
+    uint32_t chunks, tiles_per_stripe, total_tiles, group, grouped_tiles;
     uint32_t drain;                   // 1 = wait for a tile's stores before the next tile (tune key 6)
 };
 

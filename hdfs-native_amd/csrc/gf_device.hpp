@@ -75,20 +75,24 @@ struct Sel {
 // Tile order: stripes are taken G at a time and, inside a group, tiles go
 // column-major (tile-column c of all G stripes, then c+1), so the blocks in
 // flight together touch G stripes x (grid/G) columns.  G = 1 is plain
-// stripe-major order.
+// stripe-major order.  A stripe count that G does not divide leaves
+// stripes % G remainder stripes after the last whole group
+// (a.grouped_tiles = (stripes / G) * G * tiles_per_stripe); their tiles run
+// stripe-major, so a prime batch keeps the grouped order for all but its last
+// G - 1 stripes (it used to fall back to stripe-major throughout).
 __device__ __forceinline__ void tile_coords(uint32_t tile, const MatmulArgs& a, uint32_t& stripe, uint32_t& tcol) {
     const uint32_t tps = a.tiles_per_stripe;
     const uint32_t G = a.group;
-    if (G <= 1) {
+    if (G <= 1 || tile >= a.grouped_tiles) {
+        // grouped_tiles is a whole number of stripes: tile / tps is the stripe
         stripe = tile / tps;
         tcol = tile - stripe * tps;
         return;
     }
-    // the launchers pick G dividing the stripe count (group_for), so there is
-    // no short last group and G is the only divisor: loop-invariant, its
-    // reciprocal is hoisted out of the tile loop (a per-tile divisor made hipcc
-    // rebuild one with VALU float ops in the loop, whose temporaries landed in
-    // in-flight store registers and forced store drains)
+    // G and tps are launch constants: their reciprocals are hoisted out of
+    // the tile loop (a per-tile divisor made hipcc rebuild one with VALU
+    // float ops in the loop, whose temporaries landed in in-flight store
+    // registers and forced store drains)
     const uint32_t per_group = G * tps;
     const uint32_t g = tile / per_group;
     const uint32_t r = tile - g * per_group;
@@ -96,12 +100,12 @@ __device__ __forceinline__ void tile_coords(uint32_t tile, const MatmulArgs& a, 
     stripe = g * G + (r - tcol * G);
 }
 
-// Tile-order group for a batch: the largest of want, .., 2, 1 that divides
-// the stripe count (tile_coords assumes whole groups).
-__host__ __device__ inline uint32_t group_for(uint64_t stripes, uint32_t want) {
-    for (uint32_t g = want; g > 1; g--)
-        if (stripes % g == 0) return g;
-    return 1;
+// Tile-order group for a batch: `want` stripes per group (at most the
+// stripe count), and the tiles those whole groups cover.
+__host__ inline void tile_order(uint64_t stripes, uint32_t tiles_per_stripe, uint32_t want, uint32_t& group,
+                                uint32_t& grouped_tiles) {
+    group = uint32_t(want < 1 ? 1 : (stripes < want ? (stripes < 1 ? 1 : stripes) : want));
+    grouped_tiles = uint32_t((stripes / group) * group * tiles_per_stripe);
 }
 
 __device__ __forceinline__ Sel make_sel(uint32_t x) {

@@ -52,6 +52,8 @@
  *         and CRC rounds (default); 2 = role-split GF / CRC waves (one
  *         512-thread block per CU, RS(6,3) and RS(10,4) only), 3 = role-split
  *         with the CRC waves at raised priority
+ * key 22: fused encode + CRC parity: 0 = default (bit-sliced XOR network of
+ *         the RS matrix for RS(3,2), RS(6,3), RS(10,4)), 1 = v_perm tables
  * Returns HEC_OK, or HEC_ERR_INVALID_ARG for an unknown key / value.
  */
 #ifndef HDFS_EC_AMD_EXP_H

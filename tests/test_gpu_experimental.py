@@ -147,11 +147,12 @@ FUSED_TUNES = [[(11, 2)], [(11, 6)], [(16, 3)], [(16, 3), (11, 1)]]
 
 
 @pytest.mark.parametrize("k,m,cell,S", [(6, 3, 1 << 16, 3), (10, 4, 1 << 15, 2), (3, 2, 8192 + 512, 4)])
-@pytest.mark.parametrize("tunes", FUSED_TUNES)
+@pytest.mark.parametrize("tunes", FUSED_TUNES + [[(22, 1)], [(22, 1), (5, 0)]])
 def test_fused_variants_encode_vs_oracle(xlib, dev, c_oracle, k, m, cell, S, tunes):
     """Fused encode + CRC32C with the rejected variants: bank-replicated
-    slicing-by-1 / -by-2 tables (tune key 11 = 2 / 6) and one 768-thread
-    block per CU (key 16 = 3, 11-bit slicing or slicing-by-8)."""
+    slicing-by-1 / -by-2 tables (tune key 11 = 2 / 6), one 768-thread block
+    per CU (key 16 = 3, 11-bit slicing or slicing-by-8), and the v_perm table
+    parity instead of the default bit-sliced networks (key 22 = 1)."""
     bpc = 512
     data = batch_data(S, k, cell, first=77 + cell)
     par = oracle_batch_encode(c_oracle, k, m, data)
@@ -287,7 +288,7 @@ def test_tune_set_concurrent_with_launches(xlib, dev, c_oracle):
 
 
 def test_tune_set_rejects_unknown_values(xlib):
-    for key, value in [(3, 99), (1, 5), (5, 6), (11, 8), (16, 1), (17, 6), (19, 3), (20, 3), (21, 4), (22, 0), (0, 0)]:
+    for key, value in [(3, 99), (1, 5), (5, 6), (11, 8), (16, 1), (17, 6), (19, 3), (20, 3), (21, 4), (22, 2), (23, 0), (0, 0)]:
         with pytest.raises(ValueError):
             H.tune_set(key, value, xlib)
 

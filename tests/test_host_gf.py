@@ -17,3 +17,15 @@ def test_host_gf_every_isa_vs_oracle():
     out = subprocess.run([BIN], capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr[-4000:]
     assert "host gf ok" in out.stdout
+
+
+BSL_BIN = os.path.join(PKG_DIR, "build", "bitslice_check")
+
+
+def test_bitslice_networks_vs_oracle():
+    """The fused encode kernel's bit-sliced parity (8x8 bit transpose +
+    generated XOR networks) equals the oracle's RS parity, per byte."""
+    subprocess.check_call(["make", "-s", "-C", PKG_DIR, "build/bitslice_check"])
+    out = subprocess.run([BSL_BIN], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr[-4000:]
+    assert "ok" in out.stdout
