@@ -653,6 +653,17 @@ def main():
         "decode_GiBps": round(k * cell * S / (sum(dec_ms) / len(dec_ms) * 1e-3) / GIB, 2) if dec_ms else None,
         "parity_check": verified,
     }
+    if mixed and dec_ms:
+        # the mixed-pattern decode kernel alone: k survivors read + e_s rebuilt
+        # cells written per stripe, over its own launch average
+        result["roofline"]["kernel"] = (f"gf_matmul_v16<{k},{m}> encode + gf_decode_mixed<{k},{min(m, 4)}> "
+                                        f"(achieved / frac over both launch kinds)")
+        dec_avg_ms = sum(dec_ms) / len(dec_ms)
+        result["roofline"]["decode_mixed"] = {
+            "algorithmic_bytes_per_launch": dec_bytes, "avg_launch_ms": round(dec_avg_ms, 4),
+            "achieved": round(dec_bytes / (dec_avg_ms * 1e-3) / 1e9, 1),
+            "frac": round(dec_bytes / (dec_avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "erased_cells": int(erased)}
 
     if args.crc:
         result["crc32c"] = crc_leg(args, H, coder, data, parity, rec, dp, ds, pp, ps, rp, rs, shard_ptrs, miss,

@@ -26,7 +26,8 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PEAK = 8.0e12
-COMMON = ["--steps", "10", "--warmup", "3", "--spinup", "0.3", "--cpu-seconds", "0", "--host-path", "0"]
+COMMON = ["--steps", "10", "--warmup", "3", "--spinup", "0.3", "--cpu-seconds", "0", "--host-path", "0",
+          "--extra-configs", "0"]  # extra configs run other kernels shapes in the same process
 # name -> (bench args, k, m, cell, stripes, launches per step)
 CONFIGS = {
     "rs32": (["--k", "3", "--m", "2", "--stripes", "1024"], 3, 2, 1 << 20, 1024, 2),
