@@ -513,7 +513,10 @@ void hec_coder_destroy(hec_coder_t* c) {
         if (c->dbuf) (void)hipFree(c->dbuf);
         if (c->call_dev) (void)hipFree(c->call_dev);
         if (c->call_host) (void)hipHostFree(c->call_host);
-        if (c->verify_ws) (void)hipFree(c->verify_ws);
+        if (c->verify_ws) {  // stream-ordered allocation (verified read phase 2)
+            (void)hipFreeAsync(c->verify_ws, nullptr);
+            (void)hipStreamSynchronize(nullptr);
+        }
         for (int i = 0; i < 2; i++) {
             if (c->ev_mixed[i]) (void)hipEventSynchronize(c->ev_mixed[i]);
             if (c->mixed_host[i]) (void)hipHostFree(c->mixed_host[i]);
@@ -1577,11 +1580,12 @@ int hec_decode_verify_device(hec_coder_t* c, int checksum_type, const uint8_t* c
             }
             const size_t need = flat.size() * sizeof(uint32_t);
             if (c->verify_ws_bytes < need) {
-                if (c->verify_ws) (void)hipFree(c->verify_ws);
+                // stream-ordered: growing the scratch costs no device-wide sync
+                if (c->verify_ws) (void)hipFreeAsync(c->verify_ws, stream);
                 c->verify_ws = nullptr;
                 c->verify_ws_bytes = 0;
                 const size_t want = std::max(need, size_t(64) << 10);
-                HEC_HIP(hipMalloc(&c->verify_ws, want), HEC_ERR_NO_MEMORY);
+                HEC_HIP(hipMallocAsync(reinterpret_cast<void**>(&c->verify_ws), want, stream), HEC_ERR_NO_MEMORY);
                 c->verify_ws_bytes = want;
             }
             const uint32_t* d_lists = reinterpret_cast<const uint32_t*>(c->verify_ws);
@@ -1619,10 +1623,10 @@ int hec_decode_verify_device(hec_coder_t* c, int checksum_type, const uint8_t* c
         if (any_rebuild) {
             const size_t ws_need = mixed_workspace(k, c->m, stripes);
             if (c->verify_ws_bytes < ws_need) {
-                if (c->verify_ws) (void)hipFree(c->verify_ws);
+                if (c->verify_ws) (void)hipFreeAsync(c->verify_ws, stream);
                 c->verify_ws = nullptr;
                 c->verify_ws_bytes = 0;
-                HEC_HIP(hipMalloc(&c->verify_ws, ws_need), HEC_ERR_NO_MEMORY);
+                HEC_HIP(hipMallocAsync(reinterpret_cast<void**>(&c->verify_ws), ws_need, stream), HEC_ERR_NO_MEMORY);
                 c->verify_ws_bytes = ws_need;
             }
             // storage for shard indices no plan reads (absent for the whole batch)
@@ -1762,6 +1766,67 @@ int hec_group_decode_host_batch(hec_group_t* g, const uint8_t* const* h_vertical
             for (size_t s = 0; s < c->k + c->m; s++)
                 vert[s] = h_vertical[s] ? h_vertical[s] + first * cell_len : nullptr;
             return hec_decode_host_batch(c, vert, cell_len, count, h_file + first * c->k * cell_len, chunk_rows);
+        });
+    });
+}
+
+}  // extern "C"
+
+// Device-resident batches over the group: every slot's launch is enqueued
+// from the calling thread (an enqueue is microseconds and asynchronous, so
+// the GPUs run concurrently without host threads); every slot is tried, the
+// lowest failing slot's status is returned.
+namespace {
+template <class F>
+int group_enqueue(hec_group_t* g, F&& body) {
+    int first_rc = HEC_OK;
+    size_t first_slot = 0;
+    std::string first_err;
+    for (size_t i = 0; i < g->coders.size(); i++) {
+        const int rc = body(i);
+        if (rc != HEC_OK && first_rc == HEC_OK) {
+            first_rc = rc;
+            first_slot = i;
+            first_err = g_last_error;
+        }
+    }
+    if (first_rc != HEC_OK)
+        std::snprintf(g_last_error, sizeof(g_last_error), "group slot %zu: %s", first_slot, first_err.c_str());
+    return first_rc;
+}
+}  // namespace
+
+extern "C" {
+
+int hec_group_encode_device(hec_group_t* g, const uint8_t* const* d_data, const size_t* data_strides,
+                            uint8_t* const* d_parity, const size_t* parity_strides, size_t cell_len,
+                            const size_t* stripes, void* const* hip_streams) {
+    if (!g || !d_data || !data_strides || !d_parity || !parity_strides || !stripes || cell_len == 0)
+        return HEC_ERR_INVALID_ARG;
+    return guarded([&] {
+        return group_enqueue(g, [&](size_t i) {
+            hec_coder_t* c = g->coders[i];
+            if (stripes[i] == 0) return int(HEC_OK);
+            return hec_encode_device(c, d_data + i * c->k, data_strides + i * c->k, d_parity + i * c->m,
+                                     parity_strides + i * c->m, cell_len, stripes[i],
+                                     hip_streams ? hip_streams[i] : nullptr);
+        });
+    });
+}
+
+int hec_group_decode_device(hec_group_t* g, const uint8_t* const* d_shards, const size_t* shard_strides,
+                            uint8_t* const* d_out, const size_t* out_strides, size_t cell_len,
+                            const size_t* stripes, void* const* hip_streams) {
+    if (!g || !d_shards || !shard_strides || !d_out || !out_strides || !stripes || cell_len == 0)
+        return HEC_ERR_INVALID_ARG;
+    return guarded([&] {
+        return group_enqueue(g, [&](size_t i) {
+            hec_coder_t* c = g->coders[i];
+            if (stripes[i] == 0) return int(HEC_OK);
+            const size_t n = c->k + c->m;
+            return hec_decode_device(c, d_shards + i * n, shard_strides + i * n, d_out + i * c->k,
+                                     out_strides + i * c->k, cell_len, stripes[i],
+                                     hip_streams ? hip_streams[i] : nullptr);
         });
     });
 }

@@ -737,18 +737,6 @@ const void* pick_r(bool verify, int r, int slabs, int scheme, int kind, int wpe,
     }
 }
 
-// The launch's coefficients are the RS coding matrix's parity rows
-// (gen_rs_matrix, gf256.rs:40-57): the bit-sliced network applies.
-bool rs_parity_matrix(const MatmulArgs& a) {
-    if (a.k < 1 || a.k > kMaxK || a.r < 1 || a.r > kMaxR) return false;
-    for (int j = 0; j < a.r; j++)
-        for (int i = 0; i < a.k; i++) {
-            const uint8_t s = uint8_t(a.k + j) ^ uint8_t(i);
-            if (a.coef[j * kMaxK + i] != (s == 0 ? 0 : gf_div(1, s))) return false;
-        }
-    return true;
-}
-
 int launch_fused(const MatmulArgs& in, const FusedCrcArgs& cs, bool verify, int device, hipStream_t stream) {
     MatmulArgs a = in;
     const Tune tn = tune_snapshot();

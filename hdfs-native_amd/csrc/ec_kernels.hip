@@ -31,10 +31,41 @@
 #include <algorithm>
 #include <cstdint>
 
+#include "bitslice.hpp"
 #include "ec_kernels.hpp"
 #include "gf_device.hpp"
+#include "xor_networks.hpp"
 
 namespace hec {
+
+namespace {
+// A wave-uniform 64-bit value held in a VGPR (e.g. from a broadcast LDS
+// read) moved into an SGPR pair (readfirstlane is int -> int: both halves
+// go through uint32_t, no sign extension).
+__device__ __forceinline__ uint64_t uniform64(uint64_t v) {
+    const uint32_t lo = uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(v))));
+    const uint32_t hi = uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(v >> 32))));
+    return uint64_t(lo) | (uint64_t(hi) << 32);
+}
+
+// Global-address-space byte pointers for bases that arrive as integers
+// (the mixed kernel's LDS shard table): a generic pointer made from an
+// integer compiles to flat_load / flat_store, which count in lgkmcnt as well
+// as vmcnt, so every LDS wait of the tile (plan, tables) also waited for the
+// cells in flight.  Global pointers keep them global_load / global_store.
+typedef __attribute__((address_space(1))) uint8_t gbyte;
+typedef __attribute__((address_space(1))) u32x4 gu32x4;
+
+__device__ __forceinline__ const gbyte* gptr(uint64_t a) { return reinterpret_cast<const gbyte*>(a); }
+__device__ __forceinline__ gbyte* gptr_w(uint64_t a) { return reinterpret_cast<gbyte*>(a); }
+
+__device__ __forceinline__ u32x4 gload16(const gbyte* p) {
+    return __builtin_nontemporal_load(reinterpret_cast<const gu32x4*>(p));
+}
+__device__ __forceinline__ void gstore16(gbyte* p, u32x4 v) {
+    __builtin_nontemporal_store(v, reinterpret_cast<gu32x4*>(p));
+}
+}  // namespace
 
 // ---------------------------------------------------------------------------
 // Vector kernel: 16 B per lane per shard, U column chunks per lane (chunk u
@@ -183,6 +214,104 @@ __global__ __launch_bounds__(BS) void gf_matmul_v16(MatmulArgs a) {
                 for (int j = 0; j < R; j++) store16<NT>(a.out[j] + uint64_t(stripe) * a.out_stride[j] + off, racc[j]);
             }
         }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Bit-sliced encode: gf_matmul_v16's skeleton (all K x U loads issued first,
+// the previous tile's store data held live across them, store drain per
+// tile) with the RS parity rows applied as generated XOR networks
+// (xor_networks.hpp) instead of the v_perm product tables.  Each lane's U
+// chunks of an input pair up into U/2 groups of 8 dwords; a group is
+// transposed into 8 bit planes (bitslice.hpp) and folded into its R x 8
+// accumulator planes by input i's network; at the end every parity row's
+// planes are transposed back into bytes.  RS(6,3): 650 VALU per 8 dwords of
+// every input instead of 960 (no selector ops, no table reads, no LDS
+// prologue).  Only for the RS coding matrix of (K, R) (gen_rs_matrix,
+// gf256.rs:40-57): the networks are that matrix's.
+// ---------------------------------------------------------------------------
+template <int K, int R, int U, int BS>
+__global__ __launch_bounds__(BS) void gf_encode_bsl(MatmulArgs a) {
+    static_assert(bitslice::rs_net_available<K, R>() && U % 2 == 0, "bit-sliced RS encode");
+    constexpr int G = U / 2;
+    const uint32_t chunks = a.chunks;
+    const uint32_t total = a.total_tiles;
+    constexpr uint32_t TILE = BS * U;
+    u32x4 acc[U][R];  // previous tile's store data (see gf_matmul_v16)
+#pragma unroll
+    for (int u = 0; u < U; u++)
+#pragma unroll
+        for (int j = 0; j < R; j++) acc[u][j] = u32x4{0, 0, 0, 0};
+    for (uint32_t tile = blockIdx.x; tile < total; tile += gridDim.x) {
+        uint32_t stripe, tcol;
+        tile_coords(tile, a, stripe, tcol);
+        u32x4 x[U][K];
+        bool live[U];
+        uint32_t offs[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint32_t col = tcol * TILE + u * BS + threadIdx.x;
+            live[u] = col < chunks;
+            offs[u] = (live[u] ? col : 0u) * 16u;
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++)
+#pragma unroll
+            for (int i = 0; i < K; i++) x[u][i] = load16<true>((a.in[i] + uint64_t(stripe) * a.in_stride[i]) + offs[u]);
+#pragma unroll
+        for (int u = 0; u < U; u++)
+#pragma unroll
+            for (int j = 0; j < R; j++) asm volatile("" ::"v"(acc[u][j]));
+        __builtin_amdgcn_sched_barrier(0);
+        uint32_t accp[G][R * 8];
+#pragma unroll
+        for (int i = 0; i < K; i++) {
+#pragma unroll
+            for (int g = 0; g < G; g++) {
+                uint32_t pl[8] = {x[2 * g][i][0],     x[2 * g][i][1],     x[2 * g][i][2],     x[2 * g][i][3],
+                                  x[2 * g + 1][i][0], x[2 * g + 1][i][1], x[2 * g + 1][i][2], x[2 * g + 1][i][3]};
+                if (i > 0) {
+                    // opaque per input: the accumulators' XOR chains are not
+                    // reassociated across inputs (that spills)
+#pragma unroll
+                    for (int t = 0; t < R * 8; t++) asm volatile("" : "+v"(accp[g][t]));
+                }
+                bitslice::transpose8(pl);
+                bitslice::rs_absorb_at<K, R>(i, pl, accp[g]);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < G; g++)
+#pragma unroll
+            for (int j = 0; j < R; j++) {
+                uint32_t q[8];
+#pragma unroll
+                for (int t = 0; t < 8; t++) q[t] = accp[g][8 * j + t];
+                bitslice::transpose8(q);
+                acc[2 * g][j] = u32x4{q[0], q[1], q[2], q[3]};
+                acc[2 * g + 1][j] = u32x4{q[4], q[5], q[6], q[7]};
+            }
+#pragma unroll
+        for (int u = 0; u < U; u++)
+#pragma unroll
+            for (int j = 0; j < R; j++) asm volatile("" : "+v"(acc[u][j]));
+        if ((tcol + 1) * TILE <= chunks) {  // block-uniform
+#pragma unroll
+            for (int u = 0; u < U; u++)
+#pragma unroll
+                for (int j = 0; j < R; j++)
+                    store16<true>((a.out[j] + uint64_t(stripe) * a.out_stride[j]) + offs[u], acc[u][j]);
+        } else {
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                if (!live[u]) continue;
+#pragma unroll
+                for (int j = 0; j < R; j++)
+                    store16<true>((a.out[j] + uint64_t(stripe) * a.out_stride[j]) + offs[u], acc[u][j]);
+            }
+        }
+        if (a.drain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
 }
 
@@ -420,7 +549,38 @@ __global__ __launch_bounds__(BS) void gf_decode_mixed(MixedArgs a) {
             }
             if (cur_none) continue;
         }
-        const int nrows = int(__builtin_amdgcn_readfirstlane(hdr->e)) - a.row0;  // rows of this launch in the plan
+        // The tile's metadata in three dependent LDS round trips, whatever K:
+        // the header words (e, survivor and missing shard bytes), then every
+        // survivor's and output's base / stride (VGPR-addressed broadcast
+        // reads, all in flight at once), then one wait and the readfirstlanes.
+        // Reading them survivor by survivor (LDS read, wait, readfirstlane,
+        // next) cost K + R serial round trips before the tile's loads.
+        const uint32_t* hw = reinterpret_cast<const uint32_t*>(hdr);
+        constexpr int SW = (K + 3) / 4;  // words of survivor bytes (surv[] at byte 4)
+        uint32_t w_surv[SW];
+        const uint32_t w_e = hw[0];
+        const uint32_t w_miss = hw[9 + a.row0 / 4];  // miss[] at byte 36; row0 is a multiple of kMaxR = 4
+#pragma unroll
+        for (int t = 0; t < SW; t++) w_surv[t] = hw[1 + t];
+        uint64_t v_base[K], v_stride[K], v_obase[R], v_ostride[R];
+#pragma unroll
+        for (int i = 0; i < K; i++) {
+            const uint32_t sh = (w_surv[i / 4] >> (8 * (i % 4))) & 0xFFu;
+            v_base[i] = s_base[sh];
+            v_stride[i] = s_stride[sh];
+        }
+#pragma unroll
+        for (int j = 0; j < R; j++) {
+            const uint32_t mi = (w_miss >> (8 * j)) & (kMaxK - 1);  // rows past e read a valid slot, never stored
+            v_obase[j] = s_obase[mi];
+            v_ostride[j] = s_ostride[mi];
+        }
+        // all of it read before the row-count branch below (otherwise hipcc
+        // sinks the reads past it: one more round trip)
+        uint32_t w_e2 = w_e;
+#pragma unroll
+        for (int i = 0; i < K; i++) asm volatile("" : "+v"(v_base[i]), "+v"(v_stride[i]), "+v"(w_e2));
+        const int nrows = int(__builtin_amdgcn_readfirstlane(w_e2)) - a.row0;  // rows of this launch in the plan
         if (nrows <= 0) continue;
         asm volatile("" ::: "memory");
 
@@ -435,10 +595,9 @@ __global__ __launch_bounds__(BS) void gf_decode_mixed(MixedArgs a) {
         u32x4 x[U][K];
 #pragma unroll
         for (int i = 0; i < K; i++) {
-            const int sh = __builtin_amdgcn_readfirstlane(hdr->surv[i]);
-            const uint8_t* ib = reinterpret_cast<const uint8_t*>(s_base[sh]) + uint64_t(stripe) * s_stride[sh];
+            const gbyte* ib = gptr(uniform64(v_base[i]) + uint64_t(stripe) * uniform64(v_stride[i]));
 #pragma unroll
-            for (int u = 0; u < U; u++) x[u][i] = load16<true>(ib + offs[u]);
+            for (int u = 0; u < U; u++) x[u][i] = gload16(ib + offs[u]);
         }
 #pragma unroll
         for (int u = 0; u < U; u++)
@@ -486,11 +645,10 @@ __global__ __launch_bounds__(BS) void gf_decode_mixed(MixedArgs a) {
 #pragma unroll
         for (int j = 0; j < R; j++) {
             if (j >= nrows) break;  // block-uniform
-            const int mi = __builtin_amdgcn_readfirstlane(hdr->miss[a.row0 + j]);
-            uint8_t* ob = reinterpret_cast<uint8_t*>(s_obase[mi]) + uint64_t(stripe) * s_ostride[mi];
+            gbyte* ob = gptr_w(uniform64(v_obase[j]) + uint64_t(stripe) * uniform64(v_ostride[j]));
 #pragma unroll
             for (int u = 0; u < U; u++)
-                if (full || live[u]) store16<true>(ob + offs[u], acc[u][j]);
+                if (full || live[u]) gstore16(ob + offs[u], acc[u][j]);
         }
         if (a.drain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // as gf_matmul_v16
     }
@@ -525,7 +683,9 @@ __global__ __launch_bounds__(256) void gf_matmul_dw(MatmulArgs a) {
         for (int j = 0; j < R; j++) acc[j][0] = acc[j][1] = 0;
         for (int i = 0; i < k; i++) {
             const uintptr_t p = reinterpret_cast<uintptr_t>(a.in[i] + stripe * a.in_stride[i] + off);
-            const uint32_t* w = reinterpret_cast<const uint32_t*>(p & ~uintptr_t(3));
+            // global pointer: an integer-made generic one compiles to flat loads (see gbyte)
+            const __attribute__((address_space(1))) uint32_t* w =
+                reinterpret_cast<const __attribute__((address_space(1))) uint32_t*>(p & ~uintptr_t(3));
             const uint32_t sh = uint32_t(p & 3);
             const uint32_t w0 = w[0], w1 = w[1];
             const uint32_t w2 = sh ? w[2] : 0u;  // holds bytes 8g+8-sh.. of this group only when sh != 0
@@ -707,6 +867,29 @@ const void* pick_dma(int k, int r, int unroll, int bs) {
 #endif
 }
 
+// Bit-sliced encode for the (K, R) pairs with a generated network (K > 2:
+// RS(2,1)'s network is no shorter than its tables); nullptr otherwise.
+template <int K, int R>
+const void* bsl_fn(int block) {
+    if constexpr (bitslice::rs_net_available<K, R>() && K > 2) {
+        if (block == 512) return reinterpret_cast<const void*>(&gf_encode_bsl<K, R, 2, 512>);
+        return reinterpret_cast<const void*>(&gf_encode_bsl<K, R, 4, 256>);
+    }
+    (void)block;
+    return nullptr;
+}
+
+template <typename Sh>
+const void* pick_bsl(int k, int r, const Sh& sh) {
+    if (sh.unroll != (sh.block == 512 ? 2 : 4)) return nullptr;  // the compiled shapes only
+    switch (k) {
+        case 3: return r == 2 ? bsl_fn<3, 2>(sh.block) : nullptr;
+        case 6: return r == 3 ? bsl_fn<6, 3>(sh.block) : nullptr;
+        case 10: return r == 4 ? bsl_fn<10, 4>(sh.block) : nullptr;
+        default: return nullptr;
+    }
+}
+
 // Launch shape chosen from the MI355X sweeps in DESIGN.md ("Tuning"): long
 // per-wave runs (4 x 1 KiB per stream) at one 256-thread block per CU keep
 // the fewest DRAM rows open for a given bytes-in-flight.
@@ -734,6 +917,16 @@ Shape default_shape(int k, uint64_t cell_len) {
 }
 
 }  // namespace
+
+bool rs_parity_matrix(const MatmulArgs& a) {
+    if (a.k < 1 || a.k > kMaxK || a.r < 1 || a.r > kMaxR) return false;
+    for (int j = 0; j < a.r; j++)
+        for (int i = 0; i < a.k; i++) {
+            const uint8_t s = uint8_t(a.k + j) ^ uint8_t(i);
+            if (a.coef[j * kMaxK + i] != (s == 0 ? 0 : gf_div(1, s))) return false;
+        }
+    return true;
+}
 
 int launch_gf_matmul(const MatmulArgs& in, int device, hipStream_t stream) {
     MatmulArgs a = in;
@@ -780,6 +973,9 @@ int launch_gf_matmul(const MatmulArgs& in, int device, hipStream_t stream) {
             tile_mult = ek.tile_mult;
         }
 #endif
+        // the RS parity rows of a (K, R) with a generated network, register
+        // kernel: bit-sliced (tune key 23 = 1: the v_perm tables)
+        if (!fn && !sh.dma && tn.matmul_bsl != 1 && sh.unroll % 2 == 0 && rs_parity_matrix(a)) fn = pick_bsl(a.k, a.r, sh);
         if (!fn) fn = sh.dma ? pick_dma(a.k, a.r, sh.unroll, sh.block) : pick_vec(a.k, a.r, sh);
         if (!fn) return -1;
         const uint64_t tile = uint64_t(sh.block) * sh.unroll * tile_mult;

@@ -77,6 +77,11 @@ struct MixedArgs {
 // and cell_len % 16 == 0.  0 ok, -1 unsupported, >0 hipError_t.
 int launch_decode_mixed(const MixedArgs& a, int rows, int device, hipStream_t stream);
 
+// True when the launch's coefficients are the RS coding matrix's parity rows
+// (gen_rs_matrix, gf256.rs:40-57) for its (k, r): the encode kernels then
+// run the bit-sliced XOR networks of xor_networks.hpp.
+bool rs_parity_matrix(const MatmulArgs& a);
+
 // Launches the multiply for one group of <= kMaxR output rows.  0 on
 // success, -1 invalid sizes, otherwise the (positive) hipError_t.
 int launch_gf_matmul(const MatmulArgs& a, int device, hipStream_t stream);

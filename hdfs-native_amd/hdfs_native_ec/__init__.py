@@ -47,7 +47,8 @@ EXPORTS = [
     "hec_decode_device_mixed", "hec_coder_create_codec", "hec_decode_host_batch",
     "hec_crc32c_device", "hec_encode_crc_device", "hec_checksum_device", "hec_checksum_verify_device",
     "hec_decode_verify_device", "hec_group_create", "hec_group_destroy", "hec_group_size", "hec_group_coder",
-    "hec_group_range", "hec_group_encode_host_batch", "hec_group_decode_host_batch",
+    "hec_group_range", "hec_group_encode_host_batch", "hec_group_decode_host_batch", "hec_group_encode_device",
+    "hec_group_decode_device",
     "hec_device_alloc", "hec_device_free", "hec_device_numa_node", "hec_host_alloc", "hec_host_free",
     "hec_coder_acquire", "hec_coder_release", "hec_coder_pool_trim", "hec_coder_set_host_limit",
     "hec_coder_host_limit", "hec_gf_matmul_host", "hec_host_isa", "hec_encode_rows_host",
@@ -140,6 +141,8 @@ def _load(path: str = LIB_PATH) -> ctypes.CDLL:
         "hec_group_range": ([P, S, S, SP, SP], I),
         "hec_group_encode_host_batch": ([P, P, P, S, S, S], I),
         "hec_group_decode_host_batch": ([P, PP, S, S, P, S], I),
+        "hec_group_encode_device": ([P, PP, SP, PP, SP, S, SP, PP], I),
+        "hec_group_decode_device": ([P, PP, SP, PP, SP, S, SP, PP], I),
         "hec_device_alloc": ([I, S, ctypes.c_uint, ctypes.POINTER(P)], I),
         "hec_device_free": ([I, P], I),
         "hec_device_numa_node": ([I], I),
@@ -699,3 +702,19 @@ class CoderGroup:
     def decode_host_batch(self, vertical_addrs, cell_len: int, rows: int, h_file_addr: int, chunk_rows: int) -> None:
         _check(lib.hec_group_decode_host_batch(self._h, _pp([a or 0 for a in vertical_addrs]), cell_len, rows,
                                                ctypes.c_void_p(h_file_addr), chunk_rows))
+
+    def encode_device(self, data_ptrs, data_strides, parity_ptrs, parity_strides, cell_len: int, stripes,
+                      streams=None) -> None:
+        """hec_group_encode_device: per-slot lists (slot-major), each slot's
+        stripes on its own device; asynchronous on `streams` (raw handles)."""
+        _check(lib.hec_group_encode_device(self._h, _pp(data_ptrs), _sp(data_strides), _pp(parity_ptrs),
+                                           _sp(parity_strides), cell_len, _sp(stripes),
+                                           _pp(streams) if streams is not None else None))
+
+    def decode_device(self, shard_ptrs, shard_strides, out_ptrs, out_strides, cell_len: int, stripes,
+                      streams=None) -> None:
+        """hec_group_decode_device: shard_ptrs slot-major k+m per slot (None =
+        missing), out_ptrs k per slot."""
+        _check(lib.hec_group_decode_device(self._h, _pp([a or 0 for a in shard_ptrs]), _sp(shard_strides),
+                                           _pp([a or 0 for a in out_ptrs]), _sp(out_strides), cell_len,
+                                           _sp(stripes), _pp(streams) if streams is not None else None))

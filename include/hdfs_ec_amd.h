@@ -367,6 +367,27 @@ int hec_group_encode_host_batch(hec_group_t *group, const uint8_t *h_data, uint8
 int hec_group_decode_host_batch(hec_group_t *group, const uint8_t *const *h_vertical, size_t cell_len,
                                 size_t rows, uint8_t *h_file, size_t chunk_rows);
 
+/* Device-resident batches over the group (the in-process form of the
+ * bench's one-rank-per-GPU sharding; no host threads, no collective): slot i's
+ * stripes live in ITS device's HBM.  Per-slot arrays, slot-major: d_data[i*k
+ * + s] / data_strides[i*k + s] and d_parity[i*m + j] / parity_strides[i*m +
+ * j] as hec_encode_device takes them; for decode d_shards[i*(k+m) + s]
+ * (NULL = missing) / shard_strides[i*(k+m) + s] and d_out[i*k + s] /
+ * out_strides[i*k + s] as hec_decode_device.  stripes[i] = slot i's stripe
+ * count (0 = nothing), hip_streams[i] its stream on that device (NULL array =
+ * default streams).  Asynchronous like the single-coder calls: every slot's
+ * launch is enqueued from the calling thread, one device after another, and
+ * the GPUs run concurrently; synchronise the streams before reading.
+ * Returns the lowest failing slot's status; the other slots are still
+ * enqueued.  Replaces the per-writer join_all fan-out of block_writer.rs:954
+ * for device-resident stripes. */
+int hec_group_encode_device(hec_group_t *group, const uint8_t *const *d_data, const size_t *data_strides,
+                            uint8_t *const *d_parity, const size_t *parity_strides, size_t cell_len,
+                            const size_t *stripes, void *const *hip_streams);
+int hec_group_decode_device(hec_group_t *group, const uint8_t *const *d_shards, const size_t *shard_strides,
+                            uint8_t *const *d_out, const size_t *out_strides, size_t cell_len,
+                            const size_t *stripes, void *const *hip_streams);
+
 /* ---- HBM buffers for the batched API ------------------------------------ *
  * Device memory for stripe batches on `device` (hipExtMallocWithFlags).
  * Checksum sum / flag buffers passed to the checksum calls must be 4-byte

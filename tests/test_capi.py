@@ -152,6 +152,8 @@ def test_group_argument_checks_need_no_device():
     assert H.lib.hec_group_range(None, 10, 0, ctypes.byref(first), ctypes.byref(count)) == H.HEC_ERR_INVALID_ARG
     assert H.lib.hec_group_encode_host_batch(None, None, None, 16, 1, 1) == H.HEC_ERR_INVALID_ARG
     assert H.lib.hec_group_decode_host_batch(None, None, 16, 1, None, 1) == H.HEC_ERR_INVALID_ARG
+    assert H.lib.hec_group_encode_device(None, None, None, None, None, 16, None, None) == H.HEC_ERR_INVALID_ARG
+    assert H.lib.hec_group_decode_device(None, None, None, None, None, 16, None, None) == H.HEC_ERR_INVALID_ARG
     H.lib.hec_group_destroy(None)
     if not gpu_available():
         assert H.lib.hec_group_create(b"rs", 6, 3, devs, 2, ctypes.byref(out)) == H.HEC_ERR_DEVICE
@@ -189,7 +191,7 @@ def test_tune_set_validates_without_device():
     xlib = H.experimental_lib()
     assert xlib.hec_tune_set(3, 2) == H.HEC_OK
     assert xlib.hec_tune_set(3, 0) == H.HEC_OK
-    for key, value in [(6, 3), (16, 1), (3, 99), (18, 2), (17, 6), (19, 3), (20, 3), (21, 4), (22, 2), (23, 0), (0, 0)]:
+    for key, value in [(6, 3), (16, 1), (3, 99), (18, 2), (17, 6), (19, 3), (20, 3), (21, 4), (22, 2), (23, 2), (24, 0), (0, 0)]:
         assert xlib.hec_tune_set(key, value) == H.HEC_ERR_INVALID_ARG, (key, value)
 
 

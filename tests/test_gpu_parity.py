@@ -402,6 +402,44 @@ def test_device_decode_mixed_patterns(dev, c_oracle, k, m, cell):
     mixed_patterns_body(dev, c_oracle, k, m, cell, coder(k, m))
 
 
+@pytest.mark.parametrize("k,m", [(6, 3), (10, 4)])
+def test_device_decode_mixed_address_bit31(dev, c_oracle, k, m):
+    """The mixed kernel moves each survivor's and output's base address from
+    its LDS shard table into SGPRs (readfirstlane of both 32-bit halves).
+    Data, parity and output live at addresses whose low word has bit 31 set
+    (then clear), so a sign-extended low half cannot go unnoticed."""
+    S, cell = 12, 4096
+    data = batch_data(S, k, cell, first=4242 + k)
+    par = oracle_batch_encode(c_oracle, k, m, data)
+    masks = _random_masks(k, m, S, seed=77 + k)
+    masks[0] = ((1 << (k + m)) - 1) & ~((1 << m) - 1)  # worst case: data 0..m-1
+    need = S * (2 * k + m) * cell
+    big = torch.empty((1 << 31) + need + (1 << 25), dtype=torch.uint8, device=dev)
+    base = big.data_ptr()
+    for bit31 in (1, 0):
+        # first 4 KiB-aligned offset whose address has bit 31 == bit31
+        off = 0
+        while ((base + off) >> 31) & 1 != bit31:
+            off += 1 << 24
+        off += (-(base + off)) % 4096
+        assert ((base + off) >> 31) & 1 == bit31 and ((base + off + need) >> 31) & 1 == bit31
+        view = big[off:off + need]
+        d = view[:S * k * cell].view(S, k, cell)
+        p = view[S * k * cell:S * (k + m) * cell].view(S, m, cell)
+        out = view[S * (k + m) * cell:].view(S, k, cell)
+        d.copy_(torch.from_numpy(data))
+        p.copy_(torch.from_numpy(par))
+        out.fill_(0x5A)
+        H.decode_batch_mixed(coder(k, m), d, p, masks, out)
+        torch.cuda.synchronize()
+        o = out.cpu().numpy()
+        for s, mask in enumerate(masks):
+            for i in range(k):
+                if not (mask >> i) & 1:
+                    assert np.array_equal(o[s, i], data[s, i]), (bit31, s, i)
+    del big
+
+
 def mixed_patterns_body(dev, c_oracle, k, m, cell, cod, knob_pairs=(), xlib=None):
     S = 40
     data = batch_data(S, k, cell, first=900 + k)
@@ -1047,6 +1085,59 @@ def test_group_errors_and_slot_coders(dev, c_oracle):
     out = torch.zeros(rows * 6 * cell, dtype=torch.uint8).pin_memory()
     with pytest.raises(H.ErasureCodingError):
         g.decode_host_batch(ptrs, cell, rows, out.data_ptr(), 1)
+    g.close()
+
+
+@pytest.mark.parametrize("k,m,slots", [(6, 3, 3), (10, 4, 2), (3, 2, 5)])
+def test_group_device_resident_encode_decode(dev, c_oracle, k, m, slots):
+    """hec_group_encode_device / hec_group_decode_device: every slot's stripes
+    in its device's HBM (here all on device 0), each slot on its own stream,
+    uneven per-slot stripe counts (one slot empty), enqueued from one thread;
+    parity and rebuilt data bit-exact against the oracle."""
+    cell = 8192 + 16
+    g = H.CoderGroup(k, m, [0] * slots)
+    counts = [(3 + 2 * i) if i != 1 else 0 for i in range(slots)]
+    streams = [torch.cuda.Stream(dev) for _ in range(slots)]
+    datas = [batch_data(max(c, 1), k, cell, first=300 + 17 * i)[:c] for i, c in enumerate(counts)]
+    d = [torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in datas]
+    p = [torch.zeros((c, m, cell), dtype=torch.uint8, device=dev) for c in counts]
+    dp, ds, pp, ps = [], [], [], []
+    for i in range(slots):
+        a, b = H.stripe_layout_ptrs(d[i], k) if counts[i] else ([0] * k, [k * cell] * k)
+        c_, e_ = H.stripe_layout_ptrs(p[i], m) if counts[i] else ([0] * m, [m * cell] * m)
+        dp += a; ds += b; pp += c_; ps += e_
+    torch.cuda.synchronize()
+    g.encode_device(dp, ds, pp, ps, cell, counts, [s.cuda_stream for s in streams])
+    torch.cuda.synchronize()
+    for i in range(slots):
+        if counts[i]:
+            assert np.array_equal(p[i].cpu().numpy(), oracle_batch_encode(c_oracle, k, m, datas[i])), i
+    # decode: data shards 0..m-1 lost in every slot, rebuilt into out
+    out = [torch.zeros((c, k, cell), dtype=torch.uint8, device=dev) for c in counts]
+    sp, ss, op, os_ = [], [], [], []
+    for i in range(slots):
+        a, b = (dp[i * k:(i + 1) * k], ds[i * k:(i + 1) * k])
+        sp += [None if j < m else a[j] for j in range(k)] + pp[i * m:(i + 1) * m]
+        ss += b + ps[i * m:(i + 1) * m]
+        c_, e_ = H.stripe_layout_ptrs(out[i], k) if counts[i] else ([0] * k, [k * cell] * k)
+        op += c_; os_ += e_
+    g.decode_device(sp, ss, op, os_, cell, counts, [s.cuda_stream for s in streams])
+    torch.cuda.synchronize()
+    for i in range(slots):
+        if counts[i]:
+            assert torch.equal(out[i][:, :m], d[i][:, :m]), i
+    # a slot with too many losses: its status comes back, the others still run
+    bad = list(sp)
+    for j in range(m + 1):
+        bad[j] = None
+    for i in range(slots):
+        out[i].zero_()
+    with pytest.raises(H.ErasureCodingError):
+        g.decode_device(bad, ss, op, os_, cell, counts, [s.cuda_stream for s in streams])
+    torch.cuda.synchronize()
+    for i in range(1, slots):
+        if counts[i]:
+            assert torch.equal(out[i][:, :m], d[i][:, :m]), i
     g.close()
 
 
