@@ -323,9 +323,11 @@ __global__ __launch_bounds__(BS) void gf_encode_bsl(MatmulArgs a) {
 // 1 KiB (one wave-instruction each, lane-linear), read back by the SAME wave
 // (ds_read_b128 at lane*16) -- no cross-wave hand-off, no barrier.
 // ---------------------------------------------------------------------------
-template <int K, int R, int U, int BS>
+// BSL: the RS parity rows as bit-sliced XOR networks (see gf_encode_bsl).
+template <int K, int R, int U, int BS, bool BSL = false>
 __global__ __launch_bounds__(BS) void gf_matmul_dma(MatmulArgs a) {
     static_assert(K > 0, "DMA kernel needs a compile-time input count");
+    static_assert(!BSL || (bitslice::rs_net_available<K, R>() && U % 2 == 0), "bit-sliced RS encode");
     constexpr int WAVES = BS / 64;
     constexpr int PIECE = 1024;  // one wave-instruction: 64 lanes x 16 B
     // One LDS array for everything (a second __shared__ object next to the
@@ -393,6 +395,36 @@ __global__ __launch_bounds__(BS) void gf_matmul_dma(MatmulArgs a) {
         uint32_t stripe, tcol;
         tile_coords(tile, a, stripe, tcol);
         u32x4 acc[U][R];
+        if constexpr (BSL) {
+            constexpr int G = U / 2;
+            uint32_t accp[G][R * 8];
+#pragma unroll
+            for (int i = 0; i < K; i++) {
+#pragma unroll
+                for (int g = 0; g < G; g++) {
+                    uint32_t pl[8] = {x[2 * g][i][0],     x[2 * g][i][1],     x[2 * g][i][2],     x[2 * g][i][3],
+                                      x[2 * g + 1][i][0], x[2 * g + 1][i][1], x[2 * g + 1][i][2], x[2 * g + 1][i][3]};
+                    if (i > 0) {
+#pragma unroll
+                        for (int t = 0; t < R * 8; t++) asm volatile("" : "+v"(accp[g][t]));
+                    }
+                    bitslice::transpose8(pl);
+                    bitslice::rs_absorb_at<K, R>(i, pl, accp[g]);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+#pragma unroll
+            for (int g = 0; g < G; g++)
+#pragma unroll
+                for (int j = 0; j < R; j++) {
+                    uint32_t q[8];
+#pragma unroll
+                    for (int t = 0; t < 8; t++) q[t] = accp[g][8 * j + t];
+                    bitslice::transpose8(q);
+                    acc[2 * g][j] = u32x4{q[0], q[1], q[2], q[3]};
+                    acc[2 * g + 1][j] = u32x4{q[4], q[5], q[6], q[7]};
+                }
+        } else {
 #pragma unroll
         for (int u = 0; u < U; u++)
 #pragma unroll
@@ -423,6 +455,7 @@ __global__ __launch_bounds__(BS) void gf_matmul_dma(MatmulArgs a) {
             }
             __builtin_amdgcn_sched_barrier(0);
         }
+        }  // !BSL
         // wave-uniform: every lane of every chunk of this wave is live
         const bool full = __builtin_amdgcn_readfirstlane(
                               int(tcol * TILE + (U - 1) * BS + wave * 64 + 63 < chunks)) != 0;
@@ -867,6 +900,7 @@ const void* pick_dma(int k, int r, int unroll, int bs) {
 #endif
 }
 
+#ifdef HEC_EXPERIMENTAL
 // Bit-sliced encode for the (K, R) pairs with a generated network (K > 2:
 // RS(2,1)'s network is no shorter than its tables); nullptr otherwise.
 template <int K, int R>
@@ -889,6 +923,15 @@ const void* pick_bsl(int k, int r, const Sh& sh) {
         default: return nullptr;
     }
 }
+
+// LDS-DMA kernel with the bit-sliced RS parity (the product's (4, 256) shape)
+const void* pick_dma_bsl(int k, int r, int unroll, int bs) {
+    if (unroll != 4 || bs != 256) return nullptr;
+    if (k == 3 && r == 2) return reinterpret_cast<const void*>(&gf_matmul_dma<3, 2, 4, 256, true>);
+    if (k == 6 && r == 3) return reinterpret_cast<const void*>(&gf_matmul_dma<6, 3, 4, 256, true>);
+    return nullptr;
+}
+#endif  // HEC_EXPERIMENTAL
 
 // Launch shape chosen from the MI355X sweeps in DESIGN.md ("Tuning"): long
 // per-wave runs (4 x 1 KiB per stream) at one 256-thread block per CU keep
@@ -973,9 +1016,14 @@ int launch_gf_matmul(const MatmulArgs& in, int device, hipStream_t stream) {
             tile_mult = ek.tile_mult;
         }
 #endif
-        // the RS parity rows of a (K, R) with a generated network, register
-        // kernel: bit-sliced (tune key 23 = 1: the v_perm tables)
-        if (!fn && !sh.dma && tn.matmul_bsl != 1 && sh.unroll % 2 == 0 && rs_parity_matrix(a)) fn = pick_bsl(a.k, a.r, sh);
+#ifdef HEC_EXPERIMENTAL
+        // bit-sliced RS parity in the register / LDS-DMA kernels (tune key 23
+        // = 1).  Measured and not kept: same box, RS(6,3) 1
+        // MiB encode 3438-3451 vs 3671-3701 GiB/s with the v_perm tables;
+        // RS(3,2) and 64 KiB cells within noise
+        if (!fn && tn.matmul_bsl == 1 && sh.unroll % 2 == 0 && rs_parity_matrix(a))
+            fn = sh.dma ? pick_dma_bsl(a.k, a.r, sh.unroll, sh.block) : pick_bsl(a.k, a.r, sh);
+#endif
         if (!fn) fn = sh.dma ? pick_dma(a.k, a.r, sh.unroll, sh.block) : pick_vec(a.k, a.r, sh);
         if (!fn) return -1;
         const uint64_t tile = uint64_t(sh.block) * sh.unroll * tile_mult;
@@ -1067,8 +1115,13 @@ const void* mixed_pick_r(int r, bool res, bool skip) {
 }
 
 // LDS budget for a resident launch: the stripes' plan offsets plus every
-// plan (dynamic LDS up to 64 KiB needs no launch attribute)
-constexpr uint64_t kResidentMax = 64u << 10;
+// plan.  gfx950 has 160 KiB of LDS per CU and the mixed kernel's static LDS
+// is under 2 KiB; dynamic LDS past 64 KiB needs the function attribute
+// (hipFuncAttributeMaxDynamicSharedMemorySize), set at launch.  At 64 KiB,
+// RS(10,4) x 256 stripes with random 1..4 data losses (144 plans, 149 KB)
+// ran non-resident: per-stripe restaging and stripe-major tiles.
+constexpr uint64_t kResidentMax = 156u << 10;
+constexpr uint64_t kDynNoAttr = 64u << 10;
 
 }  // namespace
 
@@ -1077,19 +1130,28 @@ int launch_decode_mixed(const MixedArgs& in, int rows, int device, hipStream_t s
     const Tune tn = tune_snapshot();
     if (a.cell_len % 16 != 0 || a.cell_len / 16 > 0xFFFFFFFFull) return -1;
     const uint64_t dyn = ((a.stripes * 4 + 15) & ~uint64_t(15)) + a.blob_bytes;
-    const bool res = dyn <= kResidentMax && a.blob_bytes % 4 == 0;
+    bool res = dyn <= kResidentMax && a.blob_bytes % 4 == 0;
     // rows past a stripe's e skipped behind a scalar branch for k <= 6 (RS(6,3)
     // mixed +1.7 %), computed and dropped at the store for k = 10 (skipping
     // costs 3.5-4 % there); same-box A/B profiles/r02_ab_mixed_skip.txt.
     // Tune key 20: 1 = compute every row, 2 = skip.
     const bool skip = tn.mixed_skip == 2 || (tn.mixed_skip == 0 && a.k <= 6);
-    const void* fn = nullptr;
-    switch (a.k) {
-        case 2: fn = mixed_pick_r<2>(rows, res, skip); break;
-        case 3: fn = mixed_pick_r<3>(rows, res, skip); break;
-        case 6: fn = mixed_pick_r<6>(rows, res, skip); break;
-        case 10: fn = mixed_pick_r<10>(rows, res, skip); break;
-        default: return -1;
+    auto pick = [&](bool resident) -> const void* {
+        switch (a.k) {
+            case 2: return mixed_pick_r<2>(rows, resident, skip);
+            case 3: return mixed_pick_r<3>(rows, resident, skip);
+            case 6: return mixed_pick_r<6>(rows, resident, skip);
+            case 10: return mixed_pick_r<10>(rows, resident, skip);
+            default: return nullptr;
+        }
+    };
+    const void* fn = pick(res);
+    if (!fn) return -1;
+    if (res && dyn > kDynNoAttr &&
+        hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(dyn)) != hipSuccess) {
+        (void)hipGetLastError();
+        res = false;  // the runtime refused the LDS: restage per stripe instead
+        fn = pick(false);
     }
     const int U = a.k > 6 ? 2 : 4, BS = a.k > 6 ? 512 : 256;
     // K > 6: a grid of 8 per CU (one resident): RS(10,4) mixed decode 3216-3234

@@ -45,7 +45,7 @@ struct Tune {
     int mixed_skip = 0;         // key 20: mixed decode rows past a stripe's e: 0 default (skip for k <= 6), 1 compute all, 2 skip
     int fused_split = 0;        // key 21: fused kernels' wave roles: 0 default = 1 = every wave alternates (2 / 3 role-split)
     int fused_bsl = 0;          // key 22: fused encode parity: 0 default = bit-sliced for the RS matrix, 1 = v_perm tables
-    int matmul_bsl = 0;         // key 23: register encode kernel: 0 default = bit-sliced for the RS matrix, 1 = v_perm tables
+    int matmul_bsl = 0;         // key 23: register / LDS-DMA encode: 0 default = v_perm tables, 1 = bit-sliced RS parity (rejected)
 };
 
 #ifdef HEC_EXPERIMENTAL

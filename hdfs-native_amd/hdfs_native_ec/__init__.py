@@ -163,6 +163,8 @@ def _load(path: str = LIB_PATH) -> ctypes.CDLL:
     if hasattr(lib, "hec_tune_set"):  # the measurement build only (include/hdfs_ec_amd_exp.h)
         sig["hec_tune_set"] = ([I, I], I)
     for name, (args, res) in sig.items():
+        if os.environ.get("HEC_LIB_PATH") and not hasattr(lib, name):
+            continue  # an older build loaded for a same-box A/B: entry points it predates stay unbound
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = res

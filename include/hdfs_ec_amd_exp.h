@@ -54,9 +54,10 @@
  *         with the CRC waves at raised priority
  * key 22: fused encode + CRC parity: 0 = default (bit-sliced XOR network of
  *         the RS matrix for RS(3,2), RS(6,3), RS(10,4)), 1 = v_perm tables
- * key 23: register encode kernel (1 MiB-class cells): 0 = default
- *         (gf_encode_bsl: bit-sliced XOR network of the RS matrix for
- *         RS(3,2), RS(6,3), RS(10,4)), 1 = v_perm tables (gf_matmul_v16)
+ * key 23: register / LDS-DMA encode kernels: 0 = default (v_perm tables),
+ *         1 = bit-sliced XOR network of the RS matrix (gf_encode_bsl, and
+ *         gf_matmul_dma's BSL form; RS(3,2), RS(6,3), RS(10,4); measured
+ *         slower at RS(6,3) 1 MiB, not kept)
  * Returns HEC_OK, or HEC_ERR_INVALID_ARG for an unknown key / value.
  */
 #ifndef HDFS_EC_AMD_EXP_H

@@ -231,6 +231,17 @@ def test_eight_chunks_per_lane_small_k(xlib, dev, c_oracle, knob, k, m, cell):
 
 
 @pytest.mark.parametrize("pipeline", [1, 2])
+@pytest.mark.parametrize("grid", [0, 1, 5])
+@pytest.mark.parametrize("k,m", [(2, 1), (3, 2), (6, 3), (10, 4)])
+@pytest.mark.parametrize("cell", [8192 + 16, 3 * 65536 + 48])
+def test_bitsliced_encode_kernels(xlib, dev, c_oracle, pipeline, grid, k, m, cell):
+    # tune key 23 = 1: the RS parity rows as bit-sliced XOR networks in the
+    # register kernel (gf_encode_bsl, pipeline 1) and the LDS-DMA kernel
+    # (pipeline 2); RS(2,1) keeps the tables; partial last tiles, small grids
+    run_variant(xlib, c_oracle, dev, k, m, 3, cell, [(23, 1), (5, pipeline), (7, grid)], cell + 3 * k + grid)
+
+
+@pytest.mark.parametrize("pipeline", [1, 2])
 @pytest.mark.parametrize("k,m", [(2, 1), (3, 2), (6, 3), (10, 4)])
 @pytest.mark.parametrize("cell", [4096, 4096 + 16, 3 * 65536 + 48])
 @pytest.mark.parametrize("S", [3, 6])
@@ -288,7 +299,7 @@ def test_tune_set_concurrent_with_launches(xlib, dev, c_oracle):
 
 
 def test_tune_set_rejects_unknown_values(xlib):
-    for key, value in [(3, 99), (1, 5), (5, 6), (11, 8), (16, 1), (17, 6), (19, 3), (20, 3), (21, 4), (22, 2), (23, 0), (0, 0)]:
+    for key, value in [(3, 99), (1, 5), (5, 6), (11, 8), (16, 1), (17, 6), (19, 3), (20, 3), (21, 4), (22, 2), (23, 2), (24, 0), (0, 0)]:
         with pytest.raises(ValueError):
             H.tune_set(key, value, xlib)
 
