@@ -80,7 +80,7 @@ def parse(argv=None):
     ap.add_argument("--crc", action="store_true",
                     help="also time encode + CRC32C per 512-B chunk of all k+m cells (hec_encode_crc_device)")
     ap.add_argument("--corrupt", default="0.01,0.1",
-                    help="with --crc: fractions of stripes with one corrupt survivor for the verified read")
+                    help="with --crc: fractions of stripes with one corrupt survivor for the verified read (none = skip)")
     ap.add_argument("--ref-cases", action="store_true",
                     help="mirror rust/benches/ec.rs instead of the headline step (one JSON line)")
     ap.add_argument("--backend", default="nccl", help="process-group backend (nccl = RCCL; gloo for rehearsals)")
@@ -977,7 +977,7 @@ def crc_leg(args, H, coder, data, parity, rec, dp, ds, pp, ps, rp, rs, shard_ptr
     torch.cuda.synchronize(dev)
     corrupt["0"] = {"stripes_corrupt": 0, "ms": round((time.perf_counter() - t_0) / reps * 1e3, 3)}
     corrupt["0"]["GiBps"] = round(k * cell * S / (corrupt["0"]["ms"] * 1e-3) / GIB, 2)
-    for frac in [float(x) for x in filter(None, args.corrupt.split(","))]:
+    for frac in [float(x) for x in args.corrupt.split(",") if x and x.lower() != "none"]:
         n_bad = max(1, int(round(frac * S)))
         idx = torch.linspace(0, S - 1, n_bad, device=dev).long().unique()
         orig = data[idx, 1, 7].clone()

@@ -234,6 +234,11 @@ const void* crc_pick(int scheme, int pf) {
     // bank-replicated slicing-by-2, 4 chains: 5.14 vs 5.37 TB/s
     // (profiles/r02_probe_crc_rep2.log)
     if (scheme == 22) return crc_fn<KIND, 22>(pf);
+    // fold depth 16 / 20 dwords (CRC32C; the MSB-first kind has no fold)
+    if (scheme == 13 || scheme == 14) {
+        if constexpr (KIND == crc::kCrc32c) return scheme == 13 ? crc_fn<KIND, 13>(pf) : crc_fn<KIND, 14>(pf);
+        return crc_fn<KIND, 12>(pf);
+    }
 #endif
 #ifndef HEC_EXPERIMENTAL
     // product: the fold (CRC32C, one task of prefetch) / 11-bit slicing inside
@@ -286,7 +291,9 @@ int launch_checksum(const CrcArgs& in, int device, hipStream_t stream) {
         // prefetch: same box, 9 x 1 MiB x 1024, 1.598 ms (6.05 TB/s) vs 1.804
         // (5.36) for 11-bit slicing at its best prefetch
         // (profiles/r02k_fold/probe_crc.log); 11-bit slicing on key 11 = 5
-        const int scheme = tn.crc_variant == 1   ? 1
+        const int scheme = tn.crc_variant == 10  ? 13
+                           : tn.crc_variant == 11 ? 14
+                           : tn.crc_variant == 1   ? 1
                            : tn.crc_variant == 2 ? 4
                            : tn.crc_variant == 3 ? 8
                            : tn.crc_variant == 4 ? 16

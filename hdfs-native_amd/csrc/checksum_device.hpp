@@ -95,8 +95,12 @@ struct Fold {
     static constexpr int q[kN] = {6, 6, 5, 4, 2}, s[kN] = {17, 3, 10, 27, 1};  // offset = 32q + s
 };
 
-template <bool REFL>
+// FD = folded dwords (24: default, 256-bit tail; 16 / 20: measurement
+// schemes 13 / 14, fewer v_alignbit, a 512- / 384-bit tail of lookups).  Any
+// FD <= 25 is valid: a bit is folded only at degree >= 1024 - 32 FD >= 224 > 209.
+template <bool REFL, int FD = Fold::kDwords>
 __device__ __forceinline__ uint32_t quarter_fold(const uint32_t* t, const uint8_t* row) {
+    static_assert(FD % 2 == 0 && FD >= 2 && FD <= 24, "even fold depth, 256-bit tail at least");
     if constexpr (!REFL) {
         return quarter_w11<REFL>(t, row);
     } else {
@@ -116,7 +120,7 @@ __device__ __forceinline__ uint32_t quarter_fold(const uint32_t* t, const uint8_
 #pragma unroll
             for (int o = 0; o < Fold::kN; o++) {
                 const int hi = i - Fold::q[o], lo = hi - 1;
-                const bool h = hi >= 0 && hi < Fold::kDwords, l = lo >= 0 && lo < Fold::kDwords;
+                const bool h = hi >= 0 && hi < FD, l = lo >= 0 && lo < FD;
                 if (!h && !l) continue;
                 const uint32_t c = h && l ? __builtin_amdgcn_alignbit(w[hi], w[lo], 32 - Fold::s[o])
                                    : h    ? w[hi] << Fold::s[o]
@@ -133,7 +137,7 @@ __device__ __forceinline__ uint32_t quarter_fold(const uint32_t* t, const uint8_
         }
         uint32_t r = 0;
 #pragma unroll
-        for (int i = Fold::kDwords; i < 32; i += 2) r = step8_w11<REFL>(t, r, w[i], w[i + 1]);
+        for (int i = FD; i < 32; i += 2) r = step8_w11<REFL>(t, r, w[i], w[i + 1]);
         return r;
     }
 }
@@ -244,7 +248,8 @@ __device__ __forceinline__ uint32_t apply_shift_nib(const uint32_t (*t)[16], uin
 // 1024-thread blocks (4 waves per SIMD) with nibble shift tables so the
 // tables (9.5 KiB) and 16 wave images (144 KiB) fit one CU's LDS; 4 / 8 =
 // bank-replicated slicing-by-1; 0 = memory side only.
-constexpr bool w11(int scheme) { return scheme == 11 || scheme == 12; }  // 11-bit field tables
+// 11-bit field tables: 11-bit slicing, the fold (12) and its depth variants (13, 14)
+constexpr bool w11(int scheme) { return scheme >= 11 && scheme <= 14; }
 constexpr bool sliced(int scheme) { return scheme <= 1 || scheme == 16 || w11(scheme); }
 constexpr bool nib_shift(int scheme) { return scheme == 16 || w11(scheme); }
 
@@ -320,6 +325,10 @@ __device__ __forceinline__ uint32_t quarter(const uint32_t* s, const uint8_t* ro
         return quarter_w11<REFL>(s, row);
     else if constexpr (SCHEME == 12)
         return quarter_fold<REFL>(s, row);
+    else if constexpr (SCHEME == 13)
+        return quarter_fold<REFL, 16>(s, row);
+    else if constexpr (SCHEME == 14)
+        return quarter_fold<REFL, 20>(s, row);
     else if constexpr (sliced(SCHEME))
         return quarter_s8<REFL>(reinterpret_cast<const uint32_t(*)[256]>(s), row);
     else

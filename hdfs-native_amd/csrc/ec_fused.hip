@@ -674,6 +674,13 @@ const void* encode_fn(int slabs, int scheme, int wpe, bool pair, bool bsl) {
     // bit-sliced parity at the default slab count (tune key 22 = 1: off)
     if (bsl && scheme == 12 && wpe != 3 && slabs == fused_slabs(K, R) && (slabs == 8 || pair))
         return encode_bsl<K, R, 12, fused_slabs(K, R) == 4>(true);
+    // fold depth 16 / 20 dwords (key 11 = 10 / 11), RS(6,3) and RS(10,4) only
+    if constexpr ((K == 6 && R == 3) || (K == 10 && R == 4)) {
+        if ((scheme == 13 || scheme == 14) && bsl && wpe != 3 && slabs == fused_slabs(K, R) && (slabs == 8 || pair))
+            return scheme == 13 ? encode_bsl<K, R, 13, fused_slabs(K, R) == 4>(true)
+                                : encode_bsl<K, R, 14, fused_slabs(K, R) == 4>(true);
+    }
+    if (scheme == 13 || scheme == 14) return nullptr;
     // rejected (same-box A/B, profiles/r01_probe_fused_scheme.log,
     // r02_probe_fused_rep2.log, r02_probe_fused_wpe3_*.log):
     // bank-replicated slicing-by-1 (4 chains) and slicing-by-2 (tune key 11
@@ -698,6 +705,14 @@ const void* verify_fn(int kind, int scheme, int wpe, bool pair) {
                : reinterpret_cast<const void*>(&gf_fused_crc<K, R, SL, 12, crc::kCksum, true, 2, SL == 4>);
 #else
     if (scheme == 22) return verify_kind<K, R, 22>(kind);
+    if constexpr ((K == 6 && R == 3) || (K == 10 && R == 4)) {
+        constexpr int SL = fused_slabs(K, R);
+        if ((scheme == 13 || scheme == 14) && wpe != 3 && kind == crc::kCrc32c)
+            return scheme == 13
+                       ? reinterpret_cast<const void*>(&gf_fused_crc<K, R, SL, 13, crc::kCrc32c, true, 2, SL == 4>)
+                       : reinterpret_cast<const void*>(&gf_fused_crc<K, R, SL, 14, crc::kCrc32c, true, 2, SL == 4>);
+    }
+    if (scheme == 13 || scheme == 14) return nullptr;
     if (wpe == 3) return scheme == 11 ? verify_kind<K, R, 11, 3>(kind) : verify_kind<K, R, 1, 3>(kind);
     if (scheme == 12) return verify_kind<K, R, 12>(kind, pair);
     return scheme == 11 ? verify_kind<K, R, 11>(kind, pair) : verify_kind<K, R, 1>(kind, pair);
@@ -764,7 +779,10 @@ int launch_fused(const MatmulArgs& in, const FusedCrcArgs& cs, bool verify, int 
     // RS(6,3) x 1024 (profiles/r02k_fold/crc63_v*.json): encode + CRC 2.18-2.21
     // -> 1.96-1.97 ms (4.38-4.43 -> 4.90-4.94 TB/s), decode + verify 1.96-1.99
     // -> 1.82 ms.  11-bit slicing on key 11 = 5.
-    const int scheme = (!verify && tn.crc_variant == 2) ? 4
+    // measurement: fold depth 16 / 20 dwords (key 11 = 10 / 11)
+    const int scheme = tn.crc_variant == 10             ? 13
+                       : tn.crc_variant == 11           ? 14
+                       : (!verify && tn.crc_variant == 2) ? 4
                        : tn.crc_variant == 6            ? 22
                        : tn.crc_variant == 1            ? 1
                        : tn.crc_variant == 5            ? 11
@@ -804,6 +822,7 @@ int launch_fused(const MatmulArgs& in, const FusedCrcArgs& cs, bool verify, int 
             case 10: fn = pick_r<10>(verify, a.r, slabs, scheme, cs.kind, wpe, pair, bsl); break;
             default: return -1;
         }
+        if (!fn) return -1;  // a measurement scheme not compiled for this shape
     }
     if (!aligned) return -1;
     const uint64_t chunks = a.cell_len / 16;

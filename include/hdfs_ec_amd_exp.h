@@ -30,7 +30,9 @@
  *         11-bit slicing everywhere, 2 / 3 = bank-replicated slice-by-1 with
  *         4 / 8 chains, 4 = slice-by-8 at 4 waves per SIMD (checksum
  *         kernel), 6 = bank-replicated slice-by-2, 9 = memory side only
- *         (WRONG sums)
+ *         (WRONG sums), 10 / 11 = the fold over 16 / 20 of the quarter's 32
+ *         dwords (512- / 384-bit tail of lookups; CRC32C, RS(6,3) and
+ *         RS(10,4) in the fused kernels)
  * key 12: CRC register prefetch depth in 8-KiB tasks: 0 = default (1 for the
  *         CRC32C fold, else 2), 1 or 2
  * key 13: store cache policy of the pipe kernel (0 = nt, 1 = sc1, 2 = sc0 sc1,

@@ -70,28 +70,29 @@ struct Check {
         return v;
     }
     // scheme 12: the kernel's fold, the same offsets (32q + s) and order
-    uint32_t q_fold(const uint8_t* q) const {
+    // (fd = folded dwords: 24 for scheme 12, 16 / 20 for the measurement schemes 13 / 14)
+    uint32_t q_fold(const uint8_t* q, int fd = 24) const {
         static const int kq[5] = {6, 6, 5, 4, 2}, ks[5] = {17, 3, 10, 27, 1};
         uint32_t w[32];
         for (int i = 0; i < 32; i++) w[i] = le32(q + 4 * i);
         for (int i = 2; i < 32; i++)
             for (int o = 0; o < 5; o++) {
                 const int hi = i - kq[o], lo = hi - 1;
-                const uint32_t h = hi >= 0 && hi < 24 ? w[hi] : 0, l = lo >= 0 && lo < 24 ? w[lo] : 0;
+                const uint32_t h = hi >= 0 && hi < fd ? w[hi] : 0, l = lo >= 0 && lo < fd ? w[lo] : 0;
                 w[i] ^= (h << ks[o]) | (l >> (32 - ks[o]));
             }
         uint32_t r = 0;
-        for (int i = 24; i < 32; i += 2) {
+        for (int i = fd; i < 32; i += 2) {
             const uint32_t lo = w[i] ^ pre(r), hi = w[i + 1];
             r = t.w11[0][f0(lo)] ^ t.w11[1][f1(lo)] ^ t.w11[2][f2(lo)] ^ t.w11[3][f0(hi)] ^ t.w11[4][f1(hi)] ^
                 t.w11[5][f2(hi)];
         }
         return r;
     }
-    uint32_t chunk(const uint8_t* c, bool w11, bool fold = false) const {
+    uint32_t chunk(const uint8_t* c, bool w11, bool fold = false, int fd = 24) const {
         uint32_t v = 0;
         for (int qi = 0; qi < 4; qi++) {
-            const uint32_t r = fold ? q_fold(c + 128 * qi) : w11 ? q_w11(c + 128 * qi) : q_s8(c + 128 * qi);
+            const uint32_t r = fold ? q_fold(c + 128 * qi, fd) : w11 ? q_w11(c + 128 * qi) : q_s8(c + 128 * qi);
             v ^= qi < 3 ? (w11 ? shift_nib(qi, r) : shift_byte(qi, r)) : r;
         }
         return v ^ t.final512;
@@ -121,9 +122,9 @@ int main(int argc, char** argv) {
     Check<kCksum> cck(kTck);
     for (int k = 0; k < chunks; k++) {
         const uint8_t* c = data.data() + 512 * k;
-        std::printf("%08x %08x %08x %08x %08x %08x %08x\n", c32c.chunk(c, false), c32c.chunk(c, true),
+        std::printf("%08x %08x %08x %08x %08x %08x %08x %08x %08x\n", c32c.chunk(c, false), c32c.chunk(c, true),
                     c32c.chunk_bytes(c), cck.chunk(c, false), cck.chunk(c, true), cck.chunk_bytes(c),
-                    c32c.chunk(c, true, true));
+                    c32c.chunk(c, true, true), c32c.chunk(c, true, true, 16), c32c.chunk(c, true, true, 20));
     }
     std::fflush(stdout);
     // the data itself, for the oracle side

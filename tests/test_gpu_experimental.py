@@ -323,9 +323,10 @@ def test_mixed_many_plans_skipped_rows(xlib, dev):
 
 
 @pytest.mark.parametrize("cell,bpc,n", P.CRC32C_CASES)
-@pytest.mark.parametrize("variant,pf", [(0, 2), (1, 1), (1, 2), (5, 0), (5, 1), (5, 2), (7, 1)])
+@pytest.mark.parametrize("variant,pf", [(0, 2), (1, 1), (1, 2), (5, 0), (5, 1), (5, 2), (7, 1), (10, 1), (11, 1)])
 def test_crc32c_lookup_schemes(xlib, dev, cell, bpc, n, variant, pf):
-    # tune key 11: slicing-by-8 (1), 11-bit slicing (5), the fold (0 / 7); key 12: prefetch
+    # tune key 11: slicing-by-8 (1), 11-bit slicing (5), the fold (0 / 7), fold depth 16 / 20
+    # (10 / 11); key 12: prefetch
     P.crc32c_body(dev, cell, bpc, n, P.coder(6, 3, xlib), [(11, variant), (12, pf)], xlib)
 
 
@@ -337,7 +338,7 @@ def test_checksum_lookup_schemes(xlib, dev, ctype, cell, bpc, n, variant):
 
 
 @pytest.mark.parametrize("case", P.ENCODE_CRC_CASES)
-@pytest.mark.parametrize("fused,scheme", [(4, 0), (8, 0), (None, 0), (0, 1), (0, 5), (4, 5), (8, 1)])
+@pytest.mark.parametrize("fused,scheme", [(4, 0), (8, 0), (None, 0), (0, 1), (0, 5), (4, 5), (8, 1), (0, 10), (0, 11)])
 def test_encode_crc_knobs(xlib, dev, c_oracle, case, fused, scheme):
     # key 9 = 1: two passes; key 10: slabs per wave; key 11: lookup scheme
     pairs = [(9, 1 if fused is None else 0), (10, fused or 0), (11, scheme)]
@@ -382,6 +383,6 @@ def test_fused_input_pairing(xlib, dev, c_oracle, k, m, cell, S, slabs, pair):
 
 @pytest.mark.parametrize("ctype", P.CKSUM_TYPES)
 @pytest.mark.parametrize("case", P.VERIFY_CASES)
-@pytest.mark.parametrize("scheme", [1, 5])
+@pytest.mark.parametrize("scheme", [1, 5, 10, 11])
 def test_decode_verify_lookup_schemes(xlib, dev, c_oracle, ctype, case, scheme):
     P.decode_verify_body(dev, c_oracle, ctype, *case, P.coder(case[0], case[1], xlib), [(11, scheme)], xlib)

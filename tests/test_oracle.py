@@ -306,13 +306,14 @@ def test_device_crc_tables_vs_oracle(tmp_path):
     data = res.stderr
     assert len(data) == 512 * chunks
     lines = res.stdout.decode().split()
-    assert len(lines) == 7 * chunks
+    assert len(lines) == 9 * chunks
     for i in range(chunks):
         c = data[512 * i:512 * (i + 1)]
         want32c = O.chunk_checksums(c, 512, O.CHECKSUM_CRC32C).hex()
         want32 = O.chunk_checksums(c, 512, O.CHECKSUM_CRC32).hex()
-        row = lines[7 * i:7 * i + 7]
-        assert row[0:3] + row[6:7] == [want32c] * 4, i  # s8, w11, byte, fold (scheme 12)
+        row = lines[9 * i:9 * i + 9]
+        # s8, w11, byte, fold 24 (scheme 12), fold 16 / 20 (measurement schemes 13 / 14)
+        assert row[0:3] + row[6:9] == [want32c] * 6, i
         assert row[3:6] == [want32] * 3, i
 
 
