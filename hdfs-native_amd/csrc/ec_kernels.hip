@@ -1090,8 +1090,7 @@ const void* mixed_fn() {
 }
 
 // The product library compiles the default row policy only (rows past a
-// stripe's e skipped for k <= 6, computed and dropped above); the
-// measurement build both (tune key 20).
+// stripe's e skipped); the measurement build both (tune key 20).
 template <int K, int R>
 const void* mixed_sel(bool res, bool skip) {
 #ifdef HEC_EXPERIMENTAL
@@ -1099,8 +1098,7 @@ const void* mixed_sel(bool res, bool skip) {
                : (skip ? mixed_fn<K, R, false, true>() : mixed_fn<K, R, false, false>());
 #else
     (void)skip;
-    constexpr bool SKIP = K <= 6;
-    return res ? mixed_fn<K, R, true, SKIP>() : mixed_fn<K, R, false, SKIP>();
+    return res ? mixed_fn<K, R, true, true>() : mixed_fn<K, R, false, true>();
 #endif
 }
 
@@ -1131,11 +1129,13 @@ int launch_decode_mixed(const MixedArgs& in, int rows, int device, hipStream_t s
     if (a.cell_len % 16 != 0 || a.cell_len / 16 > 0xFFFFFFFFull) return -1;
     const uint64_t dyn = ((a.stripes * 4 + 15) & ~uint64_t(15)) + a.blob_bytes;
     bool res = dyn <= kResidentMax && a.blob_bytes % 4 == 0;
-    // rows past a stripe's e skipped behind a scalar branch for k <= 6 (RS(6,3)
-    // mixed +1.7 %), computed and dropped at the store for k = 10 (skipping
-    // costs 3.5-4 % there); same-box A/B profiles/r02_ab_mixed_skip.txt.
-    // Tune key 20: 1 = compute every row, 2 = skip.
-    const bool skip = tn.mixed_skip == 2 || (tn.mixed_skip == 0 && a.k <= 6);
+    // rows past a stripe's e skipped behind a scalar branch: RS(6,3) mixed
+    // +1.7 % (profiles/r02_ab_mixed_skip.txt); RS(10,4) x 256 decode +9.5 %
+    // since the tile metadata moved to three LDS round trips and global loads
+    // (same box, profiles/r03g/mx10: 4049-4074 vs 3683-3726 GiB/s; in round 2,
+    // with the serial metadata and flat loads, skipping lost 3.5-4 % there).
+    // Tune key 20: 1 = compute every row (measurement), 0 / 2 = skip.
+    const bool skip = tn.mixed_skip != 1;
     auto pick = [&](bool resident) -> const void* {
         switch (a.k) {
             case 2: return mixed_pick_r<2>(rows, resident, skip);

@@ -42,7 +42,7 @@ struct Tune {
     int call_piece_kib = 0;     // key 17: per-call drop-in pipeline piece, KiB per shard (0 = 256)
     int unaligned = 0;          // key 18: unaligned layouts: 0 default = dword kernel + byte tail, 1 = byte kernel only
     int fused_pair = 0;         // key 19: fused kernels at 4 slabs: 0 default / 2 = inputs two at a time, 1 = one at a time
-    int mixed_skip = 0;         // key 20: mixed decode rows past a stripe's e: 0 default (skip for k <= 6), 1 compute all, 2 skip
+    int mixed_skip = 0;         // key 20: mixed decode rows past a stripe's e: 0 default = 2 = skip, 1 compute all
     int fused_split = 0;        // key 21: fused kernels' wave roles: 0 default = 1 = every wave alternates (2 / 3 role-split)
     int fused_bsl = 0;          // key 22: fused encode parity: 0 default = bit-sliced for the RS matrix, 1 = v_perm tables
     int matmul_bsl = 0;         // key 23: register / LDS-DMA encode: 0 default = v_perm tables, 1 = bit-sliced RS parity (rejected)

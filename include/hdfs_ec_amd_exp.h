@@ -47,9 +47,8 @@
  *         1 = the byte kernel alone
  * key 19: fused kernels at 4 slabs per wave: 0 / 2 = inputs two at a time
  *         (default), 1 = one at a time
- * key 20: mixed-pattern decode, rows past a stripe's erasure count: 0 = default
- *         (skipped for k <= 6, computed and dropped for larger k), 1 = computed,
- *         2 = skipped
+ * key 20: mixed-pattern decode, rows past a stripe's erasure count: 0 / 2 =
+ *         skipped (default), 1 = computed and dropped at the store
  * key 21: fused kernels' wave roles: 0 / 1 = every wave alternates GF math
  *         and CRC rounds (default); 2 = role-split GF / CRC waves (one
  *         512-thread block per CU, RS(6,3) and RS(10,4) only), 3 = role-split

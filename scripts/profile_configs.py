@@ -43,6 +43,15 @@ KERNEL_RE = "gf_matmul"
 # kernel name, bytes per launch = the line's TB/s x ms for that leg
 CRC_CONFIGS = {"crc63": (["--crc", "--corrupt", ""], 6, 3, 1 << 20, 1024)}
 CRC_RE = "gf_fused_crc|checksum_chunks512"
+# mixed-pattern decode (bench.py --decode-mode mixed: a random 1..m data
+# shards lost per stripe): the gf_decode_mixed kernel alone, its algorithmic
+# bytes (k survivors read + the e_s rebuilt cells written per stripe) from the
+# bench line's roofline.decode_mixed
+MIXED_CONFIGS = {
+    "mx104": (["--k", "10", "--m", "4", "--stripes", "256", "--decode-mode", "mixed"], 10, 4, 1 << 20, 256),
+    "mx63": (["--decode-mode", "mixed"], 6, 3, 1 << 20, 1024),
+}
+MIXED_RE = "gf_decode_mixed"
 
 
 def fused_template_args(name):
@@ -233,6 +242,52 @@ def profile_crc(out, name):
               f"traffic x{res['traffic_over_algorithmic']}", flush=True)
 
 
+def profile_mixed(out, name):
+    args, k, m, cell, stripes = MIXED_CONFIGS[name]
+    d = os.path.join(out, name)
+    os.makedirs(d, exist_ok=True)
+    bench = ["python3", "bench.py"] + args + COMMON
+    prof = ["rocprofv3", "--kernel-trace", "--stats", "-d", os.path.join(d, "trace"), "-o", "run",
+            "--output-format", "csv", "--"]
+    run(prof + bench, os.path.join(d, "bench_trace.log"), 400)
+    line = bench_line(os.path.join(d, "bench_trace.log"))
+    dm = line["roofline"]["decode_mixed"]
+    for cnt in ("FETCH_SIZE", "WRITE_SIZE"):
+        pmc = ["rocprofv3", "--pmc", cnt, "--kernel-include-regex", MIXED_RE, "-d",
+               os.path.join(d, cnt.lower()), "-o", "run", "--output-format", "csv", "--"]
+        run(pmc + bench, os.path.join(d, f"bench_{cnt.lower()}.log"), 400)
+    trace = sorted((r for r in rows(os.path.join(d, "trace"), "*kernel_trace.csv")
+                    if MIXED_RE in r.get("Kernel_Name", "")), key=lambda r: int(r["Start_Timestamp"]))
+    durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9 for r in trace]
+    timed = durs[-line["steps"]:]
+    avg = sum(timed) / len(timed)
+    algo = dm["algorithmic_bytes_per_launch"]
+    match = lambda n: MIXED_RE in n  # noqa: E731
+    fetch = counter(os.path.join(d, "fetch_size"), "FETCH_SIZE", match)
+    write = counter(os.path.join(d, "write_size"), "WRITE_SIZE", match)
+    fetch_b = 2.0 * 1024 * sum(fetch) / len(fetch)
+    write_b = 1024.0 * sum(write) / len(write)
+    res = {
+        "config": name, "args": " ".join(args + COMMON), "k": k, "m": m, "cell": cell, "stripes": stripes,
+        "erased_cells": dm["erased_cells"], "kernel": sorted({r["Kernel_Name"] for r in trace}),
+        "dispatches": len(durs), "avg_launch_ms_timed_region": round(avg * 1e3, 4),
+        "bench_decode_avg_launch_ms": dm["avg_launch_ms"],
+        "algorithmic_bytes_per_launch": algo, "frac_from_trace": round(algo / avg / PEAK, 4),
+        "frac_bench_line": dm["frac"], "frac_bench_line_encode_plus_decode": line["roofline"]["frac"],
+        "fetch_bytes_per_launch": fetch_b, "write_bytes_per_launch": write_b,
+        "hbm_bytes_per_launch": fetch_b + write_b,
+        "traffic_over_algorithmic": round((fetch_b + write_b) / algo, 5),
+        "pmc_dispatches": {"fetch": len(fetch), "write": len(write)},
+        "corrections": "FETCH_SIZE KiB x1024 x2 (gfx950 half-count on 16B/lane streaming reads); WRITE_SIZE KiB x1024",
+        "bench_line": line,
+    }
+    with open(os.path.join(out, "summary_mixed.jsonl"), "a") as f:
+        f.write(json.dumps(res) + "\n")
+    print(f"{name}: mixed decode kernel {avg * 1e3:.4f} ms (line {dm['avg_launch_ms']}) frac trace "
+          f"{res['frac_from_trace']} line {dm['frac']} (enc+dec {line['roofline']['frac']}) "
+          f"traffic x{res['traffic_over_algorithmic']}", flush=True)
+
+
 def write_traffic(out, tag):
     """pmc_traffic_configs.json: what bench.py reads for roofline.traffic
     (matched on k, m, cell, stripes and decode mode)."""
@@ -250,11 +305,11 @@ def write_traffic(out, tag):
 
 def main():
     out = sys.argv[1]
-    names = sys.argv[2:] or list(CONFIGS) + list(CRC_CONFIGS)
+    names = sys.argv[2:] or list(CONFIGS) + list(CRC_CONFIGS) + list(MIXED_CONFIGS)
     os.makedirs(out, exist_ok=True)
     os.environ["TMPDIR"] = "/tmp"
     for n in names:
-        (profile_crc if n in CRC_CONFIGS else profile)(out, n)
+        (profile_crc if n in CRC_CONFIGS else profile_mixed if n in MIXED_CONFIGS else profile)(out, n)
     write_traffic(out, os.path.basename(os.path.normpath(out)))
     print("profile_configs ok", flush=True)
 

@@ -396,9 +396,9 @@ def _random_masks(k, m, S, seed, allow_fail=False):
 @pytest.mark.parametrize("k,m,cell", [(6, 3, 4096), (6, 3, 65536 + 64), (10, 4, 8192), (3, 2, 4096 + 16),
                                       (2, 1, 1024), (4, 2, 4096), (6, 3, 1000)])
 def test_device_decode_mixed_patterns(dev, c_oracle, k, m, cell):
-    """Random per-stripe patterns (rows past a stripe's erasure count skipped
-    for k <= 6, computed and dropped above; the measurement build forces
-    either, tests/test_gpu_experimental.py)."""
+    """Random per-stripe patterns (rows past a stripe's erasure count skipped;
+    the measurement build also runs them computed and dropped,
+    tests/test_gpu_experimental.py)."""
     mixed_patterns_body(dev, c_oracle, k, m, cell, coder(k, m))
 
 
