@@ -475,8 +475,8 @@ def test_device_decode_mixed_many_plans(dev):
     mixed_many_plans_body(dev, coder(10, 4))
 
 
-def mixed_many_plans_body(dev, cod, knob_pairs=(), xlib=None):
-    k, m, S, cell = 10, 4, 512, 4096
+def mixed_many_plans_body(dev, cod, knob_pairs=(), xlib=None, S=512):
+    k, m, cell = 10, 4, 4096
     rng = np.random.default_rng(1234)
     data = rng.integers(0, 256, size=(S, k, cell), dtype=np.uint8)
     d = torch.from_numpy(data).to(dev)
@@ -503,6 +503,15 @@ def mixed_many_plans_body(dev, cod, knob_pairs=(), xlib=None):
                 assert bool((out[s, i] == 0x5A).all()), (s, i)
             else:
                 assert torch.equal(out[s, i], d[s, i]), (s, i, bin(mask))
+
+
+@pytest.mark.parametrize("S", [24, 160, 256])
+def test_device_decode_mixed_plans_resident(dev, S):
+    """RS(10,4) with random losses of any shards: a plan blob under 64 KiB of
+    LDS (S = 24), and past 64 KiB but within the 156 KiB the launcher keeps
+    resident with the dynamic-LDS attribute (S = 160, 256; 512 above restages
+    per stripe)."""
+    mixed_many_plans_body(dev, coder(10, 4), S=S)
 
 
 def test_device_decode_mixed_not_enough_shards_launches_nothing(dev):
