@@ -681,6 +681,12 @@ const void* encode_fn(int slabs, int scheme, int wpe, bool pair, bool bsl) {
                                 : encode_bsl<K, R, 14, fused_slabs(K, R) == 4>(true);
     }
     if (scheme == 13 || scheme == 14) return nullptr;
+    // bit-sliced parity at 4 slabs in one 768-thread block per CU (3 waves per
+    // SIMD; tune key 16 = 3), RS(6,3) and RS(10,4)
+    if constexpr ((K == 6 && R == 3) || (K == 10 && R == 4)) {
+        if (bsl && scheme == 12 && wpe == 3)
+            return reinterpret_cast<const void*>(&gf_fused_crc<K, R, 4, 12, crc::kCrc32c, false, 3, false, true>);
+    }
     // rejected (same-box A/B, profiles/r01_probe_fused_scheme.log,
     // r02_probe_fused_rep2.log, r02_probe_fused_wpe3_*.log):
     // bank-replicated slicing-by-1 (4 chains) and slicing-by-2 (tune key 11
