@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #define CK(x)                                                                                      \
@@ -58,13 +59,16 @@ __global__ __launch_bounds__(BS) void skel(const uint8_t* __restrict__ in, uint8
     }
 }
 
+static bool g_contig = false;  // PROBE_CONTIG=1: physically contiguous allocations
+
 template <int K, int R>
 void run(int cus, size_t cell, uint32_t stripes) {
     constexpr int U = 4, BS = 256;
     const uint32_t chunks = uint32_t(cell / 16), tps = chunks / (BS * U), total = tps * stripes;
     uint8_t *in, *out;
-    CK(hipMalloc(&in, size_t(stripes) * K * cell));
-    CK(hipMalloc(&out, size_t(stripes) * R * cell));
+    const unsigned fl = g_contig ? hipDeviceMallocContiguous : hipDeviceMallocDefault;
+    CK(hipExtMallocWithFlags(reinterpret_cast<void**>(&in), size_t(stripes) * K * cell, fl));
+    CK(hipExtMallocWithFlags(reinterpret_cast<void**>(&out), size_t(stripes) * R * cell, fl));
     CK(hipMemset(in, 1, size_t(stripes) * K * cell));
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
@@ -93,6 +97,14 @@ int main() {
     hipDeviceProp_t p;
     CK(hipGetDeviceProperties(&p, 0));
     const int cus = p.multiProcessorCount;
+    const char* mode = std::getenv("PROBE_MODE");
+    g_contig = std::getenv("PROBE_CONTIG") && std::atoi(std::getenv("PROBE_CONTIG")) == 1;
+    if (mode && std::string(mode) == "footprint") {
+        // RS(10,4) at growing stripe counts (footprint 3.5 .. 28 GiB), warmed up first
+        run<10, 4>(cus, 1 << 20, 256);
+        for (uint32_t s : {256u, 512u, 1024u, 2048u, 256u}) run<10, 4>(cus, 1 << 20, s);
+        return 0;
+    }
     run<1, 1>(cus, 1 << 20, 4096);
     run<3, 2>(cus, 1 << 20, 1024);
     run<6, 3>(cus, 1 << 20, 1024);
