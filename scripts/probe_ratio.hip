@@ -27,7 +27,17 @@
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-template <int K, int R, int U, int BS>
+// e of a stripe in the mixed mode: 1 + (hash % R), as a per-stripe random
+// erasure count of 1..R (stores of rows past e skipped, as gf_decode_mixed)
+__host__ __device__ inline uint32_t stripe_e(uint32_t s, int R) {
+    uint32_t h = s * 0x9E3779B1u;
+    h ^= h >> 15;
+    h *= 0x85EBCA77u;
+    h ^= h >> 13;
+    return 1u + h % uint32_t(R);
+}
+
+template <int K, int R, int U, int BS, bool MIXED = false>
 __global__ __launch_bounds__(BS) void skel(const uint8_t* __restrict__ in, uint8_t* __restrict__ out, uint32_t chunks,
                                            uint32_t tps, uint32_t total, uint32_t group) {
     constexpr uint32_t TILE = BS * U;
@@ -37,6 +47,7 @@ __global__ __launch_bounds__(BS) void skel(const uint8_t* __restrict__ in, uint8
         const uint32_t tcol = r / group, stripe = g * group + (r - tcol * group);
         const uint8_t* ib = in + uint64_t(stripe) * K * cell;
         uint8_t* ob = out + uint64_t(stripe) * R * cell;
+        const int e = MIXED ? int(__builtin_amdgcn_readfirstlane(int(stripe_e(stripe, R)))) : R;
         u32x4 x[U][K];
 #pragma unroll
         for (int u = 0; u < U; u++)
@@ -51,9 +62,11 @@ __global__ __launch_bounds__(BS) void skel(const uint8_t* __restrict__ in, uint8
 #pragma unroll
             for (int i = 1; i < K; i++) acc ^= x[u][i];
 #pragma unroll
-            for (int j = 0; j < R; j++)
+            for (int j = 0; j < R; j++) {
+                if (MIXED && j >= e) break;
                 __builtin_nontemporal_store(acc + u32x4{uint32_t(j), 0, 0, 0}, reinterpret_cast<u32x4*>(
                                                 ob + j * cell + uint64_t(tcol * TILE + u * BS + threadIdx.x) * 16));
+            }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -61,7 +74,7 @@ __global__ __launch_bounds__(BS) void skel(const uint8_t* __restrict__ in, uint8
 
 static bool g_contig = false;  // PROBE_CONTIG=1: physically contiguous allocations
 
-template <int K, int R>
+template <int K, int R, bool MIXED = false>
 void run(int cus, size_t cell, uint32_t stripes) {
     constexpr int U = 4, BS = 256;
     const uint32_t chunks = uint32_t(cell / 16), tps = chunks / (BS * U), total = tps * stripes;
@@ -73,12 +86,12 @@ void run(int cus, size_t cell, uint32_t stripes) {
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
-    for (int w = 0; w < 20; w++) skel<K, R, U, BS><<<cus, BS>>>(in, out, chunks, tps, total, 4);
+    for (int w = 0; w < 20; w++) skel<K, R, U, BS, MIXED><<<cus, BS>>>(in, out, chunks, tps, total, 4);
     CK(hipDeviceSynchronize());
     std::vector<float> ms;
     for (int rep = 0; rep < 3; rep++) {
         CK(hipEventRecord(a));
-        for (int it = 0; it < 20; it++) skel<K, R, U, BS><<<cus, BS>>>(in, out, chunks, tps, total, 4);
+        for (int it = 0; it < 20; it++) skel<K, R, U, BS, MIXED><<<cus, BS>>>(in, out, chunks, tps, total, 4);
         CK(hipEventRecord(b));
         CK(hipEventSynchronize(b));
         float t;
@@ -86,9 +99,13 @@ void run(int cus, size_t cell, uint32_t stripes) {
         ms.push_back(t / 20);
     }
     const float best = *std::min_element(ms.begin(), ms.end());
-    const double bytes = double(K + R) * cell * stripes;
-    std::printf("skeleton RS(%d,%d) %zu KiB x %u: %.4f ms/launch (best of 3 x 20) %.1f GB/s = %.3f of 8 TB/s\n", K, R,
-                cell >> 10, stripes, best, bytes / best / 1e6, bytes / best / 1e6 / 8000.0);
+    double shards = 0;
+    for (uint32_t s = 0; s < stripes; s++) shards += K + (MIXED ? stripe_e(s, R) : R);
+    const double bytes = shards * cell;
+    std::printf("skeleton RS(%d,%d)%s %zu KiB x %u: %.4f ms/launch (best of 3 x 20) %.1f GB/s = %.3f of 8 TB/s"
+                " (mean writes %.2f)\n",
+                K, R, MIXED ? " mixed e" : "", cell >> 10, stripes, best, bytes / best / 1e6, bytes / best / 1e6 / 8000.0,
+                shards / stripes - K);
     CK(hipFree(in));
     CK(hipFree(out));
 }
@@ -99,6 +116,18 @@ int main() {
     const int cus = p.multiProcessorCount;
     const char* mode = std::getenv("PROBE_MODE");
     g_contig = std::getenv("PROBE_CONTIG") && std::atoi(std::getenv("PROBE_CONTIG")) == 1;
+    if (mode && std::string(mode) == "mixed") {
+        // per-stripe erasure counts 1..R against the fixed mixes of the same mean
+        for (int rep = 0; rep < 2; rep++) {
+            run<10, 4, true>(cus, 1 << 20, 256);
+            run<10, 2>(cus, 1 << 20, 256);
+            run<10, 3>(cus, 1 << 20, 256);
+            run<6, 3, true>(cus, 1 << 20, 1024);
+            run<6, 2>(cus, 1 << 20, 1024);
+            run<3, 2, true>(cus, 1 << 20, 1024);
+        }
+        return 0;
+    }
     if (mode && std::string(mode) == "footprint") {
         // RS(10,4) at growing stripe counts (footprint 3.5 .. 28 GiB), warmed up first
         run<10, 4>(cus, 1 << 20, 256);
