@@ -1147,8 +1147,11 @@ int launch_decode_mixed(const MixedArgs& in, int rows, int device, hipStream_t s
     };
     const void* fn = pick(res);
     if (!fn) return -1;
+    // The attribute is set to the resident ceiling, never to this launch's
+    // size: a coder may be shared by threads, and one thread lowering the
+    // limit between another's set and launch would fail that launch.
     if (res && dyn > kDynNoAttr &&
-        hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(dyn)) != hipSuccess) {
+        hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(kResidentMax)) != hipSuccess) {
         (void)hipGetLastError();
         res = false;  // the runtime refused the LDS: restage per stripe instead
         fn = pick(false);

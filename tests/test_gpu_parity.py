@@ -514,6 +514,34 @@ def test_device_decode_mixed_plans_resident(dev, S):
     mixed_many_plans_body(dev, coder(10, 4), S=S)
 
 
+def test_device_decode_mixed_resident_two_threads(dev):
+    """Two threads share one RS(10,4) coder, each on its own stream, decoding
+    mixed batches whose resident plan blobs need different dynamic-LDS sizes
+    past 64 KiB (S = 160 and 256), three times over: the launcher sets the
+    launch attribute to the resident ceiling, never to its own size, so one
+    thread's setting cannot fail the other's launch."""
+    import threading
+
+    cod = coder(10, 4)
+    errs = []
+
+    def run(S):
+        try:
+            with torch.cuda.stream(torch.cuda.Stream(device=dev)):
+                for _ in range(3):
+                    mixed_many_plans_body(dev, cod, S=S)
+        except Exception as e:  # noqa: BLE001 (re-raised below)
+            errs.append(e)
+
+    ts = [threading.Thread(target=run, args=(S,)) for S in (160, 256)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    if errs:
+        raise errs[0]
+
+
 def test_device_decode_mixed_not_enough_shards_launches_nothing(dev):
     k, m, S, cell = 6, 3, 4, 4096
     d = torch.zeros((S, k, cell), dtype=torch.uint8, device=dev)
