@@ -76,7 +76,7 @@ __global__ __launch_bounds__(BS) void skel(const uint8_t* __restrict__ in, uint8
 }
 
 // write-only: the same tiles and order, R output cells per stripe, no loads
-template <int R, int U, int BS>
+template <int R, int U, int BS, bool NT = true, bool DRAIN = true>
 __global__ __launch_bounds__(BS) void skelw(uint8_t* __restrict__ out, uint32_t chunks, uint32_t tps, uint32_t total,
                                             uint32_t group) {
     constexpr uint32_t TILE = BS * U;
@@ -88,29 +88,32 @@ __global__ __launch_bounds__(BS) void skelw(uint8_t* __restrict__ out, uint32_t 
 #pragma unroll
         for (int u = 0; u < U; u++)
 #pragma unroll
-            for (int j = 0; j < R; j++)
-                __builtin_nontemporal_store(u32x4{tile, uint32_t(j), uint32_t(u), threadIdx.x},
-                                            reinterpret_cast<u32x4*>(ob + j * cell +
-                                                                      uint64_t(tcol * TILE + u * BS + threadIdx.x) * 16));
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            for (int j = 0; j < R; j++) {
+                u32x4* dst = reinterpret_cast<u32x4*>(ob + j * cell + uint64_t(tcol * TILE + u * BS + threadIdx.x) * 16);
+                const u32x4 v{tile, uint32_t(j), uint32_t(u), threadIdx.x};
+                if constexpr (NT)
+                    __builtin_nontemporal_store(v, dst);
+                else
+                    *dst = v;
+            }
+        if constexpr (DRAIN) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
 }
 
-template <int R>
-void run_w(int cus, size_t cell, uint32_t stripes) {
-    constexpr int U = 4, BS = 256;
+template <int R, int U = 4, int BS = 256, bool NT = true, bool DRAIN = true>
+void run_w(int cus, size_t cell, uint32_t stripes, int bpc = 1) {
     const uint32_t chunks = uint32_t(cell / 16), tps = chunks / (BS * U), total = tps * stripes;
     uint8_t* out;
     CK(hipMalloc(&out, size_t(stripes) * R * cell));
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
-    for (int w = 0; w < 20; w++) skelw<R, U, BS><<<cus, BS>>>(out, chunks, tps, total, 4);
+    for (int w = 0; w < 20; w++) skelw<R, U, BS, NT, DRAIN><<<cus * bpc, BS>>>(out, chunks, tps, total, 4);
     CK(hipDeviceSynchronize());
     float best = 1e30f;
     for (int rep = 0; rep < 3; rep++) {
         CK(hipEventRecord(a));
-        for (int it = 0; it < 20; it++) skelw<R, U, BS><<<cus, BS>>>(out, chunks, tps, total, 4);
+        for (int it = 0; it < 20; it++) skelw<R, U, BS, NT, DRAIN><<<cus * bpc, BS>>>(out, chunks, tps, total, 4);
         CK(hipEventRecord(b));
         CK(hipEventSynchronize(b));
         float t;
@@ -118,8 +121,10 @@ void run_w(int cus, size_t cell, uint32_t stripes) {
         best = std::min(best, t / 20);
     }
     const double bytes = double(R) * cell * stripes;
-    std::printf("skeleton write-only %d cells %zu KiB x %u: %.4f ms/launch (best of 3 x 20) %.1f GB/s = %.3f of 8 TB/s\n",
-                R, cell >> 10, stripes, best, bytes / best / 1e6, bytes / best / 1e6 / 8000.0);
+    std::printf("skeleton write-only %d cells %zu KiB x %u (U %d, %d threads, %d per CU, %s, %s): %.4f ms/launch "
+                "(best of 3 x 20) %.1f GB/s = %.3f of 8 TB/s\n",
+                R, cell >> 10, stripes, U, BS, bpc, NT ? "nt" : "default policy", DRAIN ? "drained" : "no drain", best,
+                bytes / best / 1e6, bytes / best / 1e6 / 8000.0);
     CK(hipFree(out));
 }
 
@@ -259,6 +264,21 @@ int main() {
             run<6, 3, true>(cus, 1 << 20, 1024);
             run<6, 2>(cus, 1 << 20, 1024);
             run<3, 2, true>(cus, 1 << 20, 1024);
+        }
+        return 0;
+    }
+    if (mode && std::string(mode) == "writes") {
+        // write-only stream shapes: store policy, drain, chunks per lane, block size, blocks per CU
+        for (int rep = 0; rep < 2; rep++) {
+            run_w<3>(cus, 1 << 20, 2048);
+            run_w<3, 4, 256, false>(cus, 1 << 20, 2048);
+            run_w<3, 4, 256, true, false>(cus, 1 << 20, 2048);
+            run_w<3, 8, 256>(cus, 1 << 20, 2048);
+            run_w<3, 4, 512>(cus, 1 << 20, 2048);
+            run_w<3, 4, 256>(cus, 1 << 20, 2048, 2);
+            run_w<3, 4, 256>(cus, 1 << 20, 2048, 4);
+            run_w<3, 4, 256, true, false>(cus, 1 << 20, 2048, 4);
+            run_w<1, 4, 256>(cus, 1 << 20, 6144);
         }
         return 0;
     }
