@@ -213,9 +213,8 @@ void run_p(int cus, size_t cell, uint32_t stripes, uint32_t P, uint32_t pr, uint
 
 static bool g_contig = false;  // PROBE_CONTIG=1: physically contiguous allocations
 
-template <int K, int R, bool MIXED = false>
-void run(int cus, size_t cell, uint32_t stripes) {
-    constexpr int U = 4, BS = 256;
+template <int K, int R, bool MIXED = false, int U = 4, int BS = 256>
+void run(int cus, size_t cell, uint32_t stripes, int bpc = 1) {
     const uint32_t chunks = uint32_t(cell / 16), tps = chunks / (BS * U), total = tps * stripes;
     uint8_t *in, *out;
     const unsigned fl = g_contig ? hipDeviceMallocContiguous : hipDeviceMallocDefault;
@@ -225,12 +224,12 @@ void run(int cus, size_t cell, uint32_t stripes) {
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
-    for (int w = 0; w < 20; w++) skel<K, R, U, BS, MIXED><<<cus, BS>>>(in, out, chunks, tps, total, 4);
+    for (int w = 0; w < 20; w++) skel<K, R, U, BS, MIXED><<<cus * bpc, BS>>>(in, out, chunks, tps, total, 4);
     CK(hipDeviceSynchronize());
     std::vector<float> ms;
     for (int rep = 0; rep < 3; rep++) {
         CK(hipEventRecord(a));
-        for (int it = 0; it < 20; it++) skel<K, R, U, BS, MIXED><<<cus, BS>>>(in, out, chunks, tps, total, 4);
+        for (int it = 0; it < 20; it++) skel<K, R, U, BS, MIXED><<<cus * bpc, BS>>>(in, out, chunks, tps, total, 4);
         CK(hipEventRecord(b));
         CK(hipEventSynchronize(b));
         float t;
@@ -242,9 +241,14 @@ void run(int cus, size_t cell, uint32_t stripes) {
     for (uint32_t s = 0; s < stripes; s++) shards += K + (MIXED ? stripe_e(s, R) : R);
     const double bytes = shards * cell;
     std::printf("skeleton RS(%d,%d)%s %zu KiB x %u: %.4f ms/launch (best of 3 x 20) %.1f GB/s = %.3f of 8 TB/s"
-                " (mean writes %.2f)\n",
+                " (mean writes %.2f)%s\n",
                 K, R, MIXED ? " mixed e" : "", cell >> 10, stripes, best, bytes / best / 1e6, bytes / best / 1e6 / 8000.0,
-                shards / stripes - K);
+                shards / stripes - K,
+                (U == 4 && BS == 256 && bpc == 1)
+                    ? ""
+                    : (" [U " + std::to_string(U) + ", " + std::to_string(BS) + " threads, " + std::to_string(bpc) +
+                       " per CU]")
+                          .c_str());
     CK(hipFree(in));
     CK(hipFree(out));
 }
@@ -264,6 +268,22 @@ int main() {
             run<6, 3, true>(cus, 1 << 20, 1024);
             run<6, 2>(cus, 1 << 20, 1024);
             run<3, 2, true>(cus, 1 << 20, 1024);
+        }
+        return 0;
+    }
+    if (mode && std::string(mode) == "occupancy") {
+        // more waves per SIMD (the write-only stream gains 5 % at 4 blocks per CU)
+        for (int rep = 0; rep < 2; rep++) {
+            run<6, 3>(cus, 1 << 20, 1024);
+            run<6, 3, false, 4, 256>(cus, 1 << 20, 1024, 2);
+            run<6, 3, false, 4, 256>(cus, 1 << 20, 1024, 4);
+            run<6, 3, false, 2, 256>(cus, 1 << 20, 1024, 2);
+            run<6, 3, false, 2, 256>(cus, 1 << 20, 1024, 4);
+            run<3, 2>(cus, 1 << 20, 1024);
+            run<3, 2, false, 4, 256>(cus, 1 << 20, 1024, 4);
+            run<3, 2, false, 2, 256>(cus, 1 << 20, 1024, 4);
+            run<10, 4>(cus, 1 << 20, 256);
+            run<10, 4, false, 2, 256>(cus, 1 << 20, 256, 4);
         }
         return 0;
     }
