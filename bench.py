@@ -188,6 +188,80 @@ def cpu_baseline(k, m, cell, seconds, threads=1):
     return res
 
 
+def cpu_config_batch(H, k, m, cell, stripes, threads):
+    """BASELINE.json configs[0] -- RS(3,2) 1 MiB cells, a 1024-stripe batch on
+    the CPU (the reference's rust/benches/ec.rs:16-33 path, no GPU): the
+    whole batch encoded, then decoded with data shards 0..m-1 missing, by the
+    C restatement of the reference loop (kind "port", orc_encode_batch /
+    orc_decode_batch over contiguous stripe slices) and by the engine's own
+    host routine (hec_encode / hec_decode per stripe on host-only coders,
+    as the per-row drop-in calls it without a GPU), each on 1 thread
+    and on the box's CPU share.  The engine's parity is checked against the
+    port's for every stripe."""
+    import ctypes
+
+    import numpy as np
+
+    import ec_oracle
+    lib = ec_oracle.load_c_oracle()
+    rng = np.random.default_rng(0x3232)
+    data = np.frombuffer(rng.bytes(stripes * k * cell), dtype=np.uint8).reshape(stripes, k, cell)
+    present = ((1 << (k + m)) - 1) & ~((1 << m) - 1)
+    out = {}
+    ref_par = None
+    for kind in ("port", "engine_host"):
+        for th in sorted({1, max(1, threads)}):
+            par = np.empty((stripes, m, cell), dtype=np.uint8)
+            rec = np.empty((stripes, m, cell), dtype=np.uint8)
+            rcs = []
+            # host-only coders (HEC_DEVICE_HOST): the engine's host routine for
+            # every row, no device involved
+            coders = [H.Coder(k, m, H.HEC_DEVICE_HOST) for _ in range(th)] if kind == "engine_host" else []
+
+            def work(t):
+                a, b = stripes * t // th, stripes * (t + 1) // th
+                if kind == "port":
+                    rcs.append(lib.orc_encode_batch(k, m, data[a:b].ctypes.data, cell, b - a, par[a:b].ctypes.data))
+                    rcs.append(lib.orc_decode_batch(k, m, data[a:b].ctypes.data, par[a:b].ctypes.data, cell, b - a,
+                                                    ctypes.c_uint64(present), rec[a:b].ctypes.data))
+                    return
+                h = coders[t].handle
+                for s in range(a, b):
+                    ins = (ctypes.c_void_p * k)(*[data[s, i].ctypes.data for i in range(k)])
+                    outs = (ctypes.c_void_p * m)(*[par[s, j].ctypes.data for j in range(m)])
+                    rcs.append(H.lib.hec_encode(h, ins, cell, outs))
+                for s in range(a, b):
+                    shards = (ctypes.c_void_p * (k + m))(*([0] * m + [data[s, i].ctypes.data for i in range(m, k)] +
+                                                            [par[s, j].ctypes.data for j in range(m)]))
+                    recs = (ctypes.c_void_p * (k + m))(*([rec[s, i].ctypes.data for i in range(m)] + [0] * (k)))
+                    rcs.append(H.lib.hec_decode(h, shards, cell, recs))
+
+            t0 = time.perf_counter()
+            ths = [threading.Thread(target=work, args=(t,)) for t in range(th)]
+            for x in ths:
+                x.start()
+            for x in ths:
+                x.join()
+            el = time.perf_counter() - t0
+            for c in coders:
+                c.close()
+            assert all(rc == 0 for rc in rcs), f"cpu config {kind} rc {set(rcs)}"
+            assert np.array_equal(rec, data[:, :m]), f"cpu config {kind} decode mismatch"
+            if ref_par is None:
+                ref_par = par
+            else:
+                assert np.array_equal(par, ref_par), f"cpu config {kind} parity != port parity"
+            out[f"{kind}_{th}t"] = {"value": round(2 * stripes * k * cell / GIB / el, 4), "unit": "GiB/s",
+                                    "cores": th, "seconds": round(el, 3),
+                                    "kind": "port" if kind == "port" else "engine"}
+    return {"config": f"RS({k},{m}) {cell} B cells, {stripes}-stripe batch, encode + decode data 0..{m - 1} missing "
+                      f"(BASELINE.json configs[0], rust/benches/ec.rs:16-33)",
+            "legs": out, "host_isa": H.host_isa(), "host": host_info(),
+            "note": "port = oracle/ec_oracle.c (restates matrix.rs:204-231; the Rust path is unbuildable here), "
+                    "engine = hec_encode / hec_decode per stripe on the host routine; the whole batch, not a "
+                    "sample; every stripe's engine parity == port parity, rebuilt cells == data"}
+
+
 def traffic_for(path, k, m, cell, stripes, mode):
     """PMC HBM bytes per launch for this exact config, from the committed
     per-config profile (scripts/profile_configs.py: FETCH_SIZE / WRITE_SIZE
@@ -682,6 +756,9 @@ def main():
         result["cpu_baseline"] = cpu_baseline(k, m, cell, args.cpu_seconds, 1)
         if args.cpu_threads > 1:
             result["cpu_baseline_parallel"] = cpu_baseline(k, m, cell, args.cpu_seconds, args.cpu_threads)
+        if (k, m, cell) == (6, 3, 1 << 20) and args.codec == "rs" and not args.tune:
+            log("cpu config RS(3,2) x 1024")
+            result["cpu_baseline_configs"] = [cpu_config_batch(H, 3, 2, 1 << 20, 1024, args.cpu_threads)]
     elif rank == 0:
         result["cpu_baseline"] = None
 

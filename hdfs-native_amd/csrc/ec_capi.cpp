@@ -70,6 +70,7 @@ struct DeviceGuard {
     int prev = -1;
     bool ok = false;
     explicit DeviceGuard(int dev) {
+        if (dev < 0) return;  // a host-only coder (HEC_DEVICE_HOST): no device, no HIP call
         if (hipGetDevice(&prev) != hipSuccess) prev = -1;
         ok = hipSetDevice(dev) == hipSuccess;
     }
@@ -86,6 +87,7 @@ struct hec_coder {
     bool xor_codec = false;
     std::string codec;         // "rs", "xor" or "rs-legacy"
     bool pooled = false;       // handed out by hec_coder_acquire (returned by hec_coder_release)
+    bool idle = false;         // pooled and sitting in the pool (guarded by the pool mutex)
     std::vector<uint8_t> enc;  // (k+m) x k
     std::vector<uint64_t> enc_aff;  // m x k: host affine qwords of the parity rows
     // hec_encode / hec_decode rows of at most this many bytes per shard are
@@ -355,7 +357,7 @@ int call_through_device(hec_coder* c, const uint8_t* const* in, size_t nin, uint
 // ones through the device under the coder's host lock.
 int code_row(hec_coder* c, const uint8_t* mat, const uint64_t* aff, const uint8_t* const* in, size_t nin,
              uint8_t* const* out, size_t nout, size_t n) {
-    if (n <= c->host_limit.load(std::memory_order_relaxed)) {
+    if (c->device == HEC_DEVICE_HOST || n <= c->host_limit.load(std::memory_order_relaxed)) {
         hec::host::gf_matmul(mat, aff, nout, nin, in, out, n);
         return HEC_OK;
     }
@@ -374,6 +376,10 @@ int ensure_dbuf(hec_coder* c, size_t bytes) {
     c->dbuf_bytes = bytes;
     return HEC_OK;
 }
+
+// Device-resident calls on a host-only coder (HEC_DEVICE_HOST): an error, never
+// a HIP call.
+int host_only(const char* what) { return fail(HEC_ERR_DEVICE, what, hipErrorNoDevice); }
 
 template <typename F>
 int guarded(F&& f) {
@@ -462,9 +468,11 @@ int hec_coder_create_codec(const char* codec, size_t data_units, size_t parity_u
     if (name != "rs" && name != "xor" && name != "rs-legacy") return HEC_ERR_UNSUPPORTED_CODEC;
     if (name == "xor" && parity_units != 1) return HEC_ERR_INVALID_ARG;  // XOR-k-1 only
     return guarded([&] {
-        int ndev = 0;
-        HEC_HIP(hipGetDeviceCount(&ndev), HEC_ERR_DEVICE);
-        if (device < 0 || device >= ndev) return fail(HEC_ERR_DEVICE, "device ordinal", hipErrorInvalidDevice);
+        if (device != HEC_DEVICE_HOST) {
+            int ndev = 0;
+            HEC_HIP(hipGetDeviceCount(&ndev), HEC_ERR_DEVICE);
+            if (device < 0 || device >= ndev) return fail(HEC_ERR_DEVICE, "device ordinal", hipErrorInvalidDevice);
+        }
         auto* c = new hec_coder();
         c->k = data_units;
         c->m = parity_units;
@@ -475,6 +483,11 @@ int hec_coder_create_codec(const char* codec, size_t data_units, size_t parity_u
                  : name == "rs-legacy" ? hec::gen_rs_legacy_matrix(data_units, parity_units)
                                        : hec::gen_rs_matrix(data_units, parity_units);
         c->enc_aff = hec::host::affine_matrices(c->enc.data() + data_units * data_units, parity_units * data_units);
+        if (device == HEC_DEVICE_HOST) {  // host routine only: no stream, event or buffer
+            c->host_limit.store(SIZE_MAX, std::memory_order_relaxed);
+            *out = c;
+            return int(HEC_OK);
+        }
         int rc = [&] {
             DeviceGuard g(device);
             if (!g.ok) return fail(HEC_ERR_DEVICE, "hipSetDevice", hipErrorInvalidDevice);
@@ -566,14 +579,15 @@ extern "C" {
 int hec_coder_acquire(const char* codec, size_t data_units, size_t parity_units, int device, hec_coder_t** out) {
     if (!out) return HEC_ERR_INVALID_ARG;
     *out = nullptr;
-    if (device < -1) return HEC_ERR_INVALID_ARG;
+    if (device < HEC_DEVICE_HOST) return HEC_ERR_INVALID_ARG;
     return guarded([&] {
         const std::string name = codec ? codec : "rs";
-        if (device < 0) {  // any device: round-robin over the visible ones
+        if (device == -1) {  // any device: round-robin over the visible ones; none -> host-only
             int ndev = 0;
-            HEC_HIP(hipGetDeviceCount(&ndev), HEC_ERR_DEVICE);
-            if (ndev <= 0) return fail(HEC_ERR_DEVICE, "no device", hipErrorNoDevice);
-            device = int(coder_pool().next_device.fetch_add(1, std::memory_order_relaxed) % unsigned(ndev));
+            if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+                device = HEC_DEVICE_HOST;
+            else
+                device = int(coder_pool().next_device.fetch_add(1, std::memory_order_relaxed) % unsigned(ndev));
         }
         CoderPool& pool = coder_pool();
         {
@@ -582,6 +596,7 @@ int hec_coder_acquire(const char* codec, size_t data_units, size_t parity_units,
             if (it != pool.idle.end() && !it->second.empty()) {
                 *out = it->second.back();
                 it->second.pop_back();
+                (*out)->idle = false;
                 return int(HEC_OK);
             }
         }
@@ -600,8 +615,16 @@ void hec_coder_release(hec_coder_t* c) {
         try {
             CoderPool& pool = coder_pool();
             std::lock_guard<std::mutex> lk(pool.mu);
+            // a second release of a coder already in the pool is ignored: pushing
+            // it twice would hand one coder to two "exclusive" acquirers
+            if (c->idle) return;
+            // the next acquirer gets a coder with default behaviour: a host
+            // limit set by this user (e.g. 0 to force the device) does not carry over
+            c->host_limit.store(c->device == HEC_DEVICE_HOST ? SIZE_MAX : hec_coder::kDefaultHostLimit,
+                                std::memory_order_relaxed);
             auto& v = pool.idle[std::make_tuple(c->codec, c->k, c->m, c->device)];
             if (v.size() < kPoolIdlePerKey) {
+                c->idle = true;
                 v.push_back(c);
                 return;
             }
@@ -656,6 +679,7 @@ int hec_gf_matmul_host(const uint8_t* matrix, size_t rows, size_t cols, const ui
 int hec_gf_matmul_device(hec_coder_t* c, const uint8_t* matrix, size_t rows, size_t cols,
                          const uint8_t* const* d_in, const size_t* in_strides, uint8_t* const* d_out,
                          const size_t* out_strides, size_t cell_len, size_t stripes, void* hip_stream) {
+    if (c && c->device == HEC_DEVICE_HOST) return host_only("hec_gf_matmul_device");
     if (!c) return HEC_ERR_INVALID_ARG;
     return guarded([&] {
         DeviceGuard g(c->device);
@@ -676,6 +700,7 @@ int hec_encode_device(hec_coder_t* c, const uint8_t* const* d_data, const size_t
 int hec_decode_device(hec_coder_t* c, const uint8_t* const* d_shards, const size_t* shard_strides,
                       uint8_t* const* d_out, const size_t* out_strides, size_t cell_len, size_t stripes,
                       void* hip_stream) {
+    if (c && c->device == HEC_DEVICE_HOST) return host_only("hec_decode_device");
     if (!c || !d_shards || !shard_strides || cell_len == 0) return HEC_ERR_INVALID_ARG;
     return guarded([&] {
         uint8_t present[HEC_MAX_DATA_UNITS + HEC_MAX_PARITY_UNITS];
@@ -931,6 +956,7 @@ int hec_decode_device_mixed(hec_coder_t* c, const uint8_t* const* d_shards, cons
                             uint8_t* const* d_out, const size_t* out_strides, const uint64_t* present,
                             size_t cell_len, size_t stripes, void* d_workspace, size_t workspace_bytes,
                             void* hip_stream) {
+    if (c && c->device == HEC_DEVICE_HOST) return host_only("hec_decode_device_mixed");
     if (!c || !d_shards || !shard_strides || !d_out || !out_strides || !present || cell_len == 0)
         return HEC_ERR_INVALID_ARG;
     if (stripes == 0) return HEC_OK;
@@ -953,6 +979,19 @@ int hec_encode_host_batch(hec_coder_t* c, const uint8_t* h_data, uint8_t* h_pari
                           size_t stripes, size_t chunk_stripes) {
     if (!c || !h_data || !h_parity || cell_len == 0 || chunk_stripes == 0) return HEC_ERR_INVALID_ARG;
     if (stripes == 0) return HEC_OK;
+    if (c->device == HEC_DEVICE_HOST) {  // host-only coder: the host routine, stripe by stripe
+        return guarded([&] {
+            const size_t k = c->k, m = c->m;
+            const uint8_t* in[HEC_MAX_DATA_UNITS];
+            uint8_t* out[HEC_MAX_PARITY_UNITS];
+            for (size_t s = 0; s < stripes; s++) {
+                for (size_t i = 0; i < k; i++) in[i] = h_data + (s * k + i) * cell_len;
+                for (size_t j = 0; j < m; j++) out[j] = h_parity + (s * m + j) * cell_len;
+                hec::host::gf_matmul(c->enc.data() + k * k, c->enc_aff.data(), m, k, in, out, cell_len);
+            }
+            return int(HEC_OK);
+        });
+    }
     return guarded([&] {
         std::lock_guard<std::mutex> lk(c->host_mu);
         DeviceGuard g(c->device);
@@ -1064,6 +1103,18 @@ int hec_decode_host_batch(hec_coder_t* c, const uint8_t* const* h_vertical, size
         }
 
         int rc = [&]() -> int {
+            if (c->device == HEC_DEVICE_HOST) {  // host-only coder: rebuild row by row on this thread
+                const size_t e = p.missing.size();
+                const uint8_t* in[HEC_MAX_DATA_UNITS];
+                uint8_t* out[HEC_MAX_DATA_UNITS];
+                for (size_t r = 0; r < rows; r++) {
+                    for (size_t i = 0; i < k; i++) in[i] = h_vertical[p.survivors[i]] + r * cell_len;
+                    for (size_t i = 0; i < e; i++) out[i] = h_file + (r * k + p.missing[i]) * cell_len;
+                    hec::host::gf_matmul(p.matrix.data(), p.aff.data(), e, k, in, out, cell_len);
+                }
+                copy_rows(own_a, own_b);
+                return int(HEC_OK);
+            }
             std::lock_guard<std::mutex> lk(c->host_mu);
             DeviceGuard g(c->device);
             if (!g.ok) return fail(HEC_ERR_DEVICE, "hipSetDevice", hipErrorInvalidDevice);
@@ -1181,6 +1232,7 @@ int hec_encode_rows_host(hec_coder_t* c, const uint8_t* h_data, size_t data_len,
 
 int hec_encode_rows_device(hec_coder_t* c, const uint8_t* d_data, size_t data_len, uint8_t* d_parity, size_t cell_len,
                            void* d_workspace, size_t workspace_bytes, void* hip_stream) {
+    if (c && c->device == HEC_DEVICE_HOST) return host_only("hec_encode_rows_device");
     if (!c || !d_data || !d_parity || cell_len == 0) return HEC_ERR_INVALID_ARG;
     if (data_len == 0) return HEC_OK;
     const size_t k = c->k, m = c->m, row = k * cell_len;
@@ -1196,12 +1248,19 @@ int hec_encode_rows_device(hec_coder_t* c, const uint8_t* d_data, size_t data_le
         dout[j] = d_parity + j * cell_len;
         ost[j] = m * cell_len;
     }
+    // validate the workspace before anything is queued: a bad argument must not
+    // leave the full rows' parity written and the short row's not.  It is
+    // needed only when some cell of the short last row holds fewer than
+    // n0 = min(cell, L) bytes (the zero-padded copies); k == 1, or a short
+    // row whose cells all reach n0, needs none.
+    const size_t n0 = std::min(cell_len, L);
+    bool pad = false;
+    for (size_t i = 0; i < k && L; i++) pad |= (L > i * cell_len ? std::min(cell_len, L - i * cell_len) : 0) < n0;
+    if (pad && (!d_workspace || workspace_bytes < k * n0)) return HEC_ERR_INVALID_ARG;
     if (full) {
         const int rc = hec_encode_device(c, din, ist, dout, ost, cell_len, full, hip_stream);
         if (rc != HEC_OK || L == 0) return rc;
     }
-    const size_t n0 = std::min(cell_len, L);
-    if (!d_workspace || workspace_bytes < k * n0) return HEC_ERR_INVALID_ARG;
     return guarded([&] {
         DeviceGuard g(c->device);
         if (!g.ok) return fail(HEC_ERR_DEVICE, "hipSetDevice", hipErrorInvalidDevice);
@@ -1328,6 +1387,7 @@ int checksum_launch(hec_coder* c, int kind, const uint8_t* const* bases, const s
 int checksum_entry(hec_coder* c, int checksum_type, const uint8_t* const* d_bases, const size_t* strides,
                    size_t n_shards, size_t cell_len, size_t stripes, size_t bpc, uint8_t* d_out,
                    const uint8_t* d_expected, uint8_t* d_bad, void* hip_stream) {
+    if (c && c->device == HEC_DEVICE_HOST) return host_only("checksum_entry");
     const int kind = crc_kind(checksum_type);
     if (!c || !d_bases || !strides || kind < 0 || n_shards == 0 || n_shards > size_t(hec::kCrcMaxShards) ||
         cell_len == 0 || bpc == 0 || (!d_out && !d_expected) || (d_expected && !d_bad))
@@ -1373,6 +1433,7 @@ int hec_checksum_verify_device(hec_coder_t* c, int checksum_type, const uint8_t*
 int hec_encode_crc_device(hec_coder_t* c, const uint8_t* const* d_data, const size_t* data_strides,
                           uint8_t* const* d_parity, const size_t* parity_strides, size_t cell_len, size_t stripes,
                           size_t bytes_per_checksum, uint8_t* d_sums, void* hip_stream) {
+    if (c && c->device == HEC_DEVICE_HOST) return host_only("hec_encode_crc_device");
     if (!c || !d_data || !data_strides || !d_parity || !parity_strides || !d_sums || cell_len == 0 ||
         bytes_per_checksum == 0)
         return HEC_ERR_INVALID_ARG;
@@ -1437,6 +1498,7 @@ int hec_decode_verify_device(hec_coder_t* c, int checksum_type, const uint8_t* c
                              const size_t* shard_strides, uint8_t* const* d_out, const size_t* out_strides,
                              size_t cell_len, size_t stripes, size_t bytes_per_checksum, const uint8_t* d_sums,
                              uint8_t* d_bad, void* hip_stream) {
+    if (c && c->device == HEC_DEVICE_HOST) return host_only("hec_decode_verify_device");
     if (!c || !d_shards || !shard_strides || !d_out || !out_strides || cell_len == 0) return HEC_ERR_INVALID_ARG;
     if (checksum_type == HEC_CHECKSUM_NULL)
         return hec_decode_device(c, d_shards, shard_strides, d_out, out_strides, cell_len, stripes, hip_stream);

@@ -30,6 +30,7 @@ HEC_ERR_DEVICE = -4
 HEC_ERR_NO_MEMORY = -5
 HEC_ERR_SINGULAR = -6
 HEC_ERR_CHECKSUM = -7
+HEC_DEVICE_HOST = -2  # host-only coder: the engine's host routine, no GPU needed
 
 # ChecksumTypeProto values (rust/src/proto/hadoop.hdfs.rs:1363)
 CHECKSUM_NULL = 0

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define HEC_ABI_VERSION 4
+#define HEC_ABI_VERSION 5
 
 /* Status codes */
 #define HEC_OK 0
@@ -93,7 +93,16 @@ int hec_decode_plan(size_t data_units, size_t parity_units, const uint8_t *prese
 
 /* ---- Coder lifecycle (Coder::new, gf256.rs:32-38) --------------------- */
 
-/* Creates a coder for RS(data_units, parity_units) on HIP device `device`.
+/* `device` value of a host-only coder: no HIP call is made (creation cannot
+ * fail for want of a GPU).  hec_encode / hec_decode and the host-batch calls
+ * (hec_encode_host_batch, hec_decode_host_batch, hec_*_rows_host) run the
+ * engine's host routine (hec_gf_matmul_host) whatever the host limit; the
+ * device-resident calls return HEC_ERR_DEVICE.  This keeps the reference's
+ * infallible Coder::new (gf256.rs:32-38) on a host without a visible GPU. */
+#define HEC_DEVICE_HOST (-2)
+
+/* Creates a coder for RS(data_units, parity_units) on HIP device `device`
+ * (or HEC_DEVICE_HOST).
  * 1 <= data_units <= HEC_MAX_DATA_UNITS, 1 <= parity_units <= HEC_MAX_PARITY_UNITS. */
 int hec_coder_create(size_t data_units, size_t parity_units, int device, hec_coder_t **out);
 /* Same with a codec name: "rs" (the default above), "xor" (Hadoop XOR-k-1:
@@ -118,9 +127,12 @@ int hec_coder_device(const hec_coder_t *coder);
  * most 64 idle per key are kept, the rest destroyed).  An acquired coder is
  * the caller's alone until released; steady state costs a mutex and a
  * vector pop -- no stream, event or buffer creation.  device -1 = any device
- * (round-robin over the visible ones).  hec_coder_release on a coder from
- * hec_coder_create destroys it.  hec_coder_pool_trim destroys every idle
- * pooled coder and returns how many. */
+ * (round-robin over the visible ones; a host-only coder, HEC_DEVICE_HOST, when
+ * no GPU is visible), HEC_DEVICE_HOST = host-only.  Release resets the coder's host
+ * limit to the default (a setting never carries over to the next acquirer)
+ * and ignores a second release of a coder that is already idle in the pool.
+ * hec_coder_release on a coder from hec_coder_create destroys it.
+ * hec_coder_pool_trim destroys every idle pooled coder and returns how many. */
 int hec_coder_acquire(const char *codec, size_t data_units, size_t parity_units, int device, hec_coder_t **out);
 void hec_coder_release(hec_coder_t *coder);
 size_t hec_coder_pool_trim(void);
@@ -318,7 +330,9 @@ int hec_encode_rows_host(hec_coder_t *coder, const uint8_t *h_data, size_t data_
  * ceil(data_len / (k*cell_len)) rows.  The short row's short cells are
  * zero-padded into d_workspace (hec_encode_rows_workspace_size bytes, untouched
  * until the stream reaches the work), so nothing is read past d_data +
- * data_len. */
+ * data_len.  The workspace is checked before anything is queued, and is
+ * needed (may be NULL otherwise) only when some cell of the short row holds
+ * fewer than n0 bytes. */
 size_t hec_encode_rows_workspace_size(const hec_coder_t *coder, size_t cell_len);
 int hec_encode_rows_device(hec_coder_t *coder, const uint8_t *d_data, size_t data_len, uint8_t *d_parity,
                            size_t cell_len, void *d_workspace, size_t workspace_bytes, void *hip_stream);

@@ -78,7 +78,7 @@ unsafe extern "C" {
 }
 
 /// The ABI revision this shim is written against (include/hdfs_ec_amd.h).
-const ABI_VERSION: c_int = 4;
+const ABI_VERSION: c_int = 5;
 
 /// Status -> the reference's error kinds (rust/src/error.rs:32-39).
 fn err(rc: c_int) -> HdfsError {

@@ -2,7 +2,8 @@
  * ABI paths that need no GPU: every coding matrix up to RS(32,16), the
  * inversion, the decode plan of all 2^14 presence masks of RS(10,4), and the
  * coder / group creation failure paths (no device in the container: each
- * must return a status and leak nothing).  Built and run by
+ * must return a status and leak nothing), and a host-only coder
+ * (HEC_DEVICE_HOST) through every host call.  Built and run by
  * scripts/asan_host.sh (tests/test_capi.py).  Device code is not sanitized
  * (no GPU ASan on this pool). */
 #include <stdio.h>
@@ -35,10 +36,54 @@ int main(void) {
     hec_coder_t* c = 0;
     (void)hec_coder_create(6, 3, 0, &c);
     hec_coder_destroy(c);
-    /* pool: no device -> a status; release / trim of nothing */
-    if (hec_coder_acquire("rs", 6, 3, -1, &c) == HEC_OK) bad++;
+    /* pool: no device -> acquire(-1) hands out a host-only coder; a double
+     * release is ignored; trim frees it */
+    c = 0;
+    if (hec_coder_acquire("rs", 6, 3, -1, &c) != HEC_OK || hec_coder_device(c) != HEC_DEVICE_HOST) bad++;
     hec_coder_release(c);
-    (void)hec_coder_pool_trim();
+    hec_coder_release(c);
+    if (hec_coder_pool_trim() != 1) bad++;
+    /* a host-only coder end to end: rows, host batches (file-order decode),
+     * the short-row file calls, and the device calls as statuses */
+    {
+        enum { K = 6, P = 3, CELL = 4099, S = 3 };
+        hec_coder_t* h = 0;
+        if (hec_coder_create_codec("rs", K, P, HEC_DEVICE_HOST, &h) != HEC_OK) bad++;
+        uint8_t* data = (uint8_t*)malloc(S * K * CELL);
+        uint8_t* par = (uint8_t*)malloc(S * P * CELL);
+        uint8_t* file = (uint8_t*)malloc(S * K * CELL);
+        for (size_t b = 0; b < (size_t)S * K * CELL; b++) data[b] = (uint8_t)(b * 131 + 7);
+        if (hec_encode_host_batch(h, data, par, CELL, S, 2) != HEC_OK) bad++;
+        uint8_t* vert[K + P];
+        for (int i = 0; i < K + P; i++) {
+            vert[i] = (uint8_t*)malloc(S * CELL);
+            for (int s = 0; s < S; s++)
+                memcpy(vert[i] + s * CELL, i < K ? data + (s * K + i) * CELL : par + (s * P + i - K) * CELL, CELL);
+        }
+        const uint8_t* vin[K + P];
+        size_t vlen[K + P];
+        for (int i = 0; i < K + P; i++) {
+            vin[i] = (i == 1 || i == 5) ? 0 : vert[i];
+            vlen[i] = S * CELL;
+        }
+        if (hec_decode_host_batch(h, vin, CELL, S, file, 2) != HEC_OK || memcmp(file, data, S * K * CELL)) bad++;
+        memset(file, 0, S * K * CELL);
+        if (hec_decode_rows_host(h, vin, vlen, CELL, file, S * K * CELL - 5, 2) != HEC_OK ||
+            memcmp(file, data, S * K * CELL - 5)) bad++;
+        if (hec_encode_rows_host(h, data, S * K * CELL - 4000, par, CELL, 2) != HEC_OK) bad++;
+        const uint8_t* rin[K];
+        uint8_t* rout[P];
+        for (int i = 0; i < K; i++) rin[i] = data + i * CELL;
+        for (int j = 0; j < P; j++) rout[j] = par + j * CELL;
+        if (hec_encode(h, rin, CELL, rout) != HEC_OK) bad++;
+        size_t st[K + P] = {0};
+        if (hec_encode_device(h, rin, st, rout, st, CELL, 1, 0) != HEC_ERR_DEVICE) bad++;
+        for (int i = 0; i < K + P; i++) free(vert[i]);
+        free(data);
+        free(par);
+        free(file);
+        hec_coder_destroy(h);
+    }
     /* the host small-row routine over exact-size heap buffers (every tail
      * length up to 200 and a 64 KiB + 5 row): no access past the shards */
     for (size_t n = 1; n < 200 || n == 65541; n = n < 199 ? n + 1 : (n == 199 ? 65541 : 0)) {

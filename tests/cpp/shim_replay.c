@@ -55,7 +55,7 @@ static uint8_t next_byte(void) {
 enum { K = 6, M = 3 };
 
 int main(void) {
-    CHECK(hec_abi_version() == 4, "ABI %d", hec_abi_version());
+    CHECK(hec_abi_version() == 5, "ABI %d", hec_abi_version());
     hec_coder_t *c = NULL;
     int rc = hec_coder_create_codec("rs", K, M, 0, &c);
     if (rc != HEC_OK) {

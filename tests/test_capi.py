@@ -32,7 +32,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version_and_strerror():
-    assert H.lib.hec_abi_version() == 4
+    assert H.lib.hec_abi_version() == 5
     assert "Not enough valid shards" in H.strerror(H.HEC_ERR_NOT_ENOUGH_SHARDS)
     assert H.strerror(H.HEC_ERR_CHECKSUM) == "checksum error"
     assert H.strerror(12345) == "unknown status"
@@ -237,7 +237,7 @@ def test_gf_matmul_host_args():
 def test_coder_pool_args_need_no_device():
     h = ctypes.c_void_p()
     assert H.lib.hec_coder_acquire(b"rs", 6, 3, 0, None) == H.HEC_ERR_INVALID_ARG
-    assert H.lib.hec_coder_acquire(b"rs", 6, 3, -2, ctypes.byref(h)) == H.HEC_ERR_INVALID_ARG
+    assert H.lib.hec_coder_acquire(b"rs", 6, 3, -3, ctypes.byref(h)) == H.HEC_ERR_INVALID_ARG
     assert H.lib.hec_coder_acquire(b"lrc", 6, 3, 0, ctypes.byref(h)) in (H.HEC_ERR_UNSUPPORTED_CODEC,
                                                                          H.HEC_ERR_DEVICE)
     assert not h.value
@@ -245,5 +245,75 @@ def test_coder_pool_args_need_no_device():
     assert H.lib.hec_coder_set_host_limit(None, 5) == H.HEC_ERR_INVALID_ARG
     assert H.lib.hec_coder_host_limit(None) == 0
     if not gpu_available():
-        assert H.lib.hec_coder_acquire(b"rs", 6, 3, -1, ctypes.byref(h)) == H.HEC_ERR_DEVICE
-        assert H.pool_trim() == 0
+        # no GPU: "any device" is a host-only coder (Coder::new stays infallible)
+        assert H.lib.hec_coder_acquire(b"rs", 6, 3, -1, ctypes.byref(h)) == H.HEC_OK
+        assert H.lib.hec_coder_device(h) == H.HEC_DEVICE_HOST
+        H.lib.hec_coder_release(h)
+        assert H.pool_trim() == 1
+
+
+# ---- host-only coders (HEC_DEVICE_HOST): run here, no GPU ------------------
+
+def test_host_only_coder_encode_decode_vs_oracle(c_oracle):
+    """Coder::new without a GPU (gf256.rs:32-38 is infallible): a host-only
+    coder codes every row on the engine's host routine, bit-exact with the
+    oracle, at sizes far above the device host limit."""
+    import numpy as np
+    for k, m in [(3, 2), (6, 3), (10, 4)]:
+        c = H.Coder(k, m, H.HEC_DEVICE_HOST)
+        assert H.lib.hec_coder_device(c.handle) == H.HEC_DEVICE_HOST
+        c.host_limit = 0  # ignored: a host-only coder never routes to a device
+        for n in (1, 17, 4096, (1 << 20) + 3):
+            data = [np.frombuffer(os.urandom(n), dtype=np.uint8) for _ in range(k)]
+            got = c.encode([d.tobytes() for d in data])
+            want = O.c_encode(c_oracle, k, m, data)
+            assert all(g == w.tobytes() for g, w in zip(got, want)), (k, m, n)
+            full = [d.tobytes() for d in data] + got
+            for miss in [(0,), tuple(range(m)), tuple(range(k - 1, k - 1 + m))]:
+                shards = [None if i in miss else full[i] for i in range(k + m)]
+                c.decode(shards)
+                assert shards[:k] == full[:k], (k, m, n, miss)
+        c.close()
+
+
+def test_host_only_coder_batches_and_device_calls():
+    """Host-batch calls run on the host routine; device-resident calls are
+    HEC_ERR_DEVICE (never a HIP call)."""
+    import numpy as np
+    k, m, cell, S = 6, 3, 4096, 5
+    c = H.Coder(k, m, H.HEC_DEVICE_HOST)
+    data = np.frombuffer(os.urandom(S * k * cell), dtype=np.uint8).reshape(S, k, cell).copy()
+    par = np.zeros((S, m, cell), dtype=np.uint8)
+    c.encode_host_batch(data.ctypes.data, par.ctypes.data, cell, S, 2)
+    for s in range(S):
+        want = O.encode(k, m, list(data[s]))
+        assert [bytes(x) for x in par[s]] == [bytes(w) for w in want]
+    # decode straight into file order with data shards 0 and 4 lost
+    vert = [np.ascontiguousarray(data[:, i]) for i in range(k)] + [np.ascontiguousarray(par[:, j]) for j in range(m)]
+    addrs = [0 if i in (0, 4) else v.ctypes.data for i, v in enumerate(vert)]
+    out = np.zeros(S * k * cell, dtype=np.uint8)
+    c.decode_host_batch(addrs, cell, S, out.ctypes.data, 2)
+    assert np.array_equal(out, data.reshape(-1))
+    with pytest.raises(H.DeviceError):
+        c.encode_device([0] * k, [0] * k, [0] * m, [0] * m, cell, 1)
+    with pytest.raises(H.DeviceError):
+        c.decode_device([1] * (k + m), [0] * (k + m), [1] * k, [0] * k, cell, 1)
+    c.close()
+
+
+def test_pool_acquire_without_gpu_is_host_only():
+    """hec_coder_acquire(device -1) with no visible GPU hands out a host-only
+    coder; release resets the host limit and ignores a double release."""
+    if gpu_available():
+        pytest.skip("a GPU is visible: acquire(-1) picks it")
+    c = H.Coder(6, 3, -1, pooled=True)
+    assert c.device == H.HEC_DEVICE_HOST
+    raw = c.handle
+    H.lib.hec_coder_release(raw)
+    H.lib.hec_coder_release(raw)  # second release of an idle coder: ignored
+    c._h = None
+    a, b = H.Coder(6, 3, -1, pooled=True), H.Coder(6, 3, -1, pooled=True)
+    assert a.handle.value != b.handle.value, "a double release handed one coder out twice"
+    a.close()
+    b.close()
+    assert H.lib.hec_coder_pool_trim() >= 2
