@@ -21,7 +21,14 @@
 //! `mi355x` feature forwards the reference's `Coder` (rust/patches/
 //! ec_mi355x.patch): the reference builds a Coder per decoded row
 //! (`ec/mod.rs:71`), so it takes an idle engine coder from the process-wide
-//! pool (`hec_coder_acquire`) and gives it back on drop.
+//! pool (`hec_coder_acquire`) and gives it back on drop.  `Coder::new` stays
+//! infallible: without a GPU the pool hands out an engine host-only coder,
+//! and if even that fails the patched `Coder` keeps `None` and runs the
+//! reference CPU path.  The row-batched writer / reader of the same patch
+//! (`rust/src/hdfs/ec_rows.rs`, `block_reader.rs` `read_slice`) pass
+//! `ROWS_PER_CALL` rows per `encode` / `decode` as vertical stripes (shard i's
+//! cells back to back): GF(2^8) coding is bytewise, so that is one call of
+//! `ROWS_PER_CALL` times the cell length, bit-identical to the rows one by one.
 
 use std::ffi::{c_char, c_int, c_void, CStr};
 
@@ -44,6 +51,8 @@ const HEC_ERR_INVALID_ARG: c_int = -1;
 const HEC_ERR_NOT_ENOUGH_SHARDS: c_int = -2;
 const HEC_ERR_UNSUPPORTED_CODEC: c_int = -3;
 const HEC_ERR_CHECKSUM: c_int = -7;
+/// `device` of an engine host-only coder (include/hdfs_ec_amd.h).
+const HEC_DEVICE_HOST: c_int = -2;
 
 unsafe extern "C" {
     fn hec_abi_version() -> c_int;
@@ -54,6 +63,7 @@ unsafe extern "C" {
     fn hec_coder_destroy(c: *mut HecCoder);
     fn hec_coder_acquire(codec: *const c_char, k: usize, m: usize, device: c_int, out: *mut *mut HecCoder) -> c_int;
     fn hec_coder_release(c: *mut HecCoder);
+    fn hec_coder_device(c: *const HecCoder) -> c_int;
     fn hec_encode_rows_host(c: *mut HecCoder, h_data: *const u8, data_len: usize, h_parity: *mut u8,
                             cell_len: usize, chunk_stripes: usize) -> c_int;
     fn hec_decode_rows_host(c: *mut HecCoder, h_vertical: *const *const u8, vertical_len: *const usize,
@@ -239,10 +249,12 @@ fn decode_raw(raw: *mut HecCoder, k: usize, m: usize, data: &mut [Option<Bytes>]
         Some(b) => b.len(),
         None => return Err(err(HEC_ERR_NOT_ENOUGH_SHARDS)),
     };
-    // the engine reads n bytes from every present shard: hold the
-    // reference's equal-length precondition here, before the FFI call
+    // the engine reads n bytes from each of the first k present shards (the
+    // survivors it decodes from): hold the reference's equal-length
+    // precondition over exactly those (matrix.rs:212-216 asserts it over the
+    // k selected rows only; a longer or shorter shard past them is not read)
     assert!(n > 0, "shards must not be empty (matrix.rs:57)");
-    assert!(data.iter().flatten().all(|b| b.len() == n), "equal shard lengths (matrix.rs:215)");
+    assert!(data.iter().flatten().take(k).all(|b| b.len() == n), "equal shard lengths (matrix.rs:215)");
     let ins: Vec<*const u8> = data.iter().map(|d| d.as_ref().map_or(std::ptr::null(), |b| b.as_ptr())).collect();
     let mut rec: Vec<Option<BytesMut>> =
         (0..k + m).map(|i| (i < k && data[i].is_none()).then(|| BytesMut::zeroed(n))).collect();
@@ -264,7 +276,12 @@ fn decode_raw(raw: *mut HecCoder, k: usize, m: usize, data: &mut [Option<Bytes>]
 /// row (ec/mod.rs:71) and per block writer (block_writer.rs:787), so a pool
 /// hit costs a mutex and a vector pop -- no streams, events or buffers are
 /// created (`tests/cpp/shim_replay.c` times 10,000 cycles).  The device is
-/// `HDFS_EC_AMD_DEVICE` if set, else any (round-robin over the visible GPUs).
+/// `HDFS_EC_AMD_DEVICE` if set, else any (round-robin over the visible GPUs;
+/// an engine host-only coder, `HEC_DEVICE_HOST`, when none is visible).  When
+/// the device coder cannot be had (a bad `HDFS_EC_AMD_DEVICE`, device memory
+/// exhausted) `acquire` falls back to a host-only coder, so only a library
+/// that cannot allocate at all returns an error -- which the patched
+/// `Coder::new` turns into its reference CPU path.
 /// Rows below the coder's host limit are coded on the calling thread.
 pub struct PooledCoder {
     raw: *mut HecCoder,
@@ -282,8 +299,20 @@ impl PooledCoder {
             std::env::var("HDFS_EC_AMD_DEVICE").ok().and_then(|v| v.parse().ok()).unwrap_or(-1);
         let name = std::ffi::CString::new(codec).map_err(|_| HdfsError::InvalidArgument(codec.to_string()))?;
         let mut raw = std::ptr::null_mut();
-        check(unsafe { hec_coder_acquire(name.as_ptr(), data_units, parity_units, device, &mut raw) })?;
+        let rc = unsafe { hec_coder_acquire(name.as_ptr(), data_units, parity_units, device, &mut raw) };
+        if rc != HEC_OK {
+            if rc == HEC_ERR_INVALID_ARG || rc == HEC_ERR_UNSUPPORTED_CODEC {
+                return Err(err(rc));
+            }
+            log::warn!("MI355X EC engine: device coder unavailable ({}), host-only coder", err(rc));
+            check(unsafe { hec_coder_acquire(name.as_ptr(), data_units, parity_units, HEC_DEVICE_HOST, &mut raw) })?;
+        }
         Ok(Self { raw, data_units, parity_units })
+    }
+
+    /// True when this coder runs on the engine's host routine (no GPU).
+    pub fn host_only(&self) -> bool {
+        unsafe { hec_coder_device(self.raw) == HEC_DEVICE_HOST }
     }
 
     pub fn encode(&self, data: &[Bytes]) -> Vec<Bytes> {

@@ -76,6 +76,23 @@ int main(void) {
         for (int i = 0; i < K; i++) rin[i] = data + i * CELL;
         for (int j = 0; j < P; j++) rout[j] = par + j * CELL;
         if (hec_encode(h, rin, CELL, rout) != HEC_OK) bad++;
+        /* decode reads only the first k present shards (matrix.rs:212-216):
+         * a present shard past them may be shorter -- here a 1-byte heap
+         * block, which ASan would flag if the engine touched its row */
+        {
+            uint8_t *stub = (uint8_t *)malloc(1), *rec = (uint8_t *)malloc(CELL);
+            const uint8_t *sh[K + P];
+            uint8_t *out[K + P];
+            for (int i = 0; i < K + P; i++) {
+                sh[i] = i == 1 ? 0 : (i < K ? data + i * CELL : par + (i - K) * CELL);
+                out[i] = 0;
+            }
+            sh[K + 1] = stub;
+            out[1] = rec;
+            if (hec_decode(h, sh, CELL, out) != HEC_OK || memcmp(rec, data + CELL, CELL)) bad++;
+            free(stub);
+            free(rec);
+        }
         size_t st[K + P] = {0};
         if (hec_encode_device(h, rin, st, rout, st, CELL, 1, 0) != HEC_ERR_DEVICE) bad++;
         for (int i = 0; i < K + P; i++) free(vert[i]);

@@ -10,11 +10,22 @@
  *                        untouched); HEC_ERR_NOT_ENOUGH_SHARDS -> the shim's
  *                        ErasureCodingError("Not enough valid shards")
  *   encode_rows / decode_rows / GpuGroup -> the batched calls
- *   Coder::new per row (rust/patches/gf256_mi355x.patch: PooledCoder) ->
+ *   Coder::new per row (rust/patches/ec_mi355x.patch: PooledCoder) ->
  *                        hec_coder_acquire / hec_coder_release: 10,000
  *                        acquire / encode / release cycles, timed against
  *                        create / destroy and against one device-routed call
- * Built by __graft_entry__.build(); run by tests/test_shim_replay.py (GPU). */
+ *   the patch's row batching (rust/src/hdfs/ec_rows.rs CellBuffer, and
+ *                        block_reader.rs read_slice): ROWS_PER_CALL rows per
+ *                        call as vertical stripes, then the short last row
+ *                        zero-padded -- byte streams == the oracle's per-row
+ *                        encode / decode
+ *   Coder::new without a GPU -> hec_coder_acquire(-1) = a host-only coder
+ *                        (HEC_DEVICE_HOST); decode reads only the first k
+ *                        present shards (a shorter shard past them is fine,
+ *                        matrix.rs:212-216)
+ * The host-only part runs first and needs no GPU (exit 2 after it when no
+ * device is visible).  Built by __graft_entry__.build(); run by
+ * tests/test_shim_replay.py. */
 #define _POSIX_C_SOURCE 199309L
 #include <stdint.h>
 #include <stdio.h>
@@ -52,15 +63,180 @@ static uint8_t next_byte(void) {
     return (uint8_t)(rng >> 24);
 }
 
-enum { K = 6, M = 3 };
+enum { K = 6, M = 3, ROWS_PER_CALL = 4 };
+
+/* rust/src/hdfs/ec_rows.rs CellBuffer::write + encode over a file of `len`
+ * bytes: every batch of up to ROWS_PER_CALL rows is one encode of the
+ * vertical stripes (whole rows) plus one of the zero-padded short row; the
+ * k + m shard streams are compared with the oracle's row-by-row CellBuffer
+ * encode (block_writer.rs:817-851). */
+static void replay_batched_writer(hec_coder_t *c, size_t cell, size_t len) {
+    uint8_t *file = malloc(len);
+    for (size_t b = 0; b < len; b++) file[b] = next_byte();
+    const size_t row = K * cell;
+    const size_t nrows = (len + row - 1) / row;
+    /* expected streams: shard i = its cells row by row (data at their own
+     * lengths, parity at len(cell 0) of the row) */
+    uint8_t *want[K + M], *got[K + M];
+    size_t want_len[K + M], got_len[K + M];
+    for (int i = 0; i < K + M; i++) {
+        want[i] = malloc(nrows * cell + 1);
+        got[i] = malloc(nrows * cell + 1);
+        want_len[i] = got_len[i] = 0;
+    }
+    uint8_t *pad = calloc(K, cell), *rp[M];
+    for (int j = 0; j < M; j++) rp[j] = malloc(cell);
+    for (size_t r = 0; r < nrows; r++) {
+        const size_t base = r * row, L = len - base < row ? len - base : row;
+        const size_t n0 = L < cell ? L : cell;
+        const uint8_t *in[K];
+        for (int i = 0; i < K; i++) {
+            const size_t have = L > i * cell ? (L - i * cell < cell ? L - i * cell : cell) : 0;
+            memset(pad + i * cell, 0, n0);
+            memcpy(pad + i * cell, file + base + i * cell, have);
+            in[i] = pad + i * cell;
+            memcpy(want[i] + want_len[i], file + base + i * cell, have);
+            want_len[i] += have;
+        }
+        orc_encode(K, M, in, n0, rp);
+        for (int j = 0; j < M; j++) {
+            memcpy(want[K + j] + want_len[K + j], rp[j], n0);
+            want_len[K + j] += n0;
+        }
+    }
+    /* the batched writer */
+    size_t pos = 0;
+    while (pos < len) {
+        const size_t take = len - pos < ROWS_PER_CALL * row ? len - pos : ROWS_PER_CALL * row;
+        const size_t whole = take / row, L = take - whole * row;
+        const size_t slice = whole * cell + (L < cell ? L : cell); /* shard 0's bytes */
+        uint8_t *vd[K], *vp[M];
+        size_t orig[K];
+        for (int i = 0; i < K; i++) {
+            vd[i] = calloc(slice ? slice : 1, 1);
+            orig[i] = 0;
+            for (size_t r = 0; r <= whole; r++) {
+                const size_t rb = r * row + i * cell;
+                if (rb >= take) break;
+                const size_t have = take - rb < cell ? take - rb : cell;
+                memcpy(vd[i] + r * cell, file + pos + rb, have);
+                orig[i] = r * cell + have;
+            }
+        }
+        for (int j = 0; j < M; j++) vp[j] = malloc(slice ? slice : 1);
+        if (whole) {
+            int rc = hec_encode(c, (const uint8_t *const *)vd, whole * cell, vp);
+            CHECK(rc == HEC_OK, "batched encode %s", hec_strerror(rc));
+        }
+        if (slice > whole * cell) {
+            const uint8_t *tin[K];
+            uint8_t *tout[M];
+            for (int i = 0; i < K; i++) tin[i] = vd[i] + whole * cell;
+            for (int j = 0; j < M; j++) tout[j] = vp[j] + whole * cell;
+            int rc = hec_encode(c, tin, slice - whole * cell, tout);
+            CHECK(rc == HEC_OK, "short-row encode %s", hec_strerror(rc));
+        }
+        for (int i = 0; i < K; i++) {
+            memcpy(got[i] + got_len[i], vd[i], orig[i]);
+            got_len[i] += orig[i];
+            free(vd[i]);
+        }
+        for (int j = 0; j < M; j++) {
+            memcpy(got[K + j] + got_len[K + j], vp[j], slice);
+            got_len[K + j] += slice;
+            free(vp[j]);
+        }
+        pos += take;
+    }
+    for (int i = 0; i < K + M; i++) {
+        CHECK(got_len[i] == want_len[i] && memcmp(got[i], want[i], want_len[i]) == 0,
+              "batched writer stream %d (len %zu vs %zu, file %zu)", i, got_len[i], want_len[i], len);
+        free(want[i]);
+        free(got[i]);
+    }
+    for (int j = 0; j < M; j++) free(rp[j]);
+    free(pad);
+    free(file);
+}
+
+/* block_reader.rs read_slice with row batching: R rows whose survivors are
+ * the same are one ec_decode of vertical stripes (every present shard's R
+ * cells back to back) -> one hec_decode of R * cell bytes; each rebuilt
+ * cell == the original. */
+static void replay_batched_reader(hec_coder_t *c, size_t cell, size_t R, int lost_a, int lost_b) {
+    uint8_t *vert[K + M];
+    for (int i = 0; i < K; i++) {
+        vert[i] = malloc(R * cell);
+        for (size_t b = 0; b < R * cell; b++) vert[i][b] = next_byte();
+    }
+    for (int j = 0; j < M; j++) vert[K + j] = malloc(R * cell);
+    for (size_t r = 0; r < R; r++) { /* parity row by row with the oracle */
+        const uint8_t *in[K];
+        uint8_t *out[M];
+        for (int i = 0; i < K; i++) in[i] = vert[i] + r * cell;
+        for (int j = 0; j < M; j++) out[j] = vert[K + j] + r * cell;
+        orc_encode(K, M, in, cell, out);
+    }
+    const uint8_t *sh[K + M];
+    uint8_t *out[K + M];
+    for (int i = 0; i < K + M; i++) {
+        sh[i] = (i == lost_a || i == lost_b) ? NULL : vert[i];
+        out[i] = (i < K && !sh[i]) ? malloc(R * cell) : NULL;
+    }
+    int rc = hec_decode(c, sh, R * cell, out);
+    CHECK(rc == HEC_OK, "batched decode %s", hec_strerror(rc));
+    for (int i = 0; i < K; i++)
+        if (out[i]) {
+            CHECK(memcmp(out[i], vert[i], R * cell) == 0, "batched reader shard %d", i);
+            free(out[i]);
+        }
+    for (int i = 0; i < K + M; i++) free(vert[i]);
+}
+
+/* What needs no GPU: Coder::new's host-only fallback, decode over the first
+ * k present shards only, and the batched writer / reader sequences on it. */
+static void host_only_replay(void) {
+    hec_coder_t *h = NULL;
+    int rc = hec_coder_acquire("rs", K, M, HEC_DEVICE_HOST, &h);
+    CHECK(rc == HEC_OK && hec_coder_device(h) == HEC_DEVICE_HOST, "host-only acquire %s", hec_strerror(rc));
+    if (rc != HEC_OK) return;
+    /* a present shard past the first k may differ in length (never read):
+     * survivors 0,2,3,4,5,6 (n bytes); shard 7 is 1 byte long */
+    const size_t n = 3000;
+    uint8_t *d[K], *p[M], *rec = malloc(n), *stub = malloc(1);
+    for (int i = 0; i < K; i++) {
+        d[i] = malloc(n);
+        for (size_t b = 0; b < n; b++) d[i][b] = next_byte();
+    }
+    for (int j = 0; j < M; j++) p[j] = malloc(n);
+    CHECK(hec_encode(h, (const uint8_t *const *)d, n, p) == HEC_OK, "host-only encode");
+    const uint8_t *sh[K + M] = {d[0], NULL, d[2], d[3], d[4], d[5], p[0], stub, NULL};
+    uint8_t *out[K + M] = {NULL, rec, NULL, NULL, NULL, NULL, NULL, NULL, NULL};
+    CHECK(hec_decode(h, sh, n, out) == HEC_OK && memcmp(rec, d[1], n) == 0, "decode over the first k present");
+    for (int i = 0; i < K; i++) free(d[i]);
+    for (int j = 0; j < M; j++) free(p[j]);
+    free(rec);
+    free(stub);
+    /* the patch's batched writer / reader on the host-only coder */
+    const size_t cell = 4096;
+    const size_t lens[] = {1, 100, cell - 1, cell, K * cell - 4, K * cell, 3 * K * cell + 7, 4 * K * cell,
+                           4 * K * cell + 1, 9 * K * cell + 2 * cell + 5};
+    for (size_t t = 0; t < sizeof lens / sizeof lens[0]; t++) replay_batched_writer(h, cell, lens[t]);
+    replay_batched_reader(h, cell, ROWS_PER_CALL, 0, 4);
+    replay_batched_reader(h, cell, 3, 1, 2);
+    hec_coder_release(h);
+    (void)hec_coder_pool_trim();
+    printf("host-only replay %s\n", failures ? "FAILED" : "ok");
+}
 
 int main(void) {
     CHECK(hec_abi_version() == 5, "ABI %d", hec_abi_version());
+    host_only_replay();
     hec_coder_t *c = NULL;
     int rc = hec_coder_create_codec("rs", K, M, 0, &c);
     if (rc != HEC_OK) {
         fprintf(stderr, "coder create: %s (%s)\n", hec_strerror(rc), hec_last_error());
-        return 2;
+        return failures ? 1 : 2;
     }
     hec_coder_t *bad = NULL;
     CHECK(hec_coder_create_codec("lrc", K, M, 0, &bad) == HEC_ERR_UNSUPPORTED_CODEC && bad == NULL,
@@ -236,6 +412,12 @@ int main(void) {
             free(swant[j]);
         }
     }
+
+    /* the batched writer / reader through the device (1 MiB cells: the
+     * ROWS_PER_CALL-row calls exceed the host limit) */
+    hec_coder_set_host_limit(c, 256 << 10);
+    replay_batched_writer(c, 1 << 20, 4 * K * (1 << 20) + 3 * (1 << 20) + 11);
+    replay_batched_reader(c, 1 << 20, ROWS_PER_CALL, 0, 1);
 
     hec_coder_destroy(c);
     for (int i = 0; i < K; i++) free(data[i]);

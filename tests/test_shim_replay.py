@@ -1,8 +1,9 @@
 """The Rust shim (rust/src/ec/mi355x.rs) cannot be compiled in this image (no
 cargo); tests/cpp/shim_replay.c replays its C call sequence -- zero-length
 error, NOT_ENOUGH_SHARDS mapping, parity and present-data slots left
-untouched, batched rows, the group -- against the engine, checked against the
-CPU oracle."""
+untouched, batched rows, the group, the patch's row-batched writer / reader,
+the host-only Coder::new fallback -- against the engine, checked against the
+CPU oracle.  The host-only part also runs here, without a GPU."""
 import os
 import subprocess
 
@@ -33,3 +34,7 @@ def test_shim_without_device_is_clean_error():
     out = subprocess.run([BIN], capture_output=True, text=True, timeout=120)
     assert out.returncode == 2, (out.returncode, out.stderr[-2000:])
     assert "coder create" in out.stderr
+    # the host-only part ran: Coder::new's fallback coder, decode over the
+    # first k present shards, and the patch's row-batched writer / reader
+    # sequences bit-exact against the oracle's row-by-row results
+    assert "host-only replay ok" in out.stdout, out.stdout + out.stderr[-2000:]
