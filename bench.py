@@ -412,15 +412,64 @@ def per_call_sizes(H, k, m, oracle_lib):
             row[name] = {"encode_us": round(per["encode"] * 1e6, 3), "decode_us": round(per["decode"] * 1e6, 3),
                          "encode_GiBps": round(k * n / per["encode"] / GIB, 3)}
         rows.append(row)
+    # cold: every call codes a different row of a 1 GiB pool (4x the host's
+    # L3), so neither route finds its input in the CPU caches -- the case a
+    # writer or reader streaming a file meets (the hot figures
+    # above flatter the host routine at 1 MiB)
+    cold_sizes = [4096, 65536, 262144, 1 << 20, 4 << 20]
+    pool = np.frombuffer(np.random.default_rng(0xC01D).bytes(1 << 30), dtype=np.uint8)
+    par_pool = np.empty((1 << 30) * m // k, dtype=np.uint8)
+    rec_pool = np.empty((1 << 30) * m // k, dtype=np.uint8)
+    par_pool[::4096] = 0  # touch: first-touch page faults outside the timed calls
+    rec_pool[::4096] = 0
+    for n in cold_sizes:
+        R = (1 << 30) // (k * n)
+        dv = pool[:R * k * n].reshape(R, k, n)
+        pv = par_pool[:R * m * n].reshape(R, m, n)
+        rv = rec_pool[:R * m * n].reshape(R, m, n)
+        ins = [(ctypes.c_void_p * k)(*[dv[r, i].ctypes.data for i in range(k)]) for r in range(R)]
+        outs = [(ctypes.c_void_p * m)(*[pv[r, j].ctypes.data for j in range(m)]) for r in range(R)]
+        shards = [(ctypes.c_void_p * (k + m))(*([0] * m + [dv[r, i].ctypes.data for i in range(m, k)] +
+                                                [pv[r, j].ctypes.data for j in range(m)])) for r in range(R)]
+        recs = [(ctypes.c_void_p * (k + m))(*([rv[r, i].ctypes.data for i in range(m)] + [0] * k)) for r in range(R)]
+        row = next((x for x in rows if x["shard_bytes"] == n), None)
+        if row is None:
+            row = {"shard_bytes": n}
+            rows.append(row)
+        for name, limit in (("engine_device", 0), ("engine_host", 1 << 40)):
+            coder.host_limit = limit
+            per = {}
+            for op in ("encode", "decode"):
+                reps, t, r = 0, 0.0, 0
+                t0 = time.perf_counter()
+                while t < 0.25 or reps < 3:
+                    rc = (lib.hec_encode(coder.handle, ins[r], n, outs[r]) if op == "encode"
+                          else lib.hec_decode(coder.handle, shards[r], n, recs[r]))
+                    assert rc == 0
+                    r = (r + 1) % R
+                    reps += 1
+                    t = time.perf_counter() - t0
+                per[op] = t / reps
+            row.setdefault("cold", {})[name] = {"encode_us": round(per["encode"] * 1e6, 2),
+                                                "decode_us": round(per["decode"] * 1e6, 2),
+                                                "encode_GiBps": round(k * n / per["encode"] / GIB, 3),
+                                                "rows_in_pool": R}
+        assert np.array_equal(rv[0], dv[0, :m]), f"cold per-call decode {n}"
+    del pool, par_pool, rec_pool
+    rows.sort(key=lambda x: x["shard_bytes"])
     coder.host_limit = default_limit
     coder.close()
-    cross = next((r["shard_bytes"] for r in rows if r["engine_device"]["encode_us"] < r["engine_host"]["encode_us"]),
-                 None)
+    cross = next((r["shard_bytes"] for r in rows if "engine_device" in r and
+                  r["engine_device"]["encode_us"] < r["engine_host"]["encode_us"]), None)
+    cross_cold = next((r["shard_bytes"] for r in rows if "cold" in r and
+                       r["cold"]["engine_device"]["encode_us"] < r["cold"]["engine_host"]["encode_us"]), None)
     return {"rows": rows, "default_host_limit": default_limit, "host_isa": H.host_isa(),
+            "device_beats_host_from_cold": cross_cold,
             "device_beats_host_from": cross,
             "note": f"RS({k},{m}), one row per hec_encode / hec_decode (data shards 0..{m - 1} missing), pageable "
                     "buffers; engine = default routing, engine_device = host limit 0, engine_host = the engine's "
-                    "host routine forced; cpu_port = oracle/ec_oracle.c on one core"}
+                    "host routine forced; cpu_port = oracle/ec_oracle.c on one core; cold = each call on a "
+                    "different row of a 1 GiB pool (4x the L3), device forced vs host routine forced"}
 
 
 def ref_cases(args):
@@ -1008,6 +1057,15 @@ def crc_leg(args, H, coder, data, parity, rec, dp, ds, pp, ps, rp, rs, shard_ptr
         decode()
         torch.cuda.synchronize(dev)
 
+    # the plan-specialised fused kernel (jit.hpp: the decode plan's bit-sliced
+    # XOR network compiled with hiprtc), prepared before anything is timed --
+    # as a DataNode's reconstruct worker prepares its plans; HEC_JIT=0 runs the
+    # ahead-of-time v_perm kernel instead (A/B)
+    t_0 = time.perf_counter()
+    lost = [i for i in range(k + m) if shard_ptrs[i] is None]
+    jit_ready = coder.prepare_decode(lost, H.CHECKSUM_CRC32C)
+    jit_ready_c = coder.prepare_decode([0], H.CHECKSUM_CRC32C)  # the corrupt-survivor leg's plan
+    t_prep = time.perf_counter() - t_0
     for fn in (dec_verify, verify_then_decode):
         fn()
     torch.cuda.synchronize(dev)
@@ -1031,6 +1089,10 @@ def crc_leg(args, H, coder, data, parity, rec, dp, ds, pp, ps, rp, rs, shard_ptr
         "read_note": "CRC32C of the k survivors verified against their packet sums while data shards "
                      f"{{{','.join(map(str, miss))}}} are rebuilt (ReadPacket::get_data + ec_decode); "
                      "wall time of the synchronous call incl. the flag read-back",
+        "decode_verify_kernel": ("plan-specialised (bit-sliced network of the decode plan, hiprtc)" if jit_ready
+                                 else "ahead-of-time (v_perm product tables)"),
+        "jit": dict(H.jit_stats(), prepare_s=round(t_prep, 2), ready=bool(jit_ready),
+                    ready_corrupt_leg=bool(jit_ready_c)),
     })
     # corrupt survivors: data shard 0 unavailable (one spare shard beyond k),
     # and a fraction of the stripes gets one flipped byte in its first

@@ -1,7 +1,11 @@
 // checksum.hpp -- chunk-checksum kernel arguments (see checksum.hip).
 #pragma once
 
+#ifndef __HIPCC_RTC__  // hiprtc (jit.cpp) provides the HIP runtime itself
 #include <hip/hip_runtime.h>
+#else
+typedef struct ihipStream_t* hipStream_t;  // the launchers below are host code: declarations only
+#endif
 
 #include <cstdint>
 

@@ -13,7 +13,9 @@
 //                  by the "append 16*(7-i) zero bytes" tables seg[i]
 #pragma once
 
+#ifndef __HIPCC_RTC__  // hiprtc (jit.cpp) provides the HIP runtime itself
 #include <hip/hip_runtime.h>
+#endif
 
 #include <cstdint>
 

@@ -36,6 +36,7 @@
 #include "ec_kernels.hpp"
 #include "gf256.hpp"
 #include "host_gf.hpp"
+#include "jit.hpp"
 
 namespace {
 
@@ -1494,6 +1495,58 @@ int hec_encode_crc_device(hec_coder_t* c, const uint8_t* const* d_data, const si
 // stripes where a survivor failed: drop it, take the next available shard
 // (verifying it first, as read_slice starts the next parity reader), and
 // rebuild every missing or failed data cell of that stripe.
+// ---- plan-time specialisation of the fused decode + verify kernel (jit.hpp) ----
+
+int hec_coder_prepare_decode(hec_coder_t* c, const uint8_t* present, int checksum_type, int* specialised) {
+    if (specialised) *specialised = 0;
+    if (!c || !present) return HEC_ERR_INVALID_ARG;
+    const int kind = crc_kind(checksum_type);
+    if (kind < 0) return HEC_ERR_INVALID_ARG;
+    if (c->device == HEC_DEVICE_HOST) return host_only("hec_coder_prepare_decode");
+    return guarded([&]() -> int {
+        const PlanRef p_ref = cached_plan(c, present);
+        const DecodePlan& p = *p_ref;
+        if (p.status != HEC_OK) return p.status;
+        if (p.missing.empty() || p.missing.size() > size_t(hec::kMaxR)) return int(HEC_OK);  // no fused decode
+        DeviceGuard g(c->device);
+        if (!g.ok) return fail(HEC_ERR_DEVICE, "hipSetDevice", hipErrorInvalidDevice);
+        hec::jit::VerifyKernel vk;
+        const int e = int(p.missing.size());
+        const hec::Tune tn = hec::tune_snapshot();
+        const int slabs = (tn.fused_slabs == 4 || tn.fused_slabs == 8) ? tn.fused_slabs
+                                                                        : hec::jit::default_slabs(int(c->k), e);
+        const bool ok = hec::jit::verify_kernel(c->device, int(c->k), e, kind, slabs, p.matrix.data(), true, &vk);
+        if (specialised) *specialised = ok ? 1 : 0;
+        return int(HEC_OK);
+    });
+}
+
+int hec_jit_warm(size_t data_units, size_t parity_units, const uint8_t* present, int checksum_type) {
+    if (!present || data_units == 0 || data_units > HEC_MAX_DATA_UNITS || parity_units == 0 ||
+        parity_units > HEC_MAX_PARITY_UNITS)
+        return HEC_ERR_INVALID_ARG;
+    const int kind = crc_kind(checksum_type);
+    if (kind < 0) return HEC_ERR_INVALID_ARG;
+    return guarded([&]() -> int {
+        size_t e = 0, surv[HEC_MAX_DATA_UNITS], miss[HEC_MAX_DATA_UNITS];
+        uint8_t mat[HEC_MAX_DATA_UNITS * HEC_MAX_DATA_UNITS];
+        const int rc = hec_decode_plan(data_units, parity_units, present, &e, surv, miss, mat);
+        if (rc != HEC_OK) return rc;
+        const size_t k = data_units;
+        if (e == 0 || e > size_t(hec::kMaxR) || !(k == 2 || k == 3 || k == 6 || k == 10)) return int(HEC_ERR_INVALID_ARG);
+        return hec::jit::warm(int(k), int(e), kind, hec::jit::default_slabs(int(k), int(e)), mat) ? int(HEC_OK)
+                                                         : fail(HEC_ERR_DEVICE, "hiprtc compile", hipErrorNotSupported);
+    });
+}
+
+void hec_jit_stats(uint64_t* compiled, uint64_t* from_disk, uint64_t* failed, uint64_t* launches) {
+    const hec::jit::Stats st = hec::jit::stats();
+    if (compiled) *compiled = st.compiled;
+    if (from_disk) *from_disk = st.from_disk;
+    if (failed) *failed = st.failed;
+    if (launches) *launches = st.launches;
+}
+
 int hec_decode_verify_device(hec_coder_t* c, int checksum_type, const uint8_t* const* d_shards,
                              const size_t* shard_strides, uint8_t* const* d_out, const size_t* out_strides,
                              size_t cell_len, size_t stripes, size_t bytes_per_checksum, const uint8_t* d_sums,

@@ -2,7 +2,11 @@
 // stripe-cell matrix multiply (see ec_kernels.hip).
 #pragma once
 
+#ifndef __HIPCC_RTC__  // hiprtc (jit.cpp) provides the HIP runtime itself
 #include <hip/hip_runtime.h>
+#else
+typedef struct ihipStream_t* hipStream_t;  // the launchers below are host code: declarations only
+#endif
 
 #include <cstdint>
 

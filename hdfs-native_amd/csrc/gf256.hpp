@@ -6,17 +6,19 @@
 // 0b1_0001_1101)).  add = XOR, mul via exp/log over generator 2.
 #pragma once
 
+#ifndef __HIPCC_RTC__  // hiprtc (jit.cpp) compiles only the tables below
 #include <array>
 #include <cstddef>
-#include <cstdint>
 #include <cstring>
 #include <vector>
+#endif
+#include <cstdint>
 
 namespace hec {
 
 struct GfTables {
-    std::array<uint8_t, 512> exp{};
-    std::array<uint8_t, 256> log{};
+    uint8_t exp[512]{};
+    uint8_t log[256]{};
     constexpr GfTables() {
         unsigned x = 1;
         for (int i = 0; i < 255; i++) {
@@ -36,6 +38,8 @@ constexpr uint8_t gf_mul(uint8_t a, uint8_t b) {
 }
 constexpr uint8_t gf_inv(uint8_t a) { return a == 0 ? 0 : kGf.exp[255 - kGf.log[a]]; }
 constexpr uint8_t gf_div(uint8_t a, uint8_t b) { return gf_mul(a, gf_inv(b)); }
+
+#ifndef __HIPCC_RTC__
 
 // Coder::gen_rs_matrix (rust/src/ec/gf256.rs:40-57): (k+m) x k, row-major.
 // Identity on top; parity row r, column c = 1 / (r XOR c) (Hadoop
@@ -138,5 +142,7 @@ inline std::array<uint32_t, 8> perm_table_words(uint8_t c) {
             pack(p1[0], p1[1], p1[2], p1[3]), pack(p1[4], p1[5], p1[6], p1[7]),
             pack(p2[0], p2[1], p2[2], p2[3]), 0u, 0u, 0u};
 }
+
+#endif  // __HIPCC_RTC__
 
 }  // namespace hec

@@ -5,7 +5,9 @@
 // 16-B non-temporal accesses.  See ec_kernels.hip for the design.
 #pragma once
 
+#ifndef __HIPCC_RTC__  // hiprtc (jit.cpp) provides the HIP runtime itself
 #include <hip/hip_runtime.h>
+#endif
 
 #include <cstdint>
 

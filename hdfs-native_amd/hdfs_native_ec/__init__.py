@@ -53,6 +53,7 @@ EXPORTS = [
     "hec_device_alloc", "hec_device_free", "hec_device_numa_node", "hec_host_alloc", "hec_host_free",
     "hec_coder_acquire", "hec_coder_release", "hec_coder_pool_trim", "hec_coder_set_host_limit",
     "hec_coder_host_limit", "hec_gf_matmul_host", "hec_host_isa", "hec_encode_rows_host",
+    "hec_coder_prepare_decode", "hec_jit_warm", "hec_jit_stats",
     "hec_encode_rows_workspace_size", "hec_encode_rows_device", "hec_decode_rows_host",
 ]
 
@@ -154,6 +155,9 @@ def _load(path: str = LIB_PATH) -> ctypes.CDLL:
         "hec_coder_pool_trim": ([], S),
         "hec_coder_set_host_limit": ([P, S], I),
         "hec_coder_host_limit": ([P], S),
+        "hec_coder_prepare_decode": ([P, P, I, P], I),
+        "hec_jit_warm": ([S, S, P, I], I),
+        "hec_jit_stats": ([P, P, P, P], None),
         "hec_gf_matmul_host": ([P, S, S, PP, PP, S], I),
         "hec_host_isa": ([], ctypes.c_char_p),
         "hec_encode_rows_host": ([P, P, S, P, S, S], I),
@@ -439,6 +443,16 @@ class Coder:
             if data[i] is None:
                 data[i] = outs[i].tobytes()
 
+    def prepare_decode(self, missing: Sequence[int], checksum_type: int = 2) -> bool:
+        """hec_coder_prepare_decode: compile the plan-specialised fused decode
+        + verify kernel for shards `missing` unavailable, now; True when it
+        is ready (see include/hdfs_ec_amd.h)."""
+        n = self.data_units + self.parity_units
+        present = (ctypes.c_uint8 * n)(*[0 if i in set(missing) else 1 for i in range(n)])
+        flag = ctypes.c_int(0)
+        _check(self._lib.hec_coder_prepare_decode(self._h, present, checksum_type, ctypes.byref(flag)))
+        return bool(flag.value)
+
     # -- device-resident batched API ----------------------------------------
     def encode_device(self, data_ptrs, data_strides, parity_ptrs, parity_strides, cell_len, stripes,
                       stream: int = 0) -> None:
@@ -533,6 +547,20 @@ class Coder:
 
 
 # ---- torch helpers (device memory comes from torch; plumbing only) --------
+
+def jit_warm(k: int, m: int, missing: Sequence[int], checksum_type: int = 2) -> None:
+    """hec_jit_warm: the specialised decode + verify kernel for this plan into
+    the code-object caches (no device needed)."""
+    present = (ctypes.c_uint8 * (k + m))(*[0 if i in set(missing) else 1 for i in range(k + m)])
+    _check(lib.hec_jit_warm(k, m, present, checksum_type))
+
+
+def jit_stats() -> dict:
+    """hec_jit_stats: process totals of the plan-time JIT."""
+    v = [ctypes.c_uint64(0) for _ in range(4)]
+    lib.hec_jit_stats(*[ctypes.byref(x) for x in v])
+    return dict(zip(("compiled", "from_disk", "failed", "launches"), (x.value for x in v)))
+
 
 def stripe_layout_ptrs(t, units: int):
     """For a uint8 tensor [stripes, units, cell] return (ptrs, strides)."""

@@ -282,6 +282,31 @@ int hec_decode_verify_device(hec_coder_t *coder, int checksum_type, const uint8_
                              size_t cell_len, size_t stripes, size_t bytes_per_checksum, const uint8_t *d_sums,
                              uint8_t *d_bad, void *hip_stream);
 
+/* Plan-time specialisation of the fused decode + verify pass.
+ * That pass rebuilds the missing data rows with the decode plan's matrix,
+ * known only at run time, through v_perm product tables.  For a plan the
+ * engine meets, it generates the matrix's bit-sliced XOR network and compiles
+ * the same kernel with it (hiprtc, loaded with dlopen): about a third fewer
+ * VALU ops for RS(6,3) with 3 rows lost.  By default the compile runs on a
+ * background thread the first time a plan is launched, and launches use the
+ * ahead-of-time kernel until it is ready (identical results).  Code objects
+ * are cached per process and on disk ($HEC_JIT_CACHE, default
+ * ~/.cache/hdfs_ec_amd/jit; "" = none).  HEC_JIT=0 disables it, HEC_JIT=sync
+ * compiles on first use.
+ *   hec_coder_prepare_decode: compile (or load) the specialised kernel for the
+ *     presence mask present[k+m] and checksum type now, synchronously, on the
+ *     coder's device; *specialised = 1 when it is ready (0: not available --
+ *     no hiprtc, JIT off, no fused shape for this plan, or nothing missing).
+ *   hec_jit_warm: the same into the caches only, no device needed (install-
+ *     time warm-up).  HEC_ERR_INVALID_ARG for a plan without a fused kernel
+ *     (k not in {2,3,6,10}, no or more than 4 data shards missing),
+ *     HEC_ERR_DEVICE when hiprtc is absent or the compile fails.
+ *   hec_jit_stats: kernels compiled, loaded from the disk cache, failed,
+ *     and launches that ran a specialised kernel (process totals). */
+int hec_coder_prepare_decode(hec_coder_t *coder, const uint8_t *present, int checksum_type, int *specialised);
+int hec_jit_warm(size_t data_units, size_t parity_units, const uint8_t *present, int checksum_type);
+void hec_jit_stats(uint64_t *compiled, uint64_t *from_disk, uint64_t *failed, uint64_t *launches);
+
 /* Encode plus CRC32C of the k data and m parity cells (shard order
  * 0..k+m-1, same output layout as hec_crc32c_device): everything a striped
  * writer needs to emit its k+m packet streams.  One fused pass (the

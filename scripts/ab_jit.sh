@@ -1,0 +1,37 @@
+#!/bin/bash
+# GPU box, one lease: same-box A/B of the fused decode + verify kernel --
+# ahead-of-time v_perm kernel (HEC_JIT=0) vs the plan-specialised (JIT)
+# kernel at 8 and 4 slabs (measurement build, tune key 10) -- each variant
+# under rocprofv3 --kernel-trace --stats (no counters), alternated twice.
+# Usage: ab_jit.sh OUTDIR [extra bench args]
+set -o pipefail
+o=${1:-gpurun_out/ab_jit}; shift
+mkdir -p "$o"; export TMPDIR=/tmp
+B="--crc --corrupt none --steps 10 --warmup 3 --extra-configs 0 --cpu-seconds 0 --host-path 0 --verify sample $*"
+for rep in 1 2; do
+  for v in aot jit8 jit4; do
+    case $v in
+      aot) E="HEC_JIT=0"; T="";;
+      jit8) E="HEC_JIT=async"; T="--tune 10=8";;
+      jit4) E="HEC_JIT=async"; T="--tune 10=4";;
+    esac
+    d="$o/$v.$rep"
+    export $E
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$d" -o run --output-format csv -- \
+      python3 -u bench.py $B $T > "$d.log" 2>&1 || { tail -20 "$d.log"; exit 2; }
+    unset HEC_JIT
+    python3 - "$d" "$v" "$d.log" <<'PY'
+import csv, glob, json, sys
+d, v, log = sys.argv[1:]
+rows = []
+for p in glob.glob(d + "/**/*kernel_stats.csv", recursive=True):
+    rows += list(csv.DictReader(open(p)))
+line = [l for l in open(log) if l.startswith("{") and '"metric"' in l][-1]
+c = json.loads(line).get("crc32c", {})
+for r in rows:
+    if "gf_fused_crc" in r["Name"] and ", true," in r["Name"]:
+        print(v, round(float(r["AverageNs"]) / 1e6, 4), "ms x", r["Calls"], r["Name"][:110])
+print(v, "leg", c.get("decode_verify_ms"), "frac", c.get("decode_verify_frac"), c.get("decode_verify_kernel"), c.get("jit"))
+PY
+  done
+done

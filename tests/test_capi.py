@@ -317,3 +317,32 @@ def test_pool_acquire_without_gpu_is_host_only():
     a.close()
     b.close()
     assert H.lib.hec_coder_pool_trim() >= 2
+
+
+# ---- plan-time JIT (hiprtc runs on the CPU: no GPU needed to compile) -------
+
+def test_jit_warm_compiles_and_caches(tmp_path):
+    """hec_jit_warm compiles the plan-specialised decode + verify kernel with
+    hiprtc into the disk cache; a second process finds it there.  Shapes:
+    RS(6,3) with data 0..2 lost (8 slabs) and RS(10,4) with 4 lost (4 slabs,
+    inputs in pairs), CRC32C; a plan without a fused kernel is refused."""
+    import json
+    import subprocess
+    import sys
+    code = ("import json, sys; sys.path.insert(0, %r); import hdfs_native_ec as H; "
+            "H.jit_warm(6, 3, [0, 1, 2]); H.jit_warm(10, 4, [0, 1, 2, 3], 2); "
+            "print(json.dumps(H.jit_stats()))") % os.path.join(ROOT, "hdfs-native_amd")
+    env = dict(os.environ, HEC_JIT_CACHE=str(tmp_path))
+    first = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert first.returncode == 0, first.stderr[-3000:]
+    s1 = json.loads(first.stdout.strip().splitlines()[-1])
+    assert s1["compiled"] == 2 and s1["failed"] == 0, s1
+    assert len(list(tmp_path.glob("dv-*.co"))) == 2
+    second = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert second.returncode == 0, second.stderr[-3000:]
+    s2 = json.loads(second.stdout.strip().splitlines()[-1])
+    assert s2["from_disk"] == 2 and s2["compiled"] == 0, s2
+    with pytest.raises(ValueError):
+        H.jit_warm(5, 3, [0])  # k = 5: no fused decode + verify kernel
+    with pytest.raises(ValueError):
+        H.jit_warm(6, 3, [6])  # only parity lost: nothing to rebuild

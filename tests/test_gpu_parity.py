@@ -1035,6 +1035,59 @@ def decode_verify_body(dev, c_oracle, ctype, k, m, cell, bpc, missing, missing_p
                 assert not o[s, i].any(), (s, i)  # present + verified: not copied
 
 
+JIT_CASES = [c for c in VERIFY_CASES if c[0] in (2, 3, 6, 10) and c[3] == 512 and 1 <= len(c[4]) <= 4]
+
+
+@pytest.mark.parametrize("ctype", CKSUM_TYPES)
+@pytest.mark.parametrize("k,m,cell,bpc,missing,missing_parity", JIT_CASES)
+def test_decode_verify_jit_specialised_vs_oracle(dev, c_oracle, ctype, k, m, cell, bpc, missing, missing_parity):
+    """The plan-specialised fused decode + verify kernel (jit.cpp: the decode
+    plan's bit-sliced XOR network compiled with hiprtc, prepared
+    synchronously) over the same cases as the ahead-of-time kernel: rebuilt
+    data, bad flags and the error as the oracle's read_slice restatement; the
+    launch counter proves the specialised kernel ran."""
+    cod = H.Coder(k, m, 0)
+    lost = list(missing) + [k + j for j in missing_parity]
+    assert cod.prepare_decode(lost, ctype), "hiprtc unavailable on the GPU box"
+    before = H.jit_stats()["launches"]
+    decode_verify_body(dev, c_oracle, ctype, k, m, cell, bpc, missing, missing_parity, cod)
+    assert H.jit_stats()["launches"] > before
+    cod.close()
+
+
+def test_decode_verify_jit_full_size(dev):
+    """RS(6,3) 1 MiB x 64 with data shards {0,1,2} lost through the
+    specialised kernel: rebuilt cells == the originals, no flags; then with
+    {0,1} lost (one spare survivor), one flipped byte in survivor 4 of stripe
+    7 is flagged and routed around (parity 2 read instead, shard 4 rebuilt
+    in place)."""
+    k, m, cell, S = 6, 3, 1 << 20, 64
+    c = H.Coder(k, m, 0)
+    assert c.prepare_decode([0, 1, 2]) and c.prepare_decode([0, 1])
+    d = torch.empty((S, k, cell), dtype=torch.uint8, device=dev)
+    d.random_(0, 256, generator=torch.Generator(device=dev).manual_seed(17))
+    p = torch.empty((S, m, cell), dtype=torch.uint8, device=dev)
+    H.encode_batch(c, d, p)
+    sums = H.checksum_batch(c, torch.cat([d, p], dim=1), H.CHECKSUM_CRC32C, 512)
+    before = H.jit_stats()["launches"]
+    out = torch.zeros_like(d)
+    bad = H.decode_verify_batch(c, d, p, [0, 1, 2], sums, out)
+    torch.cuda.synchronize()
+    assert H.jit_stats()["launches"] == before + 1
+    assert not bad.any()
+    assert torch.equal(out[:, :3], d[:, :3])
+    d[7, 4, 777] ^= 0x10
+    out.zero_()
+    before = H.jit_stats()["launches"]
+    bad = H.decode_verify_batch(c, d, p, [0, 1], sums, out)
+    torch.cuda.synchronize()
+    assert H.jit_stats()["launches"] == before + 1
+    assert bad.nonzero().tolist() == [[7, 4]]
+    d[7, 4, 777] ^= 0x10
+    assert torch.equal(out[:, :2], d[:, :2]) and torch.equal(out[7, 4], d[7, 4])
+    c.close()
+
+
 @pytest.mark.parametrize("ctype", CKSUM_TYPES)
 def test_decode_verify_null_type_is_plain_decode(dev, c_oracle, ctype):
     k, m, cell, S = 6, 3, 1 << 14, 3

@@ -29,3 +29,17 @@ def test_bitslice_networks_vs_oracle():
     out = subprocess.run([BSL_BIN], capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stderr[-4000:]
     assert "ok" in out.stdout
+
+
+NET_BIN = os.path.join(PKG_DIR, "build", "xor_net_check")
+
+
+def test_plan_time_xor_networks_every_decode_plan():
+    """The networks the JIT-specialised decode + verify kernel runs
+    (csrc/xor_net.hpp): every decode plan of RS(3,2), RS(6,3) and RS(10,4)
+    and random 1..4-row matrices, evaluated on bit-sliced cells on the host,
+    equal the oracle's decode / multiply."""
+    subprocess.check_call(["make", "-s", "-C", PKG_DIR, "build/xor_net_check"])
+    out = subprocess.run([NET_BIN], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stdout[-4000:] + out.stderr[-4000:]
+    assert "xor net ok" in out.stdout
