@@ -12,7 +12,8 @@ for path in glob.glob(os.path.join(sys.argv[1], "**", "*counter_collection.csv")
         for r in csv.DictReader(f):
             name = r.get("Kernel_Name", "")
             short = name[:name.rfind("(")] if name.endswith(")") else name  # drop the argument list
-            short = short.split("::")[-1][:48]
+            i = min([short.find(t) for t in ("gf_", "checksum") if t in short] or [0])
+            short = short[i:][:100]  # kernel template name, namespaces of its arguments kept
             acc[(short, r["Counter_Name"])].append(float(r["Counter_Value"]))
 for (k, c), v in sorted(acc.items()):
-    print(f"{k:50s} {c:24s} n={len(v):3d} mean={sum(v) / len(v):.4g}")
+    print(f"{k:100s} {c:24s} n={len(v):3d} mean={sum(v) / len(v):.4g}")
