@@ -12,13 +12,16 @@ it instead of the v_perm product tables.  The kernel streams one input shard
 at a time, so the network is emitted per input: input i's 8 planes are folded
 into the r*8 accumulator planes; pairs of input planes that several outputs
 share are XORed once first (greedy common-subexpression pairing, Paar's
-heuristic), then every accumulator absorbs its terms two at a time through a
-3-input XOR.  Input 0 initialises the accumulators.
+heuristic, extended to triples: a 3-input XOR temp removes two terms per
+output for one op; seeded randomised greedy passes, the cheapest kept), then
+every accumulator absorbs its terms two at a time through a 3-input XOR.
+Input 0 initialises the accumulators.
 
 usage: python3 scripts/gen_xor_networks.py > hdfs-native_amd/csrc/xor_networks.hpp
 """
 import collections
 import itertools
+import random
 
 
 def gf_mul(a, b):
@@ -47,41 +50,86 @@ def bit_rows(c):
     return [{b for b in range(8) if (cols[b] >> t) & 1} for t in range(8)]
 
 
-def input_network(coefs):
-    """coefs[j] = coefficient of this input in parity row j.  Returns
-    (temps, absorb): temps = [(name, a, b)] 2-input XORs of planes/temps;
-    absorb[o] = list of operand names output plane o = 8*j + t takes in."""
-    outs = []
-    for c in coefs:
-        outs.extend(set(f"p[{b}]" for b in s) for s in bit_rows(c))
+def absorb_cost(n, first):
+    """VALU ops to fold n terms into an output plane with 3-input XORs; input
+    0 initialises the plane (one op takes up to three terms)."""
+    if first:
+        return 0 if n <= 1 else 1 + (max(0, n - 3) + 1) // 2
+    return (n + 1) // 2
+
+
+def greedy_network(outs, first, rng=None, temp=0.0):
+    """Repeatedly factor out the pair or triple of operands whose shared XOR
+    saves the most ops over the outputs holding it (a temp costs one op; a
+    triple removes two terms per output, a pair one); ties and near-ties
+    broken by rng.  Returns (temps, absorb)."""
+    outs = [set(o) for o in outs]
     temps = []
     while True:
         cnt = collections.Counter()
         for o in outs:
-            for a, b in itertools.combinations(sorted(o), 2):
-                cnt[(a, b)] += 1
-        if not cnt:
+            so = sorted(o)
+            for t in itertools.combinations(so, 2):
+                cnt[t] += 1
+            for t in itertools.combinations(so, 3):
+                cnt[t] += 1
+        scored = []
+        for t, n in cnt.items():
+            if n < 2:
+                continue
+            save = -1
+            for o in outs:
+                if all(x in o for x in t):
+                    save += absorb_cost(len(o), first) - absorb_cost(len(o) - len(t) + 1, first)
+            if save > 0:
+                scored.append((save, t))
+        if not scored:
             break
-        (a, b), n = cnt.most_common(1)[0]
-        if n < 2:
-            break
+        best = max(sv for sv, _ in scored)
+        floor = best - 1 if rng is not None and rng.random() < temp else best
+        pool = sorted(t for sv, t in scored if sv >= floor)
+        pick = rng.choice(pool) if rng is not None else pool[0]
         name = f"t{len(temps)}"
-        temps.append((name, a, b))
+        temps.append((name,) + tuple(pick))
         for o in outs:
-            if a in o and b in o:
-                o -= {a, b}
+            if all(x in o for x in pick):
+                o.difference_update(pick)
                 o.add(name)
     return temps, [sorted(o) for o in outs]
 
 
+def input_cost(temps, absorb, first):
+    return len(temps) + sum(absorb_cost(len(t), first) for t in absorb)
+
+
+def input_network(coefs, first, restarts=48):
+    """coefs[j] = coefficient of this input in parity row j.  Returns
+    (temps, absorb): temps = [(name, a, b[, c])] 2- or 3-input XORs of
+    planes / earlier temps; absorb[o] = the operands output plane o = 8*j + t
+    takes in.  The deterministic greedy plus seeded randomised passes; the
+    cheapest network wins (the plan-time generator, csrc/xor_net.hpp, does the
+    same for decode matrices)."""
+    outs = []
+    for c in coefs:
+        outs.extend(set(f"p[{b}]" for b in s) for s in bit_rows(c))
+    best = greedy_network(outs, first)
+    rng = random.Random(0x5EED + len(coefs))
+    for _ in range(restarts):
+        cand = greedy_network(outs, first, rng, 0.3)
+        if input_cost(*cand, first) < input_cost(*best, first):
+            best = cand
+    return best
+
+
 def emit_input(k, m, i, coefs):
-    temps, absorb = input_network(coefs)
+    temps, absorb = input_network(coefs, i == 0)
     n = 8 * m
     lines = [f"template <> __host__ __device__ __forceinline__ void rs_absorb<{k}, {m}, {i}>("
              f"const uint32_t (&p)[8], uint32_t (&acc)[{n}]) {{"]
     ops = 0
-    for name, a, b in temps:
-        lines.append(f"    const uint32_t {name} = {a} ^ {b};")
+    for name, *ops_in in temps:
+        expr = f"x3({ops_in[0]}, {ops_in[1]}, {ops_in[2]})" if len(ops_in) == 3 else f"{ops_in[0]} ^ {ops_in[1]}"
+        lines.append(f"    const uint32_t {name} = {expr};")
         ops += 1
     for o, terms in enumerate(absorb):
         terms = list(terms)
