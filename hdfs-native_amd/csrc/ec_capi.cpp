@@ -94,7 +94,11 @@ struct hec_coder {
     // hec_encode / hec_decode rows of at most this many bytes per shard are
     // coded on the host (hec::host), larger ones go through the device
     std::atomic<size_t> host_limit{kDefaultHostLimit};
-    static constexpr size_t kDefaultHostLimit = size_t(256) << 10;
+    // Every row on pageable buffers: the host routine beat the device route at
+    // every size measured, cold (rows from a 1 GiB pool) and hot, 4 KiB to
+    // 4 MiB per shard (profiles/r04d/); set a limit to route
+    // longer rows through the device.
+    static constexpr size_t kDefaultHostLimit = SIZE_MAX;
 
     // Decode plans keyed by presence bitmask (k+m <= 48), bounded: at most
     // kPlanCacheMax entries; past that the least recently used eighth is
@@ -359,7 +363,7 @@ int call_through_device(hec_coder* c, const uint8_t* const* in, size_t nin, uint
 int code_row(hec_coder* c, const uint8_t* mat, const uint64_t* aff, const uint8_t* const* in, size_t nin,
              uint8_t* const* out, size_t nout, size_t n) {
     if (c->device == HEC_DEVICE_HOST || n <= c->host_limit.load(std::memory_order_relaxed)) {
-        hec::host::gf_matmul(mat, aff, nout, nin, in, out, n);
+        hec::host::gf_matmul_split(mat, aff, nout, nin, in, out, n);
         return HEC_OK;
     }
     std::lock_guard<std::mutex> lk(c->host_mu);
@@ -672,7 +676,7 @@ int hec_gf_matmul_host(const uint8_t* matrix, size_t rows, size_t cols, const ui
     for (size_t j = 0; j < rows; j++)
         if (!out[j]) return HEC_ERR_INVALID_ARG;
     return guarded([&] {
-        hec::host::gf_matmul(matrix, nullptr, rows, cols, in, out, len);
+        hec::host::gf_matmul_split(matrix, nullptr, rows, cols, in, out, len);
         return int(HEC_OK);
     });
 }
@@ -988,7 +992,7 @@ int hec_encode_host_batch(hec_coder_t* c, const uint8_t* h_data, uint8_t* h_pari
             for (size_t s = 0; s < stripes; s++) {
                 for (size_t i = 0; i < k; i++) in[i] = h_data + (s * k + i) * cell_len;
                 for (size_t j = 0; j < m; j++) out[j] = h_parity + (s * m + j) * cell_len;
-                hec::host::gf_matmul(c->enc.data() + k * k, c->enc_aff.data(), m, k, in, out, cell_len);
+                hec::host::gf_matmul_split(c->enc.data() + k * k, c->enc_aff.data(), m, k, in, out, cell_len);
             }
             return int(HEC_OK);
         });
@@ -1111,7 +1115,7 @@ int hec_decode_host_batch(hec_coder_t* c, const uint8_t* const* h_vertical, size
                 for (size_t r = 0; r < rows; r++) {
                     for (size_t i = 0; i < k; i++) in[i] = h_vertical[p.survivors[i]] + r * cell_len;
                     for (size_t i = 0; i < e; i++) out[i] = h_file + (r * k + p.missing[i]) * cell_len;
-                    hec::host::gf_matmul(p.matrix.data(), p.aff.data(), e, k, in, out, cell_len);
+                    hec::host::gf_matmul_split(p.matrix.data(), p.aff.data(), e, k, in, out, cell_len);
                 }
                 copy_rows(own_a, own_b);
                 return int(HEC_OK);
@@ -1515,7 +1519,10 @@ int hec_coder_prepare_decode(hec_coder_t* c, const uint8_t* present, int checksu
         const hec::Tune tn = hec::tune_snapshot();
         const int slabs = (tn.fused_slabs == 4 || tn.fused_slabs == 8) ? tn.fused_slabs
                                                                         : hec::jit::default_slabs(int(c->k), e);
-        const bool ok = hec::jit::verify_kernel(c->device, int(c->k), e, kind, slabs, p.matrix.data(), true, &vk);
+        const int pfd = tn.jit_pfd == 2 && slabs == 4 ? 2 : hec::jit::default_pfd(int(c->k), e);
+        const int wpe = tn.fused_wpe == 3 && slabs == 4 ? 3 : 2;
+        const bool ok =
+            hec::jit::verify_kernel(c->device, int(c->k), e, kind, slabs, wpe, pfd, p.matrix.data(), true, &vk);
         if (specialised) *specialised = ok ? 1 : 0;
         return int(HEC_OK);
     });
@@ -1534,7 +1541,8 @@ int hec_jit_warm(size_t data_units, size_t parity_units, const uint8_t* present,
         if (rc != HEC_OK) return rc;
         const size_t k = data_units;
         if (e == 0 || e > size_t(hec::kMaxR) || !(k == 2 || k == 3 || k == 6 || k == 10)) return int(HEC_ERR_INVALID_ARG);
-        return hec::jit::warm(int(k), int(e), kind, hec::jit::default_slabs(int(k), int(e)), mat) ? int(HEC_OK)
+        return hec::jit::warm(int(k), int(e), kind, hec::jit::default_slabs(int(k), int(e)), 2,
+                              hec::jit::default_pfd(int(k), int(e)), mat) ? int(HEC_OK)
                                                          : fail(HEC_ERR_DEVICE, "hiprtc compile", hipErrorNotSupported);
     });
 }

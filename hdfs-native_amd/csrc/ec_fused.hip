@@ -306,6 +306,17 @@ const void* encode_fn(int slabs, int scheme, int wpe, bool pair, bool bsl) {
     // bit-sliced parity at the default slab count (tune key 22 = 1: off)
     if (bsl && scheme == 12 && wpe != 3 && slabs == fused_slabs(K, R) && (slabs == 8 || pair))
         return encode_bsl<K, R, 12, fused_slabs(K, R) == 4>(true);
+    // bit-sliced parity at 4 slabs with the inputs in pairs where the default
+    // is 8 (RS(3,2), RS(6,3); tune key 10 = 4), one or two pairs loaded ahead
+    // (key 24 = 2): the measurement twin of the specialised decode + verify shapes
+    if constexpr (bsl_shape<K, R>() && fused_slabs(K, R) == 8) {
+        if (bsl && scheme == 12 && wpe == 2 && slabs == 4 && pair)
+            return tune_snapshot().jit_pfd == 2
+                       ? reinterpret_cast<const void*>(
+                             &gf_fused_crc<K, R, 4, 12, crc::kCrc32c, false, 2, true, RsNet<K, R>, 2>)
+                       : reinterpret_cast<const void*>(
+                             &gf_fused_crc<K, R, 4, 12, crc::kCrc32c, false, 2, true, RsNet<K, R>, 1>);
+    }
     // fold depth 16 / 20 dwords (key 11 = 10 / 11), RS(6,3) and RS(10,4) only
     if constexpr ((K == 6 && R == 3) || (K == 10 && R == 4)) {
         if ((scheme == 13 || scheme == 14) && bsl && wpe != 3 && slabs == fused_slabs(K, R) && (slabs == 8 || pair))
@@ -468,12 +479,15 @@ int launch_fused(const MatmulArgs& in, const FusedCrcArgs& cs, bool verify, int 
     // count is the ahead-of-time kernel's (measurement build: tune key 10)
     jit::VerifyKernel vk;
     int use_slabs = slabs;
-    if (verify && !split && scheme == 12 && wpe == 2) {
+    if (verify && !split && scheme == 12) {
         uint8_t mat[kMaxR * kMaxK];
         for (int j = 0; j < a.r; j++)
             for (int i = 0; i < a.k; i++) mat[j * a.k + i] = a.coef[j * kMaxK + i];
         const int js = (tn.fused_slabs == 4 || tn.fused_slabs == 8) ? tn.fused_slabs : jit::default_slabs(a.k, a.r);
-        if (jit::verify_kernel(device, a.k, a.r, cs.kind, js, mat, false, &vk)) use_slabs = js;
+        const int jp = tn.jit_pfd == 2 && js == 4 ? 2 : jit::default_pfd(a.k, a.r);
+        // (3 waves per SIMD: tune key 16 = 3 with key 10 = 4; the launch's
+        // `waves` and grid already follow wpe)
+        if (jit::verify_kernel(device, a.k, a.r, cs.kind, js, wpe, jp, mat, false, &vk)) use_slabs = js;
     }
     const uint64_t chunks = a.cell_len / 16;
     // split: 4 GF waves x 8 KiB per tile; else waves x slabs x 1 KiB

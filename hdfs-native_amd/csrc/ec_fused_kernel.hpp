@@ -76,7 +76,7 @@ __device__ __forceinline__ const crc::Tables<KIND>& fused_tables() {
 // tables: RS(6,3) 650 instead of 960 VALU per 8 dwords of every shard,
 // RS(10,4) 1155 instead of 2000.  The kernel is VALU-issue bound.
 template <int K, int R, int SLABS, int SCHEME, int KIND, bool VERIFY, int WPE = 2, bool PAIR = false,
-          class NET = PermNet>
+          class NET = PermNet, int PFD = 1>
 __global__ __launch_bounds__(crcdev::sliced(SCHEME) ? 128 * WPE * (WPE - 1) : 512)
     __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void gf_fused_crc(
     MatmulArgs a, FusedCrcArgs cs) {
@@ -230,7 +230,44 @@ __global__ __launch_bounds__(crcdev::sliced(SCHEME) ? 128 * WPE * (WPE - 1) : 51
         u32x4 x[SLABS], xn[SLABS];
 #pragma unroll
         for (int u = 0; u < SLABS; u++) x[u] = load16<true>(a.in[0] + (uint64_t(stripe) * a.in_stride[0] + wbyte) + voff[u]);
-        if constexpr (PAIR && SPR == 2 && PF) {
+        auto load_in = [&](int i, u32x4 (&dst)[SLABS]) {
+#pragma unroll
+            for (int u = 0; u < SLABS; u++)
+                dst[u] = load16<true>(a.in[i] + (uint64_t(stripe) * a.in_stride[i] + wbyte) + voff[u]);
+        };
+        if constexpr (BSL && PAIR && SPR == 2 && PFD == 2) {
+            // Bit-sliced parity, inputs two at a time, loads TWO pairs ahead:
+            // pair p lives in buf[p & 1]; once its planes are absorbed the
+            // buffer is refilled with pair p + 2 before the CRC round, so two
+            // pairs' loads (16 KiB per wave at 4 slabs) are in flight across
+            // it instead of one.  The smaller bit-sliced accumulators (4
+            // slabs: R x 8 planes x 2 groups) leave the VGPRs for it.
+            u32x4 buf[2][2][SLABS];
+#pragma unroll
+            for (int u = 0; u < SLABS; u++) buf[0][0][u] = x[u];
+            if (K > 1) load_in(1, buf[0][1]);
+            if (K > 2) load_in(2, buf[1][0]);
+            if (K > 3) load_in(3, buf[1][1]);
+#pragma unroll
+            for (int i = 0; i < K; i += 2) {
+                const bool two = i + 1 < K;
+                auto& cur = buf[(i / 2) & 1];
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int u = 0; u < SLABS; u++) {
+                    stage_piece(0, u, cur[0][u]);
+                    if (two) stage_piece(1, u, cur[1][u]);
+                }
+                bsl_absorb(i, cur[0]);
+                if (two) bsl_absorb(i + 1, cur[1]);
+                __builtin_amdgcn_sched_barrier(0);
+                if (i + 4 < K) load_in(i + 4, cur[0]);
+                if (i + 5 < K) load_in(i + 5, cur[1]);
+                __builtin_amdgcn_sched_barrier(0);
+                after_stage(two ? i + 1 : i);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        } else if constexpr (PAIR && SPR == 2 && PF) {
             // Inputs two at a time (one CRC round): both shards' products go
             // into the accumulators through one chain of 3-input XORs, 3 ops
             // per (dword, output) for the pair instead of 4.  The next pair's

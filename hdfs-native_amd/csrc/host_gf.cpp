@@ -7,7 +7,12 @@
 #include <immintrin.h>
 
 #include <algorithm>
+#include <condition_variable>
+#include <cstdlib>
 #include <cstring>
+#include <functional>
+#include <mutex>
+#include <thread>
 
 #include "gf256.hpp"
 
@@ -206,6 +211,106 @@ void gf_matmul(Isa isa, const uint8_t* mat, const uint64_t* aff, size_t rows, si
         matmul_avx2(mat, rows, cols, in, out, n);
     else
         matmul_scalar(mat, rows, cols, in, out, n);
+}
+
+namespace {
+
+// Column-split helpers for long rows (gf_matmul_split): a process-wide pool
+// of worker threads, started on first use.  One split call at a time owns it
+// (try-lock): a concurrent caller codes its row on its own thread instead of
+// queueing behind another's.
+struct SplitPool {
+    std::mutex own;          // held by the call that is using the workers
+    std::mutex mu;
+    std::condition_variable go, done;
+    std::vector<std::thread> workers;
+    uint64_t gen = 0;        // job generation (workers run each generation once)
+    size_t pending = 0;      // worker pieces not finished
+    bool stop = false;
+    std::function<void(size_t)> job;  // piece index 1..workers.size()
+
+    explicit SplitPool(size_t n) {
+        for (size_t w = 0; w < n; w++)
+            workers.emplace_back([this, w] {
+                uint64_t seen = 0;
+                for (;;) {
+                    std::function<void(size_t)> f;
+                    {
+                        std::unique_lock<std::mutex> lk(mu);
+                        go.wait(lk, [&] { return stop || gen != seen; });
+                        if (stop) return;
+                        seen = gen;
+                        f = job;
+                    }
+                    f(w + 1);
+                    std::lock_guard<std::mutex> lk(mu);
+                    if (--pending == 0) done.notify_one();
+                }
+            });
+    }
+    ~SplitPool() {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            stop = true;
+        }
+        go.notify_all();
+        for (auto& t : workers) t.join();
+    }
+};
+
+size_t split_threads() {
+    static const size_t n = [] {
+        const char* v = std::getenv("HEC_HOST_THREADS");
+        long t = v && *v ? std::strtol(v, nullptr, 10) : 4;
+        const long hw = long(std::thread::hardware_concurrency());
+        if (hw > 0) t = std::min(t, hw);
+        return size_t(std::max(1L, std::min(t, 64L)));
+    }();
+    return n;
+}
+
+SplitPool* split_pool() {
+    static SplitPool* p = split_threads() > 1 ? new SplitPool(split_threads() - 1) : nullptr;  // never destroyed:
+    return p;  // workers may outlive static destruction order; the OS reaps them at exit
+}
+
+}  // namespace
+
+size_t split_min_bytes() { return size_t(256) << 10; }
+
+void gf_matmul_split(Isa isa, const uint8_t* mat, const uint64_t* aff, size_t rows, size_t cols,
+                     const uint8_t* const* in, uint8_t* const* out, size_t n) {
+    const size_t T = split_threads();
+    SplitPool* pool = n >= split_min_bytes() && T > 1 ? split_pool() : nullptr;
+    std::unique_lock<std::mutex> own;
+    if (pool) own = std::unique_lock<std::mutex>(pool->own, std::try_to_lock);
+    if (!pool || !own.owns_lock()) {
+        gf_matmul(isa, mat, aff, rows, cols, in, out, n);
+        return;
+    }
+    // T column ranges, 4 KiB aligned (no two threads write one cache line or page)
+    const size_t piece = ((n + T - 1) / T + 4095) & ~size_t(4095);
+    auto run = [&](size_t p) {
+        const size_t a = p * piece;
+        if (a >= n) return;
+        const size_t len = std::min(piece, n - a);
+        const uint8_t* pin[64];
+        uint8_t* pout[64];
+        for (size_t i = 0; i < cols; i++) pin[i] = in[i] + a;
+        for (size_t j = 0; j < rows; j++) pout[j] = out[j] + a;
+        gf_matmul(isa, mat, aff, rows, cols, pin, pout, len);
+    };
+    {
+        std::lock_guard<std::mutex> lk(pool->mu);
+        pool->job = run;
+        pool->pending = pool->workers.size();
+        pool->gen++;
+    }
+    pool->go.notify_all();
+    run(0);  // the caller's own piece
+    std::unique_lock<std::mutex> lk(pool->mu);
+    pool->done.wait(lk, [&] { return pool->pending == 0; });
+    pool->job = nullptr;
 }
 
 }  // namespace host

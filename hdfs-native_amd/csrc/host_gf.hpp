@@ -49,5 +49,20 @@ inline void gf_matmul(const uint8_t* mat, const uint64_t* aff, size_t rows, size
     gf_matmul(best_isa(), mat, aff, rows, cols, in, out, n);
 }
 
+// The same with rows of at least split_min_bytes() (256 KiB) per shard cut
+// into column ranges coded by a small process-wide worker pool plus the
+// calling thread ($HEC_HOST_THREADS threads in all, default 4; 1 = never
+// split).  A row that long is bound by one core's memory bandwidth, not its
+// GFNI units; the pieces are 4 KiB aligned.  If another call holds the pool,
+// the row is coded on the calling thread.  cols <= 64.
+void gf_matmul_split(Isa isa, const uint8_t* mat, const uint64_t* aff, size_t rows, size_t cols,
+                     const uint8_t* const* in, uint8_t* const* out, size_t n);
+size_t split_min_bytes();
+
+inline void gf_matmul_split(const uint8_t* mat, const uint64_t* aff, size_t rows, size_t cols,
+                            const uint8_t* const* in, uint8_t* const* out, size_t n) {
+    gf_matmul_split(best_isa(), mat, aff, rows, cols, in, out, n);
+}
+
 }  // namespace host
 }  // namespace hec

@@ -98,9 +98,30 @@ Mode mode() {
 
 // slabs = KiB of every cell per wave (ec_fused.hip): 8, or 4 with the
 // inputs taken two at a time
-std::string kernel_name(int k, int e, int kind, int sl) {
-    return "hec::gf_fused_crc<" + std::to_string(k) + ", " + std::to_string(e) + ", " + std::to_string(sl) + ", 12, " +
-           std::to_string(kind) + ", true, 2, " + (sl == 4 ? "true" : "false") + ", hec::jit_plan::Net>";
+// shape: sl = slabs (8, or 4 with inputs in pairs), wpe = waves per SIMD (2,
+// or 3 at 4 slabs: one 768-thread block per CU), pfd = input pairs loaded
+// ahead (4 slabs: 1 or 2)
+struct Shape {
+    int slabs, wpe, pfd;
+};
+
+std::string kernel_name(int k, int e, int kind, Shape sh) {
+    return "hec::gf_fused_crc<" + std::to_string(k) + ", " + std::to_string(e) + ", " + std::to_string(sh.slabs) +
+           ", 12, " + std::to_string(kind) + ", true, " + std::to_string(sh.wpe) + ", " +
+           (sh.slabs == 4 ? "true" : "false") + ", hec::jit_plan::Net, " + std::to_string(sh.pfd) + ">";
+}
+
+bool shape_ok(int k, int e, int kind, Shape sh) {
+    return (k == 2 || k == 3 || k == 6 || k == 10) && e >= 1 && e <= 4 && (kind == 0 || kind == 1) &&
+           (sh.slabs == 4 || sh.slabs == 8) && (sh.wpe == 2 || (sh.wpe == 3 && sh.slabs == 4)) &&
+           (sh.pfd == 1 || (sh.pfd == 2 && sh.slabs == 4));
+}
+
+std::string entry_key(int k, int e, int kind, Shape sh, const uint8_t* matrix) {
+    std::string key = std::to_string(k) + "/" + std::to_string(e) + "/" + std::to_string(kind) + "/" +
+                      std::to_string(sh.slabs) + "/" + std::to_string(sh.wpe) + "/" + std::to_string(sh.pfd) + "/";
+    key.append(reinterpret_cast<const char*>(matrix), size_t(e) * k);
+    return key;
 }
 
 std::string make_source(int k, int e, int kind, const uint8_t* matrix) {
@@ -153,7 +174,8 @@ void mkdirs(const std::string& d) {
 enum class State { kQueued, kCompiling, kReady, kFailed };
 
 struct Entry {
-    int k = 0, e = 0, kind = 0, slabs = 8;
+    int k = 0, e = 0, kind = 0;
+    Shape shape{8, 2, 1};
     std::vector<uint8_t> matrix;
     State state = State::kQueued;
     std::vector<char> code;        // code object (once kReady)
@@ -204,7 +226,7 @@ struct Jit {
     // compile (or load from disk) one entry's code object; sets kReady / kFailed
     void build(Entry& en) {
         const std::string src = make_source(en.k, en.e, en.kind, en.matrix.data());
-        const std::string name = kernel_name(en.k, en.e, en.kind, en.slabs);
+        const std::string name = kernel_name(en.k, en.e, en.kind, en.shape);
         const Rtc& r = rtc();
         int maj = 0, mnr = 0;
         if (r.ok) r.version(&maj, &mnr);
@@ -292,15 +314,13 @@ Jit& jit() {
 
 }  // namespace
 
-bool verify_kernel(int device, int k, int e, int kind, int slabs, const uint8_t* matrix, bool wait, VerifyKernel* out) {
-    if (mode() == Mode::kOff || !(k == 2 || k == 3 || k == 6 || k == 10) || e < 1 || e > 4 || (kind != 0 && kind != 1) ||
-        (slabs != 4 && slabs != 8))
-        return false;
+bool verify_kernel(int device, int k, int e, int kind, int slabs, int wpe, int pfd, const uint8_t* matrix, bool wait,
+                   VerifyKernel* out) {
+    const Shape sh{slabs, wpe, pfd};
+    if (mode() == Mode::kOff || !shape_ok(k, e, kind, sh)) return false;
     if (!rtc().ok && cache_dir().empty()) return false;
     wait = wait || mode() == Mode::kSync;
-    std::string key = std::to_string(k) + "/" + std::to_string(e) + "/" + std::to_string(kind) + "/" +
-                      std::to_string(slabs) + "/";
-    key.append(reinterpret_cast<const char*>(matrix), size_t(e) * k);
+    const std::string key = entry_key(k, e, kind, sh, matrix);
     Jit& J = jit();
     std::shared_ptr<Entry> en;
     {
@@ -311,7 +331,7 @@ bool verify_kernel(int device, int k, int e, int kind, int slabs, const uint8_t*
             en->k = k;
             en->e = e;
             en->kind = kind;
-            en->slabs = slabs;
+            en->shape = sh;
             en->matrix.assign(matrix, matrix + size_t(e) * k);
             J.entries.emplace(key, en);
             if (!wait) {
@@ -366,13 +386,10 @@ bool verify_kernel(int device, int k, int e, int kind, int slabs, const uint8_t*
     return true;
 }
 
-bool warm(int k, int e, int kind, int slabs, const uint8_t* matrix) {
-    if (!(k == 2 || k == 3 || k == 6 || k == 10) || e < 1 || e > 4 || (kind != 0 && kind != 1) ||
-        (slabs != 4 && slabs != 8))
-        return false;
-    std::string key = std::to_string(k) + "/" + std::to_string(e) + "/" + std::to_string(kind) + "/" +
-                      std::to_string(slabs) + "/";
-    key.append(reinterpret_cast<const char*>(matrix), size_t(e) * k);
+bool warm(int k, int e, int kind, int slabs, int wpe, int pfd, const uint8_t* matrix) {
+    const Shape sh{slabs, wpe, pfd};
+    if (!shape_ok(k, e, kind, sh)) return false;
+    const std::string key = entry_key(k, e, kind, sh, matrix);
     Jit& J = jit();
     std::shared_ptr<Entry> en;
     {
@@ -395,7 +412,7 @@ bool warm(int k, int e, int kind, int slabs, const uint8_t* matrix) {
             en->k = k;
             en->e = e;
             en->kind = kind;
-            en->slabs = slabs;
+            en->shape = sh;
             en->matrix.assign(matrix, matrix + size_t(e) * k);
             J.entries.emplace(key, en);
         }
@@ -414,6 +431,7 @@ Stats stats() {
 void count_launch() { jit().launches++; }
 
 int default_slabs(int k, int e) { return (e <= 3 && k <= 6) ? 8 : 4; }
+int default_pfd(int, int) { return 1; }
 
 size_t verify_source(int k, int e, int kind, const uint8_t* matrix, char* buf, size_t len) {
     const std::string s = make_source(k, e, kind, matrix);

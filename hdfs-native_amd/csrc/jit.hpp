@@ -42,14 +42,17 @@ struct VerifyKernel {
 // queued / running / failed.  wait = compile now (synchronously) if needed.
 // slabs = the launch shape (KiB of every cell per wave: 8, or 4 with the
 // inputs two at a time); default_slabs(k, e) is the ahead-of-time kernel's.
-bool verify_kernel(int device, int k, int e, int kind, int slabs, const uint8_t* matrix, bool wait,
+// wpe = waves per SIMD (2, or 3 at 4 slabs: one 768-thread block per CU);
+// pfd = input pairs loaded ahead at 4 slabs (1, or 2: two pairs in flight).
+bool verify_kernel(int device, int k, int e, int kind, int slabs, int wpe, int pfd, const uint8_t* matrix, bool wait,
                    VerifyKernel* out);
 int default_slabs(int k, int e);
+int default_pfd(int k, int e);
 
 // Compiles (or loads from the disk cache) the specialised kernel's code
 // object without a device: warms the caches ahead of use.  False when the
 // shape is not covered or the compile failed.
-bool warm(int k, int e, int kind, int slabs, const uint8_t* matrix);
+bool warm(int k, int e, int kind, int slabs, int wpe, int pfd, const uint8_t* matrix);
 
 // Counters for tests and the bench line: kernels compiled (or loaded from
 // the disk cache), compiles failed, launches that used a specialised kernel.

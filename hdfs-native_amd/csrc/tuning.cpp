@@ -15,7 +15,7 @@ namespace {
 std::atomic<int> g_cus[64];
 
 #ifdef HEC_EXPERIMENTAL
-constexpr int kKeys = 23;
+constexpr int kKeys = 24;
 std::atomic<int> g_knob[kKeys + 1];  // index = key; zero-initialised (static storage)
 std::atomic<int> g_nt{-1};           // key 2 defaults to -1 (non-temporal on)
 
@@ -50,6 +50,7 @@ Tune tune_snapshot() {
     t.fused_split = load(21);
     t.fused_bsl = load(22);
     t.matmul_bsl = load(23);
+    t.jit_pfd = load(24);
     return t;
 }
 
@@ -83,6 +84,7 @@ int tune_store(int key, int value) {
         case 21: ok = value >= 0 && value <= 3; break;
         case 22: ok = value == 0 || value == 1; break;
         case 23: ok = value == 0 || value == 1; break;
+        case 24: ok = value == 0 || value == 1 || value == 2; break;
         default: ok = false;
     }
     if (!ok) return HEC_ERR_INVALID_ARG;

@@ -136,12 +136,12 @@ inline InputNet input_network(const uint8_t* coefs, int r, bool first, int resta
 }
 
 // The k inputs' networks of an r x k matrix (row-major).
-inline std::vector<InputNet> matrix_network(const uint8_t* matrix, int r, int k) {
+inline std::vector<InputNet> matrix_network(const uint8_t* matrix, int r, int k, int restarts = 32) {
     std::vector<InputNet> nets;
     std::vector<uint8_t> col(r);
     for (int i = 0; i < k; i++) {
         for (int j = 0; j < r; j++) col[j] = matrix[j * k + i];
-        nets.push_back(input_network(col.data(), r, i == 0));
+        nets.push_back(input_network(col.data(), r, i == 0, restarts));
     }
     return nets;
 }

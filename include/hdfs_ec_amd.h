@@ -137,11 +137,15 @@ int hec_coder_acquire(const char *codec, size_t data_units, size_t parity_units,
 void hec_coder_release(hec_coder_t *coder);
 size_t hec_coder_pool_trim(void);
 
-/* Small-row policy of the host-buffer drop-ins below: rows of at most
- * `max_shard_len` bytes per shard are coded on the calling thread by the
- * engine's host routine (hec_gf_matmul_host), where a PCIe round trip would
- * cost more than the row (measured per size); larger rows go
- * through the device.  Per coder (default 256 KiB); 0 = always the device. */
+/* Routing of the host-buffer drop-ins below (hec_encode / hec_decode on
+ * pageable buffers): rows of at most `max_shard_len` bytes per shard are coded
+ * by the engine's host routine (hec_gf_matmul_host; rows of >= 256 KiB per
+ * shard split over $HEC_HOST_THREADS threads, default 4), longer ones go
+ * through the device (pinned bounce buffers, H2D, kernel, D2H).  Per coder;
+ * default SIZE_MAX = every row on the host: measured per size, cold and hot,
+ * the PCIe round trip of a pageable row never paid for itself;
+ * 0 = always the device.  The batched and device-resident calls are not
+ * affected. */
 int hec_coder_set_host_limit(hec_coder_t *coder, size_t max_shard_len);
 size_t hec_coder_host_limit(const hec_coder_t *coder);
 

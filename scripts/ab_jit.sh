@@ -1,7 +1,8 @@
 #!/bin/bash
 # GPU box, one lease: same-box A/B of the fused decode + verify kernel --
 # ahead-of-time v_perm kernel (HEC_JIT=0) vs the plan-specialised (JIT)
-# kernel at 8 and 4 slabs (measurement build, tune key 10) -- each variant
+# kernel at 8 and 4 slabs (measurement build, tune key 10; AB_VARIANTS adds
+# jit4p2 = two input pairs loaded ahead, jit4w3 = 3 waves per SIMD) -- each variant
 # under rocprofv3 --kernel-trace --stats (no counters), alternated twice.
 # Usage: ab_jit.sh OUTDIR [extra bench args]
 set -o pipefail
@@ -9,11 +10,13 @@ o=${1:-gpurun_out/ab_jit}; shift
 mkdir -p "$o"; export TMPDIR=/tmp
 B="--crc --corrupt none --steps 10 --warmup 3 --extra-configs 0 --cpu-seconds 0 --host-path 0 --verify sample $*"
 for rep in 1 2; do
-  for v in aot jit8 jit4; do
+  for v in ${AB_VARIANTS:-aot jit8 jit4}; do
     case $v in
       aot) E="HEC_JIT=0"; T="";;
       jit8) E="HEC_JIT=async"; T="--tune 10=8";;
       jit4) E="HEC_JIT=async"; T="--tune 10=4";;
+      jit4p2) E="HEC_JIT=async"; T="--tune 10=4,24=2";;
+      jit4w3) E="HEC_JIT=async"; T="--tune 10=4,16=3";;
     esac
     d="$o/$v.$rep"
     export $E

@@ -191,7 +191,7 @@ def test_tune_set_validates_without_device():
     xlib = H.experimental_lib()
     assert xlib.hec_tune_set(3, 2) == H.HEC_OK
     assert xlib.hec_tune_set(3, 0) == H.HEC_OK
-    for key, value in [(6, 3), (16, 1), (3, 99), (18, 2), (17, 6), (19, 3), (20, 3), (21, 4), (22, 2), (23, 2), (24, 0), (0, 0)]:
+    for key, value in [(6, 3), (16, 1), (3, 99), (18, 2), (17, 6), (19, 3), (20, 3), (21, 4), (22, 2), (23, 2), (24, 3), (25, 0), (0, 0)]:
         assert xlib.hec_tune_set(key, value) == H.HEC_ERR_INVALID_ARG, (key, value)
 
 
@@ -346,3 +346,20 @@ def test_jit_warm_compiles_and_caches(tmp_path):
         H.jit_warm(5, 3, [0])  # k = 5: no fused decode + verify kernel
     with pytest.raises(ValueError):
         H.jit_warm(6, 3, [6])  # only parity lost: nothing to rebuild
+
+
+def test_prepare_decode_args_without_device():
+    """hec_coder_prepare_decode: argument checks, and a host-only coder (no
+    device kernels to specialise) is HEC_ERR_DEVICE, never a HIP call."""
+    c = H.Coder(6, 3, H.HEC_DEVICE_HOST)
+    present = (ctypes.c_uint8 * 9)(0, 0, 0, 1, 1, 1, 1, 1, 1)
+    flag = ctypes.c_int(7)
+    assert H.lib.hec_coder_prepare_decode(None, present, 2, ctypes.byref(flag)) == H.HEC_ERR_INVALID_ARG
+    assert flag.value == 0
+    assert H.lib.hec_coder_prepare_decode(c.handle, None, 2, None) == H.HEC_ERR_INVALID_ARG
+    assert H.lib.hec_coder_prepare_decode(c.handle, present, 0, None) == H.HEC_ERR_INVALID_ARG  # NULL type
+    assert H.lib.hec_coder_prepare_decode(c.handle, present, 2, ctypes.byref(flag)) == H.HEC_ERR_DEVICE
+    assert flag.value == 0
+    c.close()
+    st = H.jit_stats()
+    assert set(st) == {"compiled", "from_disk", "failed", "launches"}
