@@ -32,9 +32,10 @@ for p in glob.glob(d + "/**/*kernel_stats.csv", recursive=True):
 line = [l for l in open(log) if l.startswith("{") and '"metric"' in l][-1]
 c = json.loads(line).get("crc32c", {})
 for r in rows:
-    if "gf_fused_crc" in r["Name"] and ", true," in r["Name"]:
+    if "gf_fused_crc" in r["Name"]:
         print(v, round(float(r["AverageNs"]) / 1e6, 4), "ms x", r["Calls"], r["Name"][:110])
-print(v, "leg", c.get("decode_verify_ms"), "frac", c.get("decode_verify_frac"), c.get("decode_verify_kernel"), c.get("jit"))
+print(v, "leg", c.get("decode_verify_ms"), "frac", c.get("decode_verify_frac"), c.get("decode_verify_kernel"), c.get("jit"),
+      "| encode+crc leg", c.get("encode_crc_ms"), "frac", c.get("encode_crc_frac"))
 PY
   done
 done

@@ -214,7 +214,7 @@ void run_p(int cus, size_t cell, uint32_t stripes, uint32_t P, uint32_t pr, uint
 static bool g_contig = false;  // PROBE_CONTIG=1: physically contiguous allocations
 
 template <int K, int R, bool MIXED = false, int U = 4, int BS = 256>
-void run(int cus, size_t cell, uint32_t stripes, int bpc = 1) {
+void run(int cus, size_t cell, uint32_t stripes, int bpc = 1, uint32_t group = 4) {
     const uint32_t chunks = uint32_t(cell / 16), tps = chunks / (BS * U), total = tps * stripes;
     uint8_t *in, *out;
     const unsigned fl = g_contig ? hipDeviceMallocContiguous : hipDeviceMallocDefault;
@@ -224,12 +224,12 @@ void run(int cus, size_t cell, uint32_t stripes, int bpc = 1) {
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
-    for (int w = 0; w < 20; w++) skel<K, R, U, BS, MIXED><<<cus * bpc, BS>>>(in, out, chunks, tps, total, 4);
+    for (int w = 0; w < 20; w++) skel<K, R, U, BS, MIXED><<<cus * bpc, BS>>>(in, out, chunks, tps, total, group);
     CK(hipDeviceSynchronize());
     std::vector<float> ms;
     for (int rep = 0; rep < 3; rep++) {
         CK(hipEventRecord(a));
-        for (int it = 0; it < 20; it++) skel<K, R, U, BS, MIXED><<<cus * bpc, BS>>>(in, out, chunks, tps, total, 4);
+        for (int it = 0; it < 20; it++) skel<K, R, U, BS, MIXED><<<cus * bpc, BS>>>(in, out, chunks, tps, total, group);
         CK(hipEventRecord(b));
         CK(hipEventSynchronize(b));
         float t;
@@ -244,10 +244,10 @@ void run(int cus, size_t cell, uint32_t stripes, int bpc = 1) {
                 " (mean writes %.2f)%s\n",
                 K, R, MIXED ? " mixed e" : "", cell >> 10, stripes, best, bytes / best / 1e6, bytes / best / 1e6 / 8000.0,
                 shards / stripes - K,
-                (U == 4 && BS == 256 && bpc == 1)
+                (U == 4 && BS == 256 && bpc == 1 && group == 4)
                     ? ""
                     : (" [U " + std::to_string(U) + ", " + std::to_string(BS) + " threads, " + std::to_string(bpc) +
-                       " per CU]")
+                       " per CU, group " + std::to_string(group) + "]")
                           .c_str());
     CK(hipFree(in));
     CK(hipFree(out));
@@ -268,6 +268,21 @@ int main() {
             run<6, 3, true>(cus, 1 << 20, 1024);
             run<6, 2>(cus, 1 << 20, 1024);
             run<3, 2, true>(cus, 1 << 20, 1024);
+        }
+        return 0;
+    }
+    if (mode && std::string(mode) == "order") {
+        // tile order (stripes interleaved per column group) and chunks per lane
+        // for the read-heavy mixes of the mixed-pattern decodes
+        for (int rep = 0; rep < 2; rep++) {
+            for (uint32_t g : {1u, 2u, 4u, 8u, 16u, 64u}) run<10, 4, true>(cus, 1 << 20, 256, 1, g);
+            run<10, 4, true, 2, 256>(cus, 1 << 20, 256, 2);
+            run<10, 4, true, 2, 512>(cus, 1 << 20, 256, 1);
+            run<10, 4, true, 8, 256>(cus, 1 << 20, 256, 1);
+            run<10, 4, true, 4, 256>(cus, 1 << 20, 256, 2);
+            run<10, 4, true>(cus, 1 << 20, 1024);
+            for (uint32_t g : {1u, 4u, 16u}) run<6, 3, true>(cus, 1 << 20, 1024, 1, g);
+            run<6, 3, true, 8, 256>(cus, 1 << 20, 1024, 1);
         }
         return 0;
     }
