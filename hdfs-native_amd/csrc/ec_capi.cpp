@@ -1519,7 +1519,7 @@ int hec_coder_prepare_decode(hec_coder_t* c, const uint8_t* present, int checksu
         const hec::Tune tn = hec::tune_snapshot();
         const int slabs = (tn.fused_slabs == 4 || tn.fused_slabs == 8) ? tn.fused_slabs
                                                                         : hec::jit::default_slabs(int(c->k), e);
-        const int pfd = tn.jit_pfd == 2 && slabs == 4 ? 2 : hec::jit::default_pfd(int(c->k), e);
+        const int pfd = hec::jit::pick_pfd(tn.jit_pfd, slabs, int(c->k), e);
         const int wpe = tn.fused_wpe == 3 && slabs == 4 ? 3 : 2;
         const bool ok =
             hec::jit::verify_kernel(c->device, int(c->k), e, kind, slabs, wpe, pfd, p.matrix.data(), true, &vk);

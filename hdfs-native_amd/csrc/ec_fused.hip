@@ -310,6 +310,11 @@ const void* encode_fn(int slabs, int scheme, int wpe, bool pair, bool bsl) {
     // is 8 (RS(3,2), RS(6,3); tune key 10 = 4), one or two pairs loaded ahead
     // (key 24 = 2): the measurement twin of the specialised decode + verify shapes
     if constexpr (bsl_shape<K, R>() && fused_slabs(K, R) == 8) {
+        // key 24 = 3: the default 8-slab shape with each input's loads issued
+        // before its parity math (the parity reads the staged copy)
+        if (bsl && scheme == 12 && wpe == 2 && slabs == 8 && tune_snapshot().jit_pfd == 3)
+            return reinterpret_cast<const void*>(
+                &gf_fused_crc<K, R, 8, 12, crc::kCrc32c, false, 2, false, RsNet<K, R>, 3>);
         if (bsl && scheme == 12 && wpe == 2 && slabs == 4 && pair)
             return tune_snapshot().jit_pfd == 2
                        ? reinterpret_cast<const void*>(
@@ -484,7 +489,7 @@ int launch_fused(const MatmulArgs& in, const FusedCrcArgs& cs, bool verify, int 
         for (int j = 0; j < a.r; j++)
             for (int i = 0; i < a.k; i++) mat[j * a.k + i] = a.coef[j * kMaxK + i];
         const int js = (tn.fused_slabs == 4 || tn.fused_slabs == 8) ? tn.fused_slabs : jit::default_slabs(a.k, a.r);
-        const int jp = tn.jit_pfd == 2 && js == 4 ? 2 : jit::default_pfd(a.k, a.r);
+        const int jp = jit::pick_pfd(tn.jit_pfd, js, a.k, a.r);
         // (3 waves per SIMD: tune key 16 = 3 with key 10 = 4; the launch's
         // `waves` and grid already follow wpe)
         if (jit::verify_kernel(device, a.k, a.r, cs.kind, js, wpe, jp, mat, false, &vk)) use_slabs = js;

@@ -106,7 +106,10 @@ __global__ __launch_bounds__(crcdev::sliced(SCHEME) ? 128 * WPE * (WPE - 1) : 51
     const uint64_t cell_len = a.cell_len;
     const uint64_t nck = (cell_len + 511) / 512;  // checksum chunks per cell
     const uint32_t total = a.total_tiles;
-    const int wave = threadIdx.x / 64, lane = threadIdx.x & 63;
+    // wave index as a scalar: the wave's byte offset, the shard bases and the
+    // stage pointer then stay in SGPRs (saddr + 32-bit lane offset loads and
+    // stores, no per-access 64-bit VALU address)
+    const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x / 64)), lane = threadIdx.x & 63;
     // this lane's quarter in a round: row `lane` = piece lane/8 = (shard
     // slot sir, slab), chunk half (lane/4)&1 of that slab, quarter qi
     const int qi = lane & 3, piece = lane >> 3, sir = piece / SLABS, pslab = piece % SLABS, half = (lane >> 2) & 1;
@@ -114,20 +117,28 @@ __global__ __launch_bounds__(crcdev::sliced(SCHEME) ? 128 * WPE * (WPE - 1) : 51
     uint32_t* out_sums = reinterpret_cast<uint32_t*>(cs.sums);
     const uint32_t* exp_sums = reinterpret_cast<const uint32_t*>(cs.expected);
 
+    // PFD = 3: x already holds this tile's input 0 (loaded during the
+    // previous tile's outputs)
+    bool have_next = false;
+    u32x4 x[SLABS], xn[SLABS];
     for (uint32_t tile = blockIdx.x; tile < total; tile += gridDim.x) {
         uint32_t stripe, tcol;
         tile_coords(tile, a, stripe, tcol);
         const uint64_t wbyte = uint64_t(tcol) * TILE_BYTES + uint64_t(wave) * WAVE_BYTES;  // wave's first byte
-        if (wbyte >= cell_len) continue;  // wave-uniform
+        if (wbyte >= cell_len) continue;  // wave-uniform (never a prefetched tile: those are full)
         // 32-bit lane offsets from a wave-uniform per-shard base (saddr +
         // voffset addressing); dead slabs of a short last tile read slab 0
+        // (compared in 32 bits: a 64-bit compare shares the offsets' zero
+        // extension with the address adds, which then lose the saddr form
+        // and hold every offset as a 64-bit VGPR pair)
         const uint64_t left = cell_len - wbyte;
+        const uint32_t left32 = left > 0xFFFFFFFFull ? 0xFFFFFFFFu : uint32_t(left);
         uint32_t voff[SLABS];
         bool live[SLABS];
 #pragma unroll
         for (int u = 0; u < SLABS; u++) {
             const uint32_t o = uint32_t(u) * 1024u + uint32_t(lane) * 16u;
-            live[u] = o < left;
+            live[u] = o < left32;
             voff[u] = live[u] ? o : 0u;
         }
         const uint64_t cbyte = wbyte + uint64_t(pslab) * 1024u + uint64_t(half) * 512u;
@@ -179,6 +190,10 @@ __global__ __launch_bounds__(crcdev::sliced(SCHEME) ? 128 * WPE * (WPE - 1) : 51
         auto stage_piece = [&](int slot, int u, const u32x4& v) {
             *reinterpret_cast<u32x4*>(stage + (8 * (slot * SLABS + u) + lane / 8) * PITCH + 16 * (lane % 8)) = v;
         };
+        // this lane's own 16 B of slab u in round slot `slot`, read back
+        auto staged_piece = [&](int slot, int u) {
+            return *reinterpret_cast<const u32x4*>(stage + (8 * (slot * SLABS + u) + lane / 8) * PITCH + 16 * (lane % 8));
+        };
         auto after_stage = [&](int shard) {
             if (shard % SPR == SPR - 1 || shard == NSUM - 1) crc_round(shard - shard % SPR, shard % SPR + 1);
         };
@@ -192,13 +207,15 @@ __global__ __launch_bounds__(crcdev::sliced(SCHEME) ? 128 * WPE * (WPE - 1) : 51
         }
         // BSL: group g = slabs 2g, 2g+1 (8 dwords) as R*8 bit planes
         uint32_t accp[BSL ? SLABS / 2 : 1][BSL ? R * 8 : 1];
-        // input i's share of the parity, bit-sliced (input 0 initialises accp)
-        auto bsl_absorb = [&](int i, const u32x4 (&xi)[SLABS]) {
+        // input i's share of the parity, bit-sliced (input 0 initialises accp);
+        // fetch(g, lo, hi) yields group g's two slabs
+        auto bsl_absorb_from = [&](int i, auto&& fetch) {
             if constexpr (BSL) {
 #pragma unroll
                 for (int g = 0; g < SLABS / 2; g++) {
-                    uint32_t pl[8] = {xi[2 * g][0],     xi[2 * g][1],     xi[2 * g][2],     xi[2 * g][3],
-                                      xi[2 * g + 1][0], xi[2 * g + 1][1], xi[2 * g + 1][2], xi[2 * g + 1][3]};
+                    u32x4 lo, hi;
+                    fetch(g, lo, hi);
+                    uint32_t pl[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
                     if (i > 0) {
                         // opaque per input: keeps the XOR chains of the
                         // accumulators from being reassociated across inputs
@@ -211,6 +228,12 @@ __global__ __launch_bounds__(crcdev::sliced(SCHEME) ? 128 * WPE * (WPE - 1) : 51
                     __builtin_amdgcn_sched_barrier(0);
                 }
             }
+        };
+        auto bsl_absorb = [&](int i, const u32x4 (&xi)[SLABS]) {
+            bsl_absorb_from(i, [&](int g, u32x4& lo, u32x4& hi) {
+                lo = xi[2 * g];
+                hi = xi[2 * g + 1];
+            });
         };
         // parity row j's slabs back from the planes (the transpose is its own inverse)
         auto bsl_output = [&](int j, u32x4 (&o)[SLABS]) {
@@ -227,15 +250,56 @@ __global__ __launch_bounds__(crcdev::sliced(SCHEME) ? 128 * WPE * (WPE - 1) : 51
                 }
             }
         };
-        u32x4 x[SLABS], xn[SLABS];
+        if (!have_next) {
 #pragma unroll
-        for (int u = 0; u < SLABS; u++) x[u] = load16<true>(a.in[0] + (uint64_t(stripe) * a.in_stride[0] + wbyte) + voff[u]);
+            for (int u = 0; u < SLABS; u++)
+                x[u] = load16<true>(a.in[0] + (uint64_t(stripe) * a.in_stride[0] + wbyte) + voff[u]);
+        }
+        have_next = false;
         auto load_in = [&](int i, u32x4 (&dst)[SLABS]) {
 #pragma unroll
             for (int u = 0; u < SLABS; u++)
                 dst[u] = load16<true>(a.in[i] + (uint64_t(stripe) * a.in_stride[i] + wbyte) + voff[u]);
         };
-        if constexpr (BSL && PAIR && SPR == 2 && PFD == 2) {
+        if constexpr (BSL && !PAIR && PFD == 3) {
+            // Bit-sliced parity, one input at a time, loads issued a phase
+            // earlier: input i is staged to LDS first, so its registers take
+            // input i + 1's loads BEFORE the parity math, which reads input i
+            // back from the stage (its own 16-B pieces: no barrier); the loads
+            // are in flight across the network and the CRC round instead of
+            // the CRC round only.  The next tile's input 0 is loaded during
+            // this tile's outputs (when that tile is full for this wave, so its
+            // lane offsets are the constant ones).
+#pragma unroll
+            for (int i = 0; i < K; i++) {
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int u = 0; u < SLABS; u++) stage_piece(i % SPR, u, x[u]);
+                __builtin_amdgcn_sched_barrier(0);
+                if (i + 1 < K) load_in(i + 1, x);
+                __builtin_amdgcn_sched_barrier(0);
+                bsl_absorb_from(i, [&](int g, u32x4& lo, u32x4& hi) {
+                    lo = staged_piece(i % SPR, 2 * g);
+                    hi = staged_piece(i % SPR, 2 * g + 1);
+                });
+                __builtin_amdgcn_sched_barrier(0);
+                after_stage(i);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            const uint32_t nt = tile + gridDim.x;
+            if (nt < total) {
+                uint32_t ns, ncol;
+                tile_coords(nt, a, ns, ncol);
+                const uint64_t nw = uint64_t(ncol) * TILE_BYTES + uint64_t(wave) * WAVE_BYTES;
+                if (nw + WAVE_BYTES <= cell_len) {  // wave-uniform
+#pragma unroll
+                    for (int u = 0; u < SLABS; u++)
+                        x[u] = load16<true>(a.in[0] + (uint64_t(ns) * a.in_stride[0] + nw) + uint32_t(u) * 1024u +
+                                            uint32_t(lane) * 16u);
+                    have_next = true;
+                }
+            }
+        } else if constexpr (BSL && PAIR && SPR == 2 && PFD == 2) {
             // Bit-sliced parity, inputs two at a time, loads TWO pairs ahead:
             // pair p lives in buf[p & 1]; once its planes are absorbed the
             // buffer is refilled with pair p + 2 before the CRC round, so two

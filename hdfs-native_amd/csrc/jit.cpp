@@ -100,7 +100,7 @@ Mode mode() {
 // inputs taken two at a time
 // shape: sl = slabs (8, or 4 with inputs in pairs), wpe = waves per SIMD (2,
 // or 3 at 4 slabs: one 768-thread block per CU), pfd = input pairs loaded
-// ahead (4 slabs: 1 or 2)
+// ahead (4 slabs: 1 or 2) or 3 = loads issued before the parity math (8 slabs)
 struct Shape {
     int slabs, wpe, pfd;
 };
@@ -114,7 +114,7 @@ std::string kernel_name(int k, int e, int kind, Shape sh) {
 bool shape_ok(int k, int e, int kind, Shape sh) {
     return (k == 2 || k == 3 || k == 6 || k == 10) && e >= 1 && e <= 4 && (kind == 0 || kind == 1) &&
            (sh.slabs == 4 || sh.slabs == 8) && (sh.wpe == 2 || (sh.wpe == 3 && sh.slabs == 4)) &&
-           (sh.pfd == 1 || (sh.pfd == 2 && sh.slabs == 4));
+           (sh.pfd == 1 || (sh.pfd == 2 && sh.slabs == 4) || (sh.pfd == 3 && sh.slabs == 8));
 }
 
 std::string entry_key(int k, int e, int kind, Shape sh, const uint8_t* matrix) {
@@ -432,6 +432,12 @@ void count_launch() { jit().launches++; }
 
 int default_slabs(int k, int e) { return (e <= 3 && k <= 6) ? 8 : 4; }
 int default_pfd(int, int) { return 1; }
+
+int pick_pfd(int key, int slabs, int k, int e) {
+    if (key == 2 && slabs == 4) return 2;
+    if (key == 3 && slabs == 8) return 3;
+    return default_pfd(k, e);
+}
 
 size_t verify_source(int k, int e, int kind, const uint8_t* matrix, char* buf, size_t len) {
     const std::string s = make_source(k, e, kind, matrix);

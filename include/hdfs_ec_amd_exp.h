@@ -59,8 +59,11 @@
  *         1 = bit-sliced XOR network of the RS matrix (gf_encode_bsl, and
  *         gf_matmul_dma's BSL form; RS(3,2), RS(6,3), RS(10,4); measured
  *         slower at RS(6,3) 1 MiB, not kept)
- * key 24: plan-specialised (JIT) decode + verify at 4 slabs (key 10 = 4):
- *         input pairs loaded ahead, 0 / 1 = one (default), 2 = two
+ * key 24: fused kernels' load schedule: 0 / 1 = default; 2 = at 4 slabs
+ *         (key 10 = 4; JIT decode + verify, bit-sliced encode twins) two
+ *         input pairs loaded ahead; 3 = at 8 slabs (JIT decode + verify, the
+ *         bit-sliced encode) each input's loads issued before the parity
+ *         math of the previous one, which reads its staged copy
  * Returns HEC_OK, or HEC_ERR_INVALID_ARG for an unknown key / value.
  */
 #ifndef HDFS_EC_AMD_EXP_H

@@ -2,7 +2,8 @@
 # GPU box, one lease: same-box A/B of the fused decode + verify kernel --
 # ahead-of-time v_perm kernel (HEC_JIT=0) vs the plan-specialised (JIT)
 # kernel at 8 and 4 slabs (measurement build, tune key 10; AB_VARIANTS adds
-# jit4p2 = two input pairs loaded ahead, jit4w3 = 3 waves per SIMD) -- each variant
+# jit4p2 = two input pairs loaded ahead, jit4w3 = 3 waves per SIMD, jit8p3 = loads
+# issued before the parity math; the encode + CRC leg follows keys 10 / 24 too) -- each variant
 # under rocprofv3 --kernel-trace --stats (no counters), alternated twice.
 # Usage: ab_jit.sh OUTDIR [extra bench args]
 set -o pipefail
@@ -17,6 +18,7 @@ for rep in 1 2; do
       jit4) E="HEC_JIT=async"; T="--tune 10=4";;
       jit4p2) E="HEC_JIT=async"; T="--tune 10=4,24=2";;
       jit4w3) E="HEC_JIT=async"; T="--tune 10=4,16=3";;
+      jit8p3) E="HEC_JIT=async"; T="--tune 10=8,24=3";;
     esac
     d="$o/$v.$rep"
     export $E

@@ -147,12 +147,14 @@ FUSED_TUNES = [[(11, 2)], [(11, 6)], [(16, 3)], [(16, 3), (11, 1)]]
 
 
 @pytest.mark.parametrize("k,m,cell,S", [(6, 3, 1 << 16, 3), (10, 4, 1 << 15, 2), (3, 2, 8192 + 512, 4)])
-@pytest.mark.parametrize("tunes", FUSED_TUNES + [[(22, 1)], [(22, 1), (5, 0)]])
+@pytest.mark.parametrize("tunes", FUSED_TUNES + [[(22, 1)], [(22, 1), (5, 0)], [(24, 3)], [(10, 4)], [(10, 4), (24, 2)]])
 def test_fused_variants_encode_vs_oracle(xlib, dev, c_oracle, k, m, cell, S, tunes):
     """Fused encode + CRC32C with the rejected variants: bank-replicated
     slicing-by-1 / -by-2 tables (tune key 11 = 2 / 6), one 768-thread block
-    per CU (key 16 = 3, 11-bit slicing or slicing-by-8), and the v_perm table
-    parity instead of the default bit-sliced networks (key 22 = 1)."""
+    per CU (key 16 = 3, 11-bit slicing or slicing-by-8), the v_perm table
+    parity instead of the default bit-sliced networks (key 22 = 1), and the
+    load schedules: early issue at 8 slabs (key 24 = 3), inputs in pairs at 4
+    slabs with one or two pairs ahead (key 10 = 4, key 24 = 2)."""
     bpc = 512
     data = batch_data(S, k, cell, first=77 + cell)
     par = oracle_batch_encode(c_oracle, k, m, data)
@@ -209,6 +211,48 @@ def test_fused_variants_verify_vs_oracle(xlib, dev, c_oracle, ctype, k, m, cell,
     assert np.array_equal(b, want_bad)
     assert np.array_equal(o[:, 0], data[:, 0])
     assert np.array_equal(o[1, 2], data[1, 2])
+
+
+def _xjit_launches(xlib):
+    import ctypes
+    v = [ctypes.c_uint64(0) for _ in range(4)]
+    xlib.hec_jit_stats(*[ctypes.byref(x) for x in v])
+    return v[3].value
+
+
+JIT_SHAPE_CASES = [
+    # (k, m, cell, missing, tunes, checksum type): every case a fresh hiprtc compile
+    (6, 3, 1 << 15, (0, 1, 2), [(24, 3)], H.CHECKSUM_CRC32C),
+    (6, 3, (1 << 15) + 512, (0,), [(24, 3)], H.CHECKSUM_CRC32),
+    (3, 2, 8192 + 512, (0, 1), [(24, 3)], H.CHECKSUM_CRC32C),
+    (6, 3, 1 << 15, (0, 1, 2), [(10, 4)], H.CHECKSUM_CRC32C),
+    (6, 3, (1 << 15) + 512, (0, 2), [(10, 4), (24, 2)], H.CHECKSUM_CRC32C),
+    (10, 4, 1 << 14, (0, 1, 2, 3), [(10, 4), (24, 2)], H.CHECKSUM_CRC32),
+    (6, 3, 1 << 15, (1,), [(10, 4), (16, 3)], H.CHECKSUM_CRC32C),
+    (10, 4, (1 << 14) + 512, (0, 5), [(10, 4), (16, 3)], H.CHECKSUM_CRC32C),
+    (6, 3, 1 << 15, (0, 1, 2), [(10, 8)], H.CHECKSUM_CRC32),
+]
+
+
+@pytest.mark.parametrize("k,m,cell,missing,tunes,ctype", JIT_SHAPE_CASES)
+def test_jit_verify_shapes_vs_oracle(xlib, dev, c_oracle, k, m, cell, missing, tunes, ctype):
+    """The plan-specialised decode + verify kernel at every shape the
+    measurement build can ask for (slabs, waves per SIMD, load schedule),
+    prepared synchronously on a measurement-build coder: rebuilt data, bad
+    flags and errors as the oracle's read_slice restatement (the parity suite's
+    body); the library's launch counter proves the specialised kernel ran."""
+    for key, value in tunes:
+        H.tune_set(key, value, xlib)
+    try:
+        cod = H.Coder(k, m, 0, lib=xlib)
+        assert cod.prepare_decode(list(missing), ctype), "hiprtc unavailable on the GPU box"
+        before = _xjit_launches(xlib)
+        P.decode_verify_body(dev, c_oracle, ctype, k, m, cell, 512, list(missing), [], cod)
+        assert _xjit_launches(xlib) > before
+        cod.close()
+    finally:
+        for key, _ in tunes:
+            H.tune_set(key, 0, xlib)
 
 
 # ---- knob-selected shapes of the product kernels -------------------------
@@ -299,7 +343,7 @@ def test_tune_set_concurrent_with_launches(xlib, dev, c_oracle):
 
 
 def test_tune_set_rejects_unknown_values(xlib):
-    for key, value in [(3, 99), (1, 5), (5, 6), (11, 8), (16, 1), (17, 6), (19, 3), (20, 3), (21, 4), (22, 2), (23, 2), (24, 0), (0, 0)]:
+    for key, value in [(3, 99), (1, 5), (5, 6), (11, 8), (16, 1), (17, 6), (19, 3), (20, 3), (21, 4), (22, 2), (23, 2), (24, 4), (25, 0), (0, 0)]:
         with pytest.raises(ValueError):
             H.tune_set(key, value, xlib)
 
