@@ -3,14 +3,15 @@
 # ahead-of-time v_perm kernel (HEC_JIT=0) vs the plan-specialised (JIT)
 # kernel at 8 and 4 slabs (measurement build, tune key 10; AB_VARIANTS adds
 # jit4p2 = two input pairs loaded ahead, jit4w3 = 3 waves per SIMD, jit8p3 = loads
-# issued before the parity math; the encode + CRC leg follows keys 10 / 24 too) -- each variant
+# issued before the parity math, jit4cold = jit4 compiled in-process from an
+# empty code-object cache; the encode + CRC leg follows keys 10 / 24 too) -- each variant
 # under rocprofv3 --kernel-trace --stats (no counters), alternated twice.
 # Usage: ab_jit.sh OUTDIR [extra bench args]
 set -o pipefail
 o=${1:-gpurun_out/ab_jit}; shift
 mkdir -p "$o"; export TMPDIR=/tmp
 B="--crc --corrupt none --steps 10 --warmup 3 --extra-configs 0 --cpu-seconds 0 --host-path 0 --verify sample $*"
-for rep in 1 2; do
+for rep in $(seq 1 ${AB_REPS:-2}); do
   for v in ${AB_VARIANTS:-aot jit8 jit4}; do
     case $v in
       aot) E="HEC_JIT=0"; T="";;
@@ -19,12 +20,13 @@ for rep in 1 2; do
       jit4p2) E="HEC_JIT=async"; T="--tune 10=4,24=2";;
       jit4w3) E="HEC_JIT=async"; T="--tune 10=4,16=3";;
       jit8p3) E="HEC_JIT=async"; T="--tune 10=8,24=3";;
+      jit4cold) E="HEC_JIT=async HEC_JIT_CACHE=$o/cache.$rep.$RANDOM"; T="--tune 10=4";;
     esac
     d="$o/$v.$rep"
     export $E
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$d" -o run --output-format csv -- \
       python3 -u bench.py $B $T > "$d.log" 2>&1 || { tail -20 "$d.log"; exit 2; }
-    unset HEC_JIT
+    unset HEC_JIT HEC_JIT_CACHE
     python3 - "$d" "$v" "$d.log" <<'PY'
 import csv, glob, json, sys
 d, v, log = sys.argv[1:]
