@@ -90,6 +90,12 @@ __global__ __launch_bounds__(crcdev::sliced(SCHEME) ? 128 * WPE * (WPE - 1) : 51
     constexpr int BS = crcdev::sliced(SCHEME) ? 128 * WPE * (WPE - 1) : 512, WAVES = BS / 64;
     constexpr int PITCH = 144, STAGE = 64 * PITCH, SPR = 8 / SLABS;
     constexpr int NSUM = VERIFY ? K : K + R;  // checksummed shards
+    // VERIFY with PFD = 4: the tile's expected chunk sums (CPS per survivor
+    // per wave) are loaded with its first input, NWANT per lane, and each CRC
+    // round takes its own from them by a lane shuffle instead of a global load
+    // whose latency the round would wait for
+    constexpr bool WANT_PF = VERIFY && PFD == 4;
+    constexpr int CPS = SLABS * 2, NWANT = WANT_PF ? (NSUM * CPS + 63) / 64 : 1;
     constexpr uint32_t WAVE_BYTES = SLABS * 1024u, TILE_BYTES = WAVES * WAVE_BYTES;
     constexpr bool PF = R * SLABS <= 24;  // register prefetch of the next shard
     __shared__ PermTable s_tab[R][K];  // K columns: scheme 11 needs 2 x 79 KiB per CU
@@ -145,6 +151,7 @@ __global__ __launch_bounds__(crcdev::sliced(SCHEME) ? 128 * WPE * (WPE - 1) : 51
         const bool in_cell = cbyte < cell_len;
         const bool full = in_cell && cell_len - cbyte >= 512u;  // same for a chunk's 4 lanes
 
+        uint32_t wreg[NWANT];  // WANT_PF: the tile's expected sums (filled with input 0's loads)
         // `first` is a compile-time constant at every (unrolled) call site,
         // so the shard ids are scalar kernarg reads
         auto sum_cell = [&](int first) {
@@ -157,7 +164,17 @@ __global__ __launch_bounds__(crcdev::sliced(SCHEME) ? 128 * WPE * (WPE - 1) : 51
             asm volatile("" ::: "memory");
             const bool live_c = in_cell && sir < count;
             uint32_t want = 0;
-            if (VERIFY && live_c && qi == 0) want = exp_sums[sum_cell(first) * nck + cbyte / 512];  // issued before the lookups
+            if constexpr (WANT_PF) {
+                // from the tile's prefetched sums: entry (first + sir) * CPS + chunk
+                const int f = (first + sir) * CPS + pslab * 2 + half;
+#pragma unroll
+                for (int h = 0; h < NWANT; h++) {
+                    const uint32_t v = uint32_t(__shfl(int(wreg[h]), f & 63));
+                    if ((f >> 6) == h) want = v;
+                }
+            } else if (VERIFY && live_c && qi == 0) {
+                want = exp_sums[sum_cell(first) * nck + cbyte / 512];  // issued before the lookups
+            }
             uint32_t val = 0;
             if (full && sir < count) {
                 uint32_t r = crcdev::quarter<SCHEME, REFL>(s_ctabs, stage + lane * PITCH, lane);
@@ -256,6 +273,18 @@ __global__ __launch_bounds__(crcdev::sliced(SCHEME) ? 128 * WPE * (WPE - 1) : 51
                 x[u] = load16<true>(a.in[0] + (uint64_t(stripe) * a.in_stride[0] + wbyte) + voff[u]);
         }
         have_next = false;
+        if constexpr (WANT_PF) {
+            const uint64_t c0 = wbyte / 512;
+#pragma unroll
+            for (int h = 0; h < NWANT; h++) {
+                const int f = lane + 64 * h, s = f / CPS, c = f % CPS;
+                uint32_t sid = 0;
+#pragma unroll
+                for (int t = 0; t < NSUM; t++) sid = s == t ? cs.shard_id[t] : sid;
+                const bool ok = s < NSUM && wbyte + uint64_t(c) * 512u < cell_len;
+                wreg[h] = ok ? exp_sums[(uint64_t(stripe) * cs.n_total + sid) * nck + c0 + uint64_t(c)] : 0u;
+            }
+        }
         auto load_in = [&](int i, u32x4 (&dst)[SLABS]) {
 #pragma unroll
             for (int u = 0; u < SLABS; u++)

@@ -63,7 +63,9 @@
  *         (key 10 = 4; JIT decode + verify, bit-sliced encode twins) two
  *         input pairs loaded ahead; 3 = at 8 slabs (JIT decode + verify, the
  *         bit-sliced encode) each input's loads issued before the parity
- *         math of the previous one, which reads its staged copy
+ *         math of the previous one, which reads its staged copy; 4 = (JIT
+ *         decode + verify) the expected chunk sums loaded once per tile and
+ *         shuffled to the CRC rounds
  * Returns HEC_OK, or HEC_ERR_INVALID_ARG for an unknown key / value.
  */
 #ifndef HDFS_EC_AMD_EXP_H
