@@ -481,7 +481,8 @@ int launch_fused(const MatmulArgs& in, const FusedCrcArgs& cs, bool verify, int 
     if (!aligned) return -1;
     // decode + verify at the default scheme: the plan's own bit-sliced network
     // when its specialised kernel is compiled (jit.hpp), same block; its slab
-    // count is the ahead-of-time kernel's (measurement build: tune key 10)
+    // count is jit::default_slabs (4; measurement build: tune key 10), the
+    // tile geometry below follows it
     jit::VerifyKernel vk;
     int use_slabs = slabs;
     if (verify && !split && scheme == 12) {

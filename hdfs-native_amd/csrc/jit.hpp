@@ -41,9 +41,11 @@ struct VerifyKernel {
 // device), or false: JIT off or unavailable, shape not covered, compile
 // queued / running / failed.  wait = compile now (synchronously) if needed.
 // slabs = the launch shape (KiB of every cell per wave: 8, or 4 with the
-// inputs two at a time); default_slabs(k, e) is the ahead-of-time kernel's.
+// inputs two at a time); default_slabs(k, e) is the specialised kernel's
+// default (4: measured faster than 8 for every plan tried), which may differ
+// from the ahead-of-time kernel's (8 at k <= 6, e <= 3).
 // wpe = waves per SIMD (2, or 3 at 4 slabs: one 768-thread block per CU);
-// pfd = input pairs loaded ahead at 4 slabs (1, or 2: two pairs in flight).
+// pfd = load schedule (1 default; measurement shapes: pick_pfd).
 bool verify_kernel(int device, int k, int e, int kind, int slabs, int wpe, int pfd, const uint8_t* matrix, bool wait,
                    VerifyKernel* out);
 int default_slabs(int k, int e);
