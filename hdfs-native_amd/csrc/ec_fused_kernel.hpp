@@ -95,6 +95,12 @@ __global__ __launch_bounds__(crcdev::sliced(SCHEME) ? 128 * WPE * (WPE - 1) : 51
     // round takes its own from them by a lane shuffle instead of a global load
     // whose latency the round would wait for
     constexpr bool WANT_PF = VERIFY && PFD == 4;
+    // VERIFY with PFD = 5 (default shapes: inputs one at a time, or in pairs
+    // with one pair ahead): the rebuilt rows are stored, and the next tile's
+    // first inputs loaded, BEFORE the last input's CRC round, which then
+    // covers their latency; otherwise the next tile's first loads queue
+    // behind this tile's stores (vmcnt retires in order) with nothing to do
+    constexpr bool EARLY_OUT = VERIFY && PFD == 5;
     constexpr int CPS = SLABS * 2, NWANT = WANT_PF ? (NSUM * CPS + 63) / 64 : 1;
     constexpr uint32_t WAVE_BYTES = SLABS * 1024u, TILE_BYTES = WAVES * WAVE_BYTES;
     constexpr bool PF = R * SLABS <= 24;  // register prefetch of the next shard
@@ -267,7 +273,8 @@ __global__ __launch_bounds__(crcdev::sliced(SCHEME) ? 128 * WPE * (WPE - 1) : 51
                 }
             }
         };
-        if (!have_next) {
+        const bool pref = have_next;  // x (and xn with pairs, EARLY_OUT) hold this tile's first inputs
+        if (!pref) {
 #pragma unroll
             for (int u = 0; u < SLABS; u++)
                 x[u] = load16<true>(a.in[0] + (uint64_t(stripe) * a.in_stride[0] + wbyte) + voff[u]);
@@ -289,6 +296,48 @@ __global__ __launch_bounds__(crcdev::sliced(SCHEME) ? 128 * WPE * (WPE - 1) : 51
 #pragma unroll
             for (int u = 0; u < SLABS; u++)
                 dst[u] = load16<true>(a.in[i] + (uint64_t(stripe) * a.in_stride[i] + wbyte) + voff[u]);
+        };
+        // the next tile's input 0 (and 1: `two`) into x (xn) when that tile is
+        // full for this wave (its lane offsets are then the constant ones)
+        auto prefetch_next = [&](bool two) {
+            const uint32_t nt = tile + gridDim.x;
+            if (nt < total) {
+                uint32_t ns, ncol;
+                tile_coords(nt, a, ns, ncol);
+                const uint64_t nw = uint64_t(ncol) * TILE_BYTES + uint64_t(wave) * WAVE_BYTES;
+                if (nw + WAVE_BYTES <= cell_len) {  // wave-uniform
+#pragma unroll
+                    for (int u = 0; u < SLABS; u++)
+                        x[u] = load16<true>(a.in[0] + (uint64_t(ns) * a.in_stride[0] + nw) + uint32_t(u) * 1024u +
+                                            uint32_t(lane) * 16u);
+                    if (two) {
+#pragma unroll
+                        for (int u = 0; u < SLABS; u++)
+                            xn[u] = load16<true>(a.in[1] + (uint64_t(ns) * a.in_stride[1] + nw) + uint32_t(u) * 1024u +
+                                                 uint32_t(lane) * 16u);
+                    }
+                    have_next = true;
+                }
+            }
+        };
+        // the R output rows: stored (encode: and checksummed, one round each)
+        auto emit_outputs = [&]() {
+#pragma unroll
+            for (int j = 0; j < R; j++) {
+                u32x4 o[SLABS];
+                if constexpr (BSL) {
+                    bsl_output(j, o);
+                } else {
+#pragma unroll
+                    for (int u = 0; u < SLABS; u++) o[u] = acc[u][j];
+                }
+#pragma unroll
+                for (int u = 0; u < SLABS; u++) {
+                    if (live[u]) store16<true>(a.out[j] + (uint64_t(stripe) * a.out_stride[j] + wbyte) + voff[u], o[u]);
+                    if constexpr (!VERIFY) stage_piece((K + j) % SPR, u, o[u]);
+                }
+                if constexpr (!VERIFY) after_stage(K + j);
+            }
         };
         if constexpr (BSL && !PAIR && PFD == 3) {
             // Bit-sliced parity, one input at a time, loads issued a phase
@@ -315,19 +364,7 @@ __global__ __launch_bounds__(crcdev::sliced(SCHEME) ? 128 * WPE * (WPE - 1) : 51
                 after_stage(i);
                 __builtin_amdgcn_sched_barrier(0);
             }
-            const uint32_t nt = tile + gridDim.x;
-            if (nt < total) {
-                uint32_t ns, ncol;
-                tile_coords(nt, a, ns, ncol);
-                const uint64_t nw = uint64_t(ncol) * TILE_BYTES + uint64_t(wave) * WAVE_BYTES;
-                if (nw + WAVE_BYTES <= cell_len) {  // wave-uniform
-#pragma unroll
-                    for (int u = 0; u < SLABS; u++)
-                        x[u] = load16<true>(a.in[0] + (uint64_t(ns) * a.in_stride[0] + nw) + uint32_t(u) * 1024u +
-                                            uint32_t(lane) * 16u);
-                    have_next = true;
-                }
-            }
+            prefetch_next(false);
         } else if constexpr (BSL && PAIR && SPR == 2 && PFD == 2) {
             // Bit-sliced parity, inputs two at a time, loads TWO pairs ahead:
             // pair p lives in buf[p & 1]; once its planes are absorbed the
@@ -365,7 +402,7 @@ __global__ __launch_bounds__(crcdev::sliced(SCHEME) ? 128 * WPE * (WPE - 1) : 51
             // into the accumulators through one chain of 3-input XORs, 3 ops
             // per (dword, output) for the pair instead of 4.  The next pair's
             // loads are issued after this pair's GF math, before its round.
-            if (K > 1) {
+            if (K > 1 && !(EARLY_OUT && pref)) {
 #pragma unroll
                 for (int u = 0; u < SLABS; u++)
                     xn[u] = load16<true>(a.in[1] + (uint64_t(stripe) * a.in_stride[1] + wbyte) + voff[u]);
@@ -446,6 +483,13 @@ __global__ __launch_bounds__(crcdev::sliced(SCHEME) ? 128 * WPE * (WPE - 1) : 51
                     for (int u = 0; u < SLABS; u++)
                         xn[u] = load16<true>(a.in[i + 3] + (uint64_t(stripe) * a.in_stride[i + 3] + wbyte) + voff[u]);
                 }
+                if constexpr (EARLY_OUT) {
+                    if (i + 2 >= K) {  // last pair: rows out and the next tile's loads before its round
+                        __builtin_amdgcn_sched_barrier(0);
+                        emit_outputs();
+                        prefetch_next(K > 1);
+                    }
+                }
                 __builtin_amdgcn_sched_barrier(0);
                 after_stage(two ? i + 1 : i);
                 __builtin_amdgcn_sched_barrier(0);
@@ -504,6 +548,13 @@ __global__ __launch_bounds__(crcdev::sliced(SCHEME) ? 128 * WPE * (WPE - 1) : 51
                     for (int u = 0; u < SLABS; u++)
                         x[u] = load16<true>(a.in[i + 1] + (uint64_t(stripe) * a.in_stride[i + 1] + wbyte) + voff[u]);
                 }
+                if constexpr (EARLY_OUT) {
+                    if (i + 1 == K) {  // last input: rows out and the next tile's input 0 before its round
+                        __builtin_amdgcn_sched_barrier(0);
+                        emit_outputs();
+                        prefetch_next(false);
+                    }
+                }
                 __builtin_amdgcn_sched_barrier(0);
                 after_stage(i);
                 __builtin_amdgcn_sched_barrier(0);
@@ -515,21 +566,23 @@ __global__ __launch_bounds__(crcdev::sliced(SCHEME) ? 128 * WPE * (WPE - 1) : 51
                 }
             }
         }
+        if constexpr (!EARLY_OUT) {
 #pragma unroll
-        for (int j = 0; j < R; j++) {
-            u32x4 o[SLABS];
-            if constexpr (BSL) {
-                bsl_output(j, o);
-            } else {
+            for (int j = 0; j < R; j++) {
+                u32x4 o[SLABS];
+                if constexpr (BSL) {
+                    bsl_output(j, o);
+                } else {
 #pragma unroll
-                for (int u = 0; u < SLABS; u++) o[u] = acc[u][j];
+                    for (int u = 0; u < SLABS; u++) o[u] = acc[u][j];
+                }
+#pragma unroll
+                for (int u = 0; u < SLABS; u++) {
+                    if (live[u]) store16<true>(a.out[j] + (uint64_t(stripe) * a.out_stride[j] + wbyte) + voff[u], o[u]);
+                    if constexpr (!VERIFY) stage_piece((K + j) % SPR, u, o[u]);
+                }
+                if constexpr (!VERIFY) after_stage(K + j);
             }
-#pragma unroll
-            for (int u = 0; u < SLABS; u++) {
-                if (live[u]) store16<true>(a.out[j] + (uint64_t(stripe) * a.out_stride[j] + wbyte) + voff[u], o[u]);
-                if constexpr (!VERIFY) stage_piece((K + j) % SPR, u, o[u]);
-            }
-            if constexpr (!VERIFY) after_stage(K + j);
         }
     }
 }

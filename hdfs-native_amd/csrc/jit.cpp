@@ -101,7 +101,9 @@ Mode mode() {
 // shape: sl = slabs (8, or 4 with inputs in pairs), wpe = waves per SIMD (2,
 // or 3 at 4 slabs: one 768-thread block per CU), pfd = input pairs loaded
 // ahead (4 slabs: 1 or 2) or 3 = loads issued before the parity math (8 slabs)
-// or 4 = one pair / input ahead with the expected sums prefetched per tile
+// or 4 = one pair / input ahead with the expected sums prefetched per tile,
+// 5 = the rebuilt rows stored and the next tile's first inputs loaded before
+// the last CRC round
 struct Shape {
     int slabs, wpe, pfd;
 };
@@ -115,7 +117,7 @@ std::string kernel_name(int k, int e, int kind, Shape sh) {
 bool shape_ok(int k, int e, int kind, Shape sh) {
     return (k == 2 || k == 3 || k == 6 || k == 10) && e >= 1 && e <= 4 && (kind == 0 || kind == 1) &&
            (sh.slabs == 4 || sh.slabs == 8) && (sh.wpe == 2 || (sh.wpe == 3 && sh.slabs == 4)) &&
-           (sh.pfd == 1 || (sh.pfd == 2 && sh.slabs == 4) || (sh.pfd == 3 && sh.slabs == 8) || sh.pfd == 4);
+           (sh.pfd == 1 || (sh.pfd == 2 && sh.slabs == 4) || (sh.pfd == 3 && sh.slabs == 8) || sh.pfd == 4 || sh.pfd == 5);
 }
 
 std::string entry_key(int k, int e, int kind, Shape sh, const uint8_t* matrix) {
@@ -439,7 +441,7 @@ int default_pfd(int, int) { return 1; }
 int pick_pfd(int key, int slabs, int k, int e) {
     if (key == 2 && slabs == 4) return 2;
     if (key == 3 && slabs == 8) return 3;
-    if (key == 4) return 4;
+    if (key == 4 || key == 5) return key;
     return default_pfd(k, e);
 }
 

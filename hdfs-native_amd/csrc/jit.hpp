@@ -51,7 +51,7 @@ bool verify_kernel(int device, int k, int e, int kind, int slabs, int wpe, int p
 int default_slabs(int k, int e);
 int default_pfd(int k, int e);
 // the pfd a measurement-build tune key 24 value asks for at this slab count
-// (2 at 4 slabs, 3 at 8, 4 at either; anything else: default_pfd)
+// (2 at 4 slabs, 3 at 8, 4 and 5 at either; anything else: default_pfd)
 int pick_pfd(int key, int slabs, int k, int e);
 
 // Compiles (or loads from the disk cache) the specialised kernel's code

@@ -84,7 +84,7 @@ int tune_store(int key, int value) {
         case 21: ok = value >= 0 && value <= 3; break;
         case 22: ok = value == 0 || value == 1; break;
         case 23: ok = value == 0 || value == 1; break;
-        case 24: ok = value >= 0 && value <= 4; break;
+        case 24: ok = value >= 0 && value <= 5; break;
         default: ok = false;
     }
     if (!ok) return HEC_ERR_INVALID_ARG;

@@ -65,7 +65,9 @@
  *         bit-sliced encode) each input's loads issued before the parity
  *         math of the previous one, which reads its staged copy; 4 = (JIT
  *         decode + verify) the expected chunk sums loaded once per tile and
- *         shuffled to the CRC rounds
+ *         shuffled to the CRC rounds; 5 = (JIT decode + verify) the rebuilt
+ *         rows stored and the next tile's first inputs loaded before the
+ *         last input's CRC round
  * Returns HEC_OK, or HEC_ERR_INVALID_ARG for an unknown key / value.
  */
 #ifndef HDFS_EC_AMD_EXP_H

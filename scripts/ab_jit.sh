@@ -4,7 +4,9 @@
 # kernel at 8 and 4 slabs (measurement build, tune key 10; AB_VARIANTS adds
 # jit4p2 = two input pairs loaded ahead, jit4w3 = 3 waves per SIMD, jit8p3 = loads
 # issued before the parity math, jit4cold = jit4 compiled in-process from an
-# empty code-object cache, jit8p4 / jit4p4 = expected sums loaded per tile; the
+# empty code-object cache, jit8p4 / jit4p4 = expected sums loaded per tile,
+# jit4p5 / jit8p5 = rebuilt rows stored and the next tile's first inputs loaded
+# before the last CRC round; the
 # encode + CRC leg follows keys 10 / 24 too) -- each variant
 # under rocprofv3 --kernel-trace --stats (no counters), alternated twice.
 # Usage: ab_jit.sh OUTDIR [extra bench args]
@@ -23,6 +25,8 @@ for rep in $(seq 1 ${AB_REPS:-2}); do
       jit8p3) E="HEC_JIT=async"; T="--tune 10=8,24=3";;
       jit8p4) E="HEC_JIT=async"; T="--tune 10=8,24=4";;
       jit4p4) E="HEC_JIT=async"; T="--tune 10=4,24=4";;
+      jit4p5) E="HEC_JIT=async"; T="--tune 10=4,24=5";;
+      jit8p5) E="HEC_JIT=async"; T="--tune 10=8,24=5";;
       jit4cold) E="HEC_JIT=async HEC_JIT_CACHE=$o/cache.$rep.$RANDOM"; T="--tune 10=4";;
     esac
     d="$o/$v.$rep"

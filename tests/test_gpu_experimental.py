@@ -236,6 +236,12 @@ JIT_SHAPE_CASES = [
     (6, 3, (1 << 15) + 512, (0, 2), [(10, 4), (24, 4)], H.CHECKSUM_CRC32C),
     (10, 4, (1 << 14) + 512, (0, 1, 2, 3), [(24, 4)], H.CHECKSUM_CRC32C),
     (3, 2, 8192 + 512, (0, 1), [(24, 4)], H.CHECKSUM_CRC32),
+    (6, 3, 1 << 15, (0, 1, 2), [(24, 5)], H.CHECKSUM_CRC32C),
+    (6, 3, (1 << 15) + 512, (1,), [(24, 5)], H.CHECKSUM_CRC32),
+    (6, 3, (1 << 15) + 512, (0, 2), [(10, 8), (24, 5)], H.CHECKSUM_CRC32C),
+    (10, 4, (1 << 14) + 512, (0, 1, 2, 3), [(24, 5)], H.CHECKSUM_CRC32C),
+    (3, 2, 8192 + 512, (0, 1), [(24, 5)], H.CHECKSUM_CRC32),
+    (2, 1, 8192, (0,), [(24, 5)], H.CHECKSUM_CRC32C),
 ]
 
 
@@ -348,7 +354,7 @@ def test_tune_set_concurrent_with_launches(xlib, dev, c_oracle):
 
 
 def test_tune_set_rejects_unknown_values(xlib):
-    for key, value in [(3, 99), (1, 5), (5, 6), (11, 8), (16, 1), (17, 6), (19, 3), (20, 3), (21, 4), (22, 2), (23, 2), (24, 5), (25, 0), (0, 0)]:
+    for key, value in [(3, 99), (1, 5), (5, 6), (11, 8), (16, 1), (17, 6), (19, 3), (20, 3), (21, 4), (22, 2), (23, 2), (24, 6), (25, 0), (0, 0)]:
         with pytest.raises(ValueError):
             H.tune_set(key, value, xlib)
 
