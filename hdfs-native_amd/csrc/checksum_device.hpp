@@ -144,6 +144,57 @@ __device__ __forceinline__ uint32_t quarter_fold(const uint32_t* t, const uint8_
     }
 }
 
+// Scheme 15 (CRC32C; measurement build): the same fold, then the 256-bit
+// tail through slicing-by-32 tables (checksum_tables.hpp Slice32, 32 KiB):
+// 32 lookups with no dependency between them, one LDS round trip, where the
+// 11-bit tail chains four (each step's index depends on the previous
+// register).  t = the 32 x 256 tables in LDS.
+template <bool REFL>
+__device__ __forceinline__ uint32_t quarter_fold32(const uint32_t* t, const uint8_t* row) {
+    static_assert(REFL, "the fold is for the reflected register");
+    uint32_t w[32];
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const v4u v = *reinterpret_cast<const v4u*>(row + i * 16);
+        w[4 * i] = v.x, w[4 * i + 1] = v.y, w[4 * i + 2] = v.z, w[4 * i + 3] = v.w;
+    }
+#pragma unroll
+    for (int i = 2; i < 32; i++) {
+        uint32_t acc = w[i], pend = 0;
+        bool has = false;
+#pragma unroll
+        for (int o = 0; o < Fold::kN; o++) {
+            const int hi = i - Fold::q[o], lo = hi - 1;
+            const bool h = hi >= 0 && hi < Fold::kDwords, l = lo >= 0 && lo < Fold::kDwords;
+            if (!h && !l) continue;
+            const uint32_t c = h && l ? __builtin_amdgcn_alignbit(w[hi], w[lo], 32 - Fold::s[o])
+                               : h    ? w[hi] << Fold::s[o]
+                                      : w[lo] >> (32 - Fold::s[o]);
+            if (has) {
+                acc = x3(acc, pend, c);
+                has = false;
+            } else {
+                pend = c;
+                has = true;
+            }
+        }
+        w[i] = has ? acc ^ pend : acc;
+    }
+    // tail byte i (0..31) of dwords 24..31 -> t[31 - i][byte]
+    uint32_t v[32];
+#pragma unroll
+    for (int d = 0; d < 8; d++)
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            const int i = 4 * d + b;
+            v[i] = t[(31 - i) * 256 + ((w[Fold::kDwords + d] >> (8 * b)) & 0xFFu)];
+        }
+    uint32_t r = 0;
+#pragma unroll
+    for (int i = 0; i < 32; i += 2) r = x3(r, v[i], v[i + 1]);
+    return r;
+}
+
 template <bool REFL>
 __device__ __forceinline__ uint32_t quarter_s8(const uint32_t (*tab)[256], const uint8_t* row) {
     uint32_t r = 0;
@@ -244,7 +295,8 @@ __device__ __forceinline__ uint32_t apply_shift_nib(const uint32_t (*t)[16], uin
     return v;
 }
 
-// Schemes: 1 = slicing-by-8 (256-thread blocks); 11 = 11-bit slicing (6
+// Schemes: 15 = the fold + a slicing-by-32 tail (CRC32C, measurement);
+// 1 = slicing-by-8 (256-thread blocks); 11 = 11-bit slicing (6
 // lookups per 8 bytes from 40 KiB of tables, nibble shift tables; 256-thread
 // blocks, 2 per CU); 16 = slicing-by-8 in
 // 1024-thread blocks (4 waves per SIMD) with nibble shift tables so the
@@ -252,8 +304,8 @@ __device__ __forceinline__ uint32_t apply_shift_nib(const uint32_t (*t)[16], uin
 // bank-replicated slicing-by-1; 0 = memory side only.
 // 11-bit field tables: 11-bit slicing, the fold (12) and its depth variants (13, 14)
 constexpr bool w11(int scheme) { return scheme >= 11 && scheme <= 14; }
-constexpr bool sliced(int scheme) { return scheme <= 1 || scheme == 16 || w11(scheme); }
-constexpr bool nib_shift(int scheme) { return scheme == 16 || w11(scheme); }
+constexpr bool sliced(int scheme) { return scheme <= 1 || scheme == 15 || scheme == 16 || w11(scheme); }
+constexpr bool nib_shift(int scheme) { return scheme == 15 || scheme == 16 || w11(scheme); }
 
 // slice[8][256] (schemes 1, 16) | rep[256][32] (schemes 4, 8) ; shift[3][4][256]
 // (shift_nib[3][8][16] for scheme 16) ; seg[7][4][256] (schemes 4, 8)
@@ -261,6 +313,7 @@ constexpr bool nib_shift(int scheme) { return scheme == 16 || w11(scheme); }
 template <int SCHEME>
 struct TableLayout {
     static constexpr int kMainWords = SCHEME == 22   ? 2 * 256 * 32 + 4 * 256
+                                      : SCHEME == 15 ? 32 * 256
                                       : w11(SCHEME) ? 4 * 2048 + 2 * 1024
                                       : sliced(SCHEME) ? 8 * 256
                                                        : 256 * 32;
@@ -301,6 +354,8 @@ __device__ __forceinline__ void stage_tables(uint32_t* s, const crc::Tables<KIND
             s[t] = REFL ? v : __builtin_bswap32(v);
         }
         for (int t = threadIdx.x; t < 4 * 256; t += BS) s[2 * 256 * 32 + t] = (&tab.seg[5][0][0])[t];
+    } else if constexpr (SCHEME == 15) {
+        // the slicing-by-32 tables come from their own constant (stage_slice32)
     } else if constexpr (w11(SCHEME)) {
         constexpr int off[6] = {0, 2048, 4096, 5120, 7168, 9216}, len[6] = {2048, 2048, 1024, 2048, 2048, 1024};
 #pragma unroll
@@ -331,6 +386,8 @@ __device__ __forceinline__ uint32_t quarter(const uint32_t* s, const uint8_t* ro
         return quarter_fold<REFL, 16>(s, row);
     else if constexpr (SCHEME == 14)
         return quarter_fold<REFL, 20>(s, row);
+    else if constexpr (SCHEME == 15)
+        return quarter_fold32<REFL>(s, row);
     else if constexpr (sliced(SCHEME))
         return quarter_s8<REFL>(reinterpret_cast<const uint32_t(*)[256]>(s), row);
     else

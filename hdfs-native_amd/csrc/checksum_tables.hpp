@@ -128,5 +128,20 @@ struct Tables {
     }
 };
 
+// Slicing-by-32 byte tables: t[j][x] = the register after byte x then j zero
+// bytes from state 0 (t[0] = the classic table, t[1..7] = Tables::slice), so
+// 32 bytes from state 0 fold to XOR_i t[31 - i][m_i] with no dependency
+// between the lookups (the fused kernels' scheme 15 tail; measurement build).
+template <int KIND>
+struct Slice32 {
+    uint32_t t[32][256]{};
+    constexpr Slice32() {
+        const Tables<KIND> base;
+        for (int x = 0; x < 256; x++) t[0][x] = base.slice[0][x];
+        for (int j = 1; j < 32; j++)
+            for (int x = 0; x < 256; x++) t[j][x] = Tables<KIND>::zero_bytes(t[0], t[j - 1][x], 1);
+    }
+};
+
 }  // namespace crc
 }  // namespace hec

@@ -1521,8 +1521,9 @@ int hec_coder_prepare_decode(hec_coder_t* c, const uint8_t* present, int checksu
                                                                         : hec::jit::default_slabs(int(c->k), e);
         const int pfd = hec::jit::pick_pfd(tn.jit_pfd, slabs, int(c->k), e);
         const int wpe = tn.fused_wpe == 3 && slabs == 4 ? 3 : 2;
+        const int scheme = tn.crc_variant == 12 && kind == 0 ? 15 : 12;  // measurement: slicing-by-32 tail
         const bool ok =
-            hec::jit::verify_kernel(c->device, int(c->k), e, kind, slabs, wpe, pfd, p.matrix.data(), true, &vk);
+            hec::jit::verify_kernel(c->device, int(c->k), e, kind, slabs, wpe, pfd, p.matrix.data(), true, &vk, scheme);
         if (specialised) *specialised = ok ? 1 : 0;
         return int(HEC_OK);
     });

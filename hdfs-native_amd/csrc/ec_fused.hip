@@ -327,8 +327,11 @@ const void* encode_fn(int slabs, int scheme, int wpe, bool pair, bool bsl) {
         if ((scheme == 13 || scheme == 14) && bsl && wpe != 3 && slabs == fused_slabs(K, R) && (slabs == 8 || pair))
             return scheme == 13 ? encode_bsl<K, R, 13, fused_slabs(K, R) == 4>(true)
                                 : encode_bsl<K, R, 14, fused_slabs(K, R) == 4>(true);
+        // slicing-by-32 CRC tail (key 11 = 12)
+        if (scheme == 15 && bsl && wpe != 3 && slabs == fused_slabs(K, R) && (slabs == 8 || pair))
+            return encode_bsl<K, R, 15, fused_slabs(K, R) == 4>(true);
     }
-    if (scheme == 13 || scheme == 14) return nullptr;
+    if (scheme == 13 || scheme == 14 || scheme == 15) return nullptr;
     // bit-sliced parity at 4 slabs in one 768-thread block per CU (3 waves per
     // SIMD; tune key 16 = 3), RS(6,3) and RS(10,4)
     if constexpr ((K == 6 && R == 3) || (K == 10 && R == 4)) {
@@ -365,8 +368,10 @@ const void* verify_fn(int kind, int scheme, int wpe, bool pair) {
             return scheme == 13
                        ? reinterpret_cast<const void*>(&gf_fused_crc<K, R, SL, 13, crc::kCrc32c, true, 2, SL == 4>)
                        : reinterpret_cast<const void*>(&gf_fused_crc<K, R, SL, 14, crc::kCrc32c, true, 2, SL == 4>);
+        if (scheme == 15 && wpe != 3 && kind == crc::kCrc32c)
+            return reinterpret_cast<const void*>(&gf_fused_crc<K, R, SL, 15, crc::kCrc32c, true, 2, SL == 4>);
     }
-    if (scheme == 13 || scheme == 14) return nullptr;
+    if (scheme == 13 || scheme == 14 || scheme == 15) return nullptr;
     if (wpe == 3) return scheme == 11 ? verify_kind<K, R, 11, 3>(kind) : verify_kind<K, R, 1, 3>(kind);
     if (scheme == 12) return verify_kind<K, R, 12>(kind, pair);
     return scheme == 11 ? verify_kind<K, R, 11>(kind, pair) : verify_kind<K, R, 1>(kind, pair);
@@ -436,6 +441,7 @@ int launch_fused(const MatmulArgs& in, const FusedCrcArgs& cs, bool verify, int 
     // measurement: fold depth 16 / 20 dwords (key 11 = 10 / 11)
     const int scheme = tn.crc_variant == 10             ? 13
                        : tn.crc_variant == 11           ? 14
+                       : tn.crc_variant == 12           ? 15
                        : (!verify && tn.crc_variant == 2) ? 4
                        : tn.crc_variant == 6            ? 22
                        : tn.crc_variant == 1            ? 1
@@ -485,7 +491,7 @@ int launch_fused(const MatmulArgs& in, const FusedCrcArgs& cs, bool verify, int 
     // tile geometry below follows it
     jit::VerifyKernel vk;
     int use_slabs = slabs;
-    if (verify && !split && scheme == 12) {
+    if (verify && !split && (scheme == 12 || (scheme == 15 && cs.kind == crc::kCrc32c))) {
         uint8_t mat[kMaxR * kMaxK];
         for (int j = 0; j < a.r; j++)
             for (int i = 0; i < a.k; i++) mat[j * a.k + i] = a.coef[j * kMaxK + i];
@@ -493,7 +499,7 @@ int launch_fused(const MatmulArgs& in, const FusedCrcArgs& cs, bool verify, int 
         const int jp = jit::pick_pfd(tn.jit_pfd, js, a.k, a.r);
         // (3 waves per SIMD: tune key 16 = 3 with key 10 = 4; the launch's
         // `waves` and grid already follow wpe)
-        if (jit::verify_kernel(device, a.k, a.r, cs.kind, js, wpe, jp, mat, false, &vk)) use_slabs = js;
+        if (jit::verify_kernel(device, a.k, a.r, cs.kind, js, wpe, jp, mat, false, &vk, scheme)) use_slabs = js;
     }
     const uint64_t chunks = a.cell_len / 16;
     // split: 4 GF waves x 8 KiB per tile; else waves x slabs x 1 KiB

@@ -51,6 +51,14 @@ __device__ __forceinline__ const crc::Tables<KIND>& fused_tables() {
     else
         return kFusedCksum;
 }
+
+// scheme 15's slicing-by-32 tables (32 KiB), emitted only where a scheme-15
+// kernel is instantiated
+template <int KIND>
+__device__ __forceinline__ const uint32_t* fused_slice32() {
+    static constexpr crc::Slice32<KIND> kT{};
+    return &kT.t[0][0];
+}
 }  // namespace
 
 // Layout: a wave owns SLABS KiB (SLABS slabs of 1 KiB, one 16-B load per
@@ -112,6 +120,11 @@ __global__ __launch_bounds__(crcdev::sliced(SCHEME) ? 128 * WPE * (WPE - 1) : 51
     __shared__ __attribute__((aligned(16))) uint8_t s_stage[WAVES * STAGE];
     prologue<R, BS, K>(a, K, s_tab, s_exp, s_log, s_coef);
     crcdev::stage_tables<SCHEME, BS>(s_ctabs, fused_tables<KIND>());
+    if constexpr (SCHEME == 15) {
+        static_assert(KIND == crc::kCrc32c, "scheme 15 folds the reflected register");
+        const uint32_t* t32 = fused_slice32<KIND>();
+        for (int t = threadIdx.x; t < 32 * 256; t += BS) s_ctabs[t] = t32[t];
+    }
     __syncthreads();
     const uint32_t kfinal = fused_tables<KIND>().final512;
 

@@ -106,23 +106,26 @@ Mode mode() {
 // the last CRC round
 struct Shape {
     int slabs, wpe, pfd;
+    int scheme = 12;  // CRC lookup scheme: 12 (the fold + 11-bit tail), 15 (slicing-by-32 tail; CRC32C)
 };
 
 std::string kernel_name(int k, int e, int kind, Shape sh) {
     return "hec::gf_fused_crc<" + std::to_string(k) + ", " + std::to_string(e) + ", " + std::to_string(sh.slabs) +
-           ", 12, " + std::to_string(kind) + ", true, " + std::to_string(sh.wpe) + ", " +
+           ", " + std::to_string(sh.scheme) + ", " + std::to_string(kind) + ", true, " + std::to_string(sh.wpe) + ", " +
            (sh.slabs == 4 ? "true" : "false") + ", hec::jit_plan::Net, " + std::to_string(sh.pfd) + ">";
 }
 
 bool shape_ok(int k, int e, int kind, Shape sh) {
     return (k == 2 || k == 3 || k == 6 || k == 10) && e >= 1 && e <= 4 && (kind == 0 || kind == 1) &&
            (sh.slabs == 4 || sh.slabs == 8) && (sh.wpe == 2 || (sh.wpe == 3 && sh.slabs == 4)) &&
-           (sh.pfd == 1 || (sh.pfd == 2 && sh.slabs == 4) || (sh.pfd == 3 && sh.slabs == 8) || sh.pfd == 4 || sh.pfd == 5);
+           (sh.pfd == 1 || (sh.pfd == 2 && sh.slabs == 4) || (sh.pfd == 3 && sh.slabs == 8) || sh.pfd == 4 || sh.pfd == 5) &&
+           (sh.scheme == 12 || (sh.scheme == 15 && kind == 0));
 }
 
 std::string entry_key(int k, int e, int kind, Shape sh, const uint8_t* matrix) {
     std::string key = std::to_string(k) + "/" + std::to_string(e) + "/" + std::to_string(kind) + "/" +
-                      std::to_string(sh.slabs) + "/" + std::to_string(sh.wpe) + "/" + std::to_string(sh.pfd) + "/";
+                      std::to_string(sh.slabs) + "/" + std::to_string(sh.wpe) + "/" + std::to_string(sh.pfd) + "/" +
+                      std::to_string(sh.scheme) + "/";
     key.append(reinterpret_cast<const char*>(matrix), size_t(e) * k);
     return key;
 }
@@ -318,8 +321,8 @@ Jit& jit() {
 }  // namespace
 
 bool verify_kernel(int device, int k, int e, int kind, int slabs, int wpe, int pfd, const uint8_t* matrix, bool wait,
-                   VerifyKernel* out) {
-    const Shape sh{slabs, wpe, pfd};
+                   VerifyKernel* out, int scheme) {
+    const Shape sh{slabs, wpe, pfd, scheme};
     if (mode() == Mode::kOff || !shape_ok(k, e, kind, sh)) return false;
     if (!rtc().ok && cache_dir().empty()) return false;
     wait = wait || mode() == Mode::kSync;
@@ -389,8 +392,8 @@ bool verify_kernel(int device, int k, int e, int kind, int slabs, int wpe, int p
     return true;
 }
 
-bool warm(int k, int e, int kind, int slabs, int wpe, int pfd, const uint8_t* matrix) {
-    const Shape sh{slabs, wpe, pfd};
+bool warm(int k, int e, int kind, int slabs, int wpe, int pfd, const uint8_t* matrix, int scheme) {
+    const Shape sh{slabs, wpe, pfd, scheme};
     if (!shape_ok(k, e, kind, sh)) return false;
     const std::string key = entry_key(k, e, kind, sh, matrix);
     Jit& J = jit();

@@ -46,8 +46,10 @@ struct VerifyKernel {
 // from the ahead-of-time kernel's (8 at k <= 6, e <= 3).
 // wpe = waves per SIMD (2, or 3 at 4 slabs: one 768-thread block per CU);
 // pfd = load schedule (1 default; measurement shapes: pick_pfd).
+// scheme = the CRC lookup scheme (12 default; 15 = slicing-by-32 tail,
+// CRC32C only, measurement build)
 bool verify_kernel(int device, int k, int e, int kind, int slabs, int wpe, int pfd, const uint8_t* matrix, bool wait,
-                   VerifyKernel* out);
+                   VerifyKernel* out, int scheme = 12);
 int default_slabs(int k, int e);
 int default_pfd(int k, int e);
 // the pfd a measurement-build tune key 24 value asks for at this slab count
@@ -57,7 +59,7 @@ int pick_pfd(int key, int slabs, int k, int e);
 // Compiles (or loads from the disk cache) the specialised kernel's code
 // object without a device: warms the caches ahead of use.  False when the
 // shape is not covered or the compile failed.
-bool warm(int k, int e, int kind, int slabs, int wpe, int pfd, const uint8_t* matrix);
+bool warm(int k, int e, int kind, int slabs, int wpe, int pfd, const uint8_t* matrix, int scheme = 12);
 
 // Counters for tests and the bench line: kernels compiled (or loaded from
 // the disk cache), compiles failed, launches that used a specialised kernel.

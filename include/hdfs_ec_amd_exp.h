@@ -32,7 +32,9 @@
  *         kernel), 6 = bank-replicated slice-by-2, 9 = memory side only
  *         (WRONG sums), 10 / 11 = the fold over 16 / 20 of the quarter's 32
  *         dwords (512- / 384-bit tail of lookups; CRC32C, RS(6,3) and
- *         RS(10,4) in the fused kernels)
+ *         RS(10,4) in the fused kernels), 12 = the fold with a
+ *         slicing-by-32 tail (32 independent lookups; CRC32C, the same
+ *         fused shapes and the specialised decode + verify)
  * key 12: CRC register prefetch depth in 8-KiB tasks: 0 = default (1 for the
  *         CRC32C fold, else 2), 1 or 2
  * key 13: store cache policy of the pipe kernel (0 = nt, 1 = sc1, 2 = sc0 sc1,

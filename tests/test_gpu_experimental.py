@@ -213,6 +213,13 @@ def test_fused_variants_verify_vs_oracle(xlib, dev, c_oracle, ctype, k, m, cell,
     assert np.array_equal(o[1, 2], data[1, 2])
 
 
+@pytest.mark.parametrize("k,m,cell,S", [(6, 3, 1 << 16, 3), (6, 3, (1 << 15) + 512 + 100, 2), (10, 4, 1 << 15, 2)])
+def test_fused_encode_slice32_tail_vs_oracle(xlib, dev, c_oracle, k, m, cell, S):
+    """Fused encode + CRC32C with the slicing-by-32 CRC tail (tune key 11 =
+    12): parity and every chunk sum, short last chunks included."""
+    test_fused_variants_encode_vs_oracle(xlib, dev, c_oracle, k, m, cell, S, [(11, 12)])
+
+
 def _xjit_launches(xlib):
     import ctypes
     v = [ctypes.c_uint64(0) for _ in range(4)]
@@ -242,6 +249,10 @@ JIT_SHAPE_CASES = [
     (10, 4, (1 << 14) + 512, (0, 1, 2, 3), [(24, 5)], H.CHECKSUM_CRC32C),
     (3, 2, 8192 + 512, (0, 1), [(24, 5)], H.CHECKSUM_CRC32),
     (2, 1, 8192, (0,), [(24, 5)], H.CHECKSUM_CRC32C),
+    (6, 3, 1 << 15, (0, 1, 2), [(11, 12)], H.CHECKSUM_CRC32C),
+    (6, 3, (1 << 15) + 512, (1,), [(11, 12)], H.CHECKSUM_CRC32C),
+    (10, 4, (1 << 14) + 512, (0, 1, 2, 3), [(11, 12)], H.CHECKSUM_CRC32C),
+    (3, 2, 8192 + 512, (0, 1), [(11, 12), (10, 8)], H.CHECKSUM_CRC32C),
 ]
 
 
