@@ -6,7 +6,8 @@
 # issued before the parity math, jit4cold = jit4 compiled in-process from an
 # empty code-object cache, jit8p4 / jit4p4 = expected sums loaded per tile,
 # jit4p5 / jit8p5 = rebuilt rows stored and the next tile's first inputs loaded
-# before the last CRC round; the
+# before the last CRC round, jitdef = the measurement build at its defaults,
+# s15 = the CRC tail through slicing-by-32 tables (key 11 = 12); the
 # encode + CRC leg follows keys 10 / 24 too) -- each variant
 # under rocprofv3 --kernel-trace --stats (no counters), alternated twice.
 # Usage: ab_jit.sh OUTDIR [extra bench args]
@@ -26,6 +27,8 @@ for rep in $(seq 1 ${AB_REPS:-2}); do
       jit8p4) E="HEC_JIT=async"; T="--tune 10=8,24=4";;
       jit4p4) E="HEC_JIT=async"; T="--tune 10=4,24=4";;
       jit4p5) E="HEC_JIT=async"; T="--tune 10=4,24=5";;
+      jitdef) E="HEC_JIT=async"; T="--tune 11=0";;
+      s15) E="HEC_JIT=async"; T="--tune 11=12";;
       jit8p5) E="HEC_JIT=async"; T="--tune 10=8,24=5";;
       jit4cold) E="HEC_JIT=async HEC_JIT_CACHE=$o/cache.$rep.$RANDOM"; T="--tune 10=4";;
     esac
