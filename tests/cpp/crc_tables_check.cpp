@@ -10,6 +10,8 @@
 //         11-bit slicing over its last 32 B (checksum_device.hpp Fold);
 //   byte: the classic byte-serial loop, from the table slot the 11-bit
 //         scheme's tail reads (w11[5][x]);
+//   fold32: (CRC32C) the same fold, then the last 32 B through the
+//         slicing-by-32 tables (Slice32, measurement scheme 15);
 // and printed as hex, one line per chunk, for tests/test_oracle.py to compare
 // with the oracle.  Input: splitmix64 bytes (seed argv[1], chunks argv[2]).
 #include <cstdint>
@@ -71,7 +73,8 @@ struct Check {
     }
     // scheme 12: the kernel's fold, the same offsets (32q + s) and order
     // (fd = folded dwords: 24 for scheme 12, 16 / 20 for the measurement schemes 13 / 14)
-    uint32_t q_fold(const uint8_t* q, int fd = 24) const {
+    // s32 = Slice32 tables: the tail's 32 bytes as independent lookups (scheme 15)
+    uint32_t q_fold(const uint8_t* q, int fd = 24, const Slice32<KIND>* s32 = nullptr) const {
         static const int kq[5] = {6, 6, 5, 4, 2}, ks[5] = {17, 3, 10, 27, 1};
         uint32_t w[32];
         for (int i = 0; i < 32; i++) w[i] = le32(q + 4 * i);
@@ -82,6 +85,10 @@ struct Check {
                 w[i] ^= (h << ks[o]) | (l >> (32 - ks[o]));
             }
         uint32_t r = 0;
+        if (s32) {
+            for (int i = 0; i < 32; i++) r ^= s32->t[31 - i][(w[24 + i / 4] >> (8 * (i % 4))) & 0xFF];
+            return r;
+        }
         for (int i = fd; i < 32; i += 2) {
             const uint32_t lo = w[i] ^ pre(r), hi = w[i + 1];
             r = t.w11[0][f0(lo)] ^ t.w11[1][f1(lo)] ^ t.w11[2][f2(lo)] ^ t.w11[3][f0(hi)] ^ t.w11[4][f1(hi)] ^
@@ -89,10 +96,11 @@ struct Check {
         }
         return r;
     }
-    uint32_t chunk(const uint8_t* c, bool w11, bool fold = false, int fd = 24) const {
+    uint32_t chunk(const uint8_t* c, bool w11, bool fold = false, int fd = 24,
+                   const Slice32<KIND>* s32 = nullptr) const {
         uint32_t v = 0;
         for (int qi = 0; qi < 4; qi++) {
-            const uint32_t r = fold ? q_fold(c + 128 * qi, fd) : w11 ? q_w11(c + 128 * qi) : q_s8(c + 128 * qi);
+            const uint32_t r = fold ? q_fold(c + 128 * qi, fd, s32) : w11 ? q_w11(c + 128 * qi) : q_s8(c + 128 * qi);
             v ^= qi < 3 ? (w11 ? shift_nib(qi, r) : shift_byte(qi, r)) : r;
         }
         return v ^ t.final512;
@@ -109,6 +117,7 @@ struct Check {
 
 static const Tables<kCrc32c> kT32c;
 static const Tables<kCksum> kTck;
+static const Slice32<kCrc32c> kS32c;
 
 int main(int argc, char** argv) {
     uint64_t seed = argc > 1 ? std::strtoull(argv[1], nullptr, 0) : 1;
@@ -122,9 +131,10 @@ int main(int argc, char** argv) {
     Check<kCksum> cck(kTck);
     for (int k = 0; k < chunks; k++) {
         const uint8_t* c = data.data() + 512 * k;
-        std::printf("%08x %08x %08x %08x %08x %08x %08x %08x %08x\n", c32c.chunk(c, false), c32c.chunk(c, true),
+        std::printf("%08x %08x %08x %08x %08x %08x %08x %08x %08x %08x\n", c32c.chunk(c, false), c32c.chunk(c, true),
                     c32c.chunk_bytes(c), cck.chunk(c, false), cck.chunk(c, true), cck.chunk_bytes(c),
-                    c32c.chunk(c, true, true), c32c.chunk(c, true, true, 16), c32c.chunk(c, true, true, 20));
+                    c32c.chunk(c, true, true), c32c.chunk(c, true, true, 16), c32c.chunk(c, true, true, 20),
+                    c32c.chunk(c, true, true, 24, &kS32c));
     }
     std::fflush(stdout);
     // the data itself, for the oracle side

@@ -306,14 +306,15 @@ def test_device_crc_tables_vs_oracle(tmp_path):
     data = res.stderr
     assert len(data) == 512 * chunks
     lines = res.stdout.decode().split()
-    assert len(lines) == 9 * chunks
+    assert len(lines) == 10 * chunks
     for i in range(chunks):
         c = data[512 * i:512 * (i + 1)]
         want32c = O.chunk_checksums(c, 512, O.CHECKSUM_CRC32C).hex()
         want32 = O.chunk_checksums(c, 512, O.CHECKSUM_CRC32).hex()
-        row = lines[9 * i:9 * i + 9]
-        # s8, w11, byte, fold 24 (scheme 12), fold 16 / 20 (measurement schemes 13 / 14)
-        assert row[0:3] + row[6:9] == [want32c] * 6, i
+        row = lines[10 * i:10 * i + 10]
+        # s8, w11, byte, fold 24 (scheme 12), fold 16 / 20 (measurement schemes 13 / 14),
+        # fold 24 + slicing-by-32 tail (measurement scheme 15)
+        assert row[0:3] + row[6:10] == [want32c] * 7, i
         assert row[3:6] == [want32] * 3, i
 
 
