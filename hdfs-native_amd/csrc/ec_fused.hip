@@ -482,7 +482,9 @@ int launch_fused(const MatmulArgs& in, const FusedCrcArgs& cs, bool verify, int 
             case 10: fn = pick_r<10>(verify, a.r, slabs, scheme, cs.kind, wpe, pair, bsl); break;
             default: return -1;
         }
-        if (!fn) return -1;  // a measurement scheme not compiled for this shape
+        // a measurement scheme not compiled for this shape (decode + verify:
+        // unless its specialised kernel is ready, below)
+        if (!fn && !verify) return -1;
     }
     if (!aligned) return -1;
     // decode + verify at the default scheme: the plan's own bit-sliced network
@@ -501,6 +503,7 @@ int launch_fused(const MatmulArgs& in, const FusedCrcArgs& cs, bool verify, int 
         // `waves` and grid already follow wpe)
         if (jit::verify_kernel(device, a.k, a.r, cs.kind, js, wpe, jp, mat, false, &vk, scheme)) use_slabs = js;
     }
+    if (!fn && !vk.fn) return -1;
     const uint64_t chunks = a.cell_len / 16;
     // split: 4 GF waves x 8 KiB per tile; else waves x slabs x 1 KiB
     const uint64_t tile_bytes = split ? 4u * 8192u : 1024u * uint64_t(use_slabs) * uint64_t(waves);
@@ -512,6 +515,7 @@ int launch_fused(const MatmulArgs& in, const FusedCrcArgs& cs, bool verify, int 
     a.tiles_per_stripe = uint32_t(tps);
     a.total_tiles = uint32_t(total);
     tile_order(a.stripes, a.tiles_per_stripe, tn.group > 0 ? uint32_t(tn.group) : 4u, a.group, a.grouped_tiles);
+    a.col_rot = uint32_t(tn.col_rot);  // measurement (key 25); 0 in the product
     // LDS: ~61 KiB per 256-thread block (two per CU) / ~131 KiB per 512-thread block (one)
     // a grid of 8 blocks per CU (2 or 1 resident): finer-grained dynamic
     // scheduling beats exactly the resident blocks by 3 % (RS(6,3)) to 5 %

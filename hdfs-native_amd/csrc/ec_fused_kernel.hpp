@@ -142,13 +142,23 @@ __global__ __launch_bounds__(crcdev::sliced(SCHEME) ? 128 * WPE * (WPE - 1) : 51
     uint32_t* out_sums = reinterpret_cast<uint32_t*>(cs.sums);
     const uint32_t* exp_sums = reinterpret_cast<const uint32_t*>(cs.expected);
 
+    // tile -> (stripe, column), with the columns of stripe s rotated by
+    // s * col_rot (measurement: concurrent stripes of a tile-order group then
+    // sit at different offsets of their cells)
+    auto coords = [&](uint32_t t, uint32_t& stripe, uint32_t& tcol) {
+        tile_coords(t, a, stripe, tcol);
+        if (a.col_rot) {
+            tcol += (stripe * a.col_rot) % a.tiles_per_stripe;
+            if (tcol >= a.tiles_per_stripe) tcol -= a.tiles_per_stripe;
+        }
+    };
     // PFD = 3: x already holds this tile's input 0 (loaded during the
     // previous tile's outputs)
     bool have_next = false;
     u32x4 x[SLABS], xn[SLABS];
     for (uint32_t tile = blockIdx.x; tile < total; tile += gridDim.x) {
         uint32_t stripe, tcol;
-        tile_coords(tile, a, stripe, tcol);
+        coords(tile, stripe, tcol);
         const uint64_t wbyte = uint64_t(tcol) * TILE_BYTES + uint64_t(wave) * WAVE_BYTES;  // wave's first byte
         if (wbyte >= cell_len) continue;  // wave-uniform (never a prefetched tile: those are full)
         // 32-bit lane offsets from a wave-uniform per-shard base (saddr +
@@ -316,7 +326,7 @@ __global__ __launch_bounds__(crcdev::sliced(SCHEME) ? 128 * WPE * (WPE - 1) : 51
             const uint32_t nt = tile + gridDim.x;
             if (nt < total) {
                 uint32_t ns, ncol;
-                tile_coords(nt, a, ns, ncol);
+                coords(nt, ns, ncol);
                 const uint64_t nw = uint64_t(ncol) * TILE_BYTES + uint64_t(wave) * WAVE_BYTES;
                 if (nw + WAVE_BYTES <= cell_len) {  // wave-uniform
 #pragma unroll

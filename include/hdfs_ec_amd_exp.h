@@ -70,6 +70,8 @@
  *         shuffled to the CRC rounds; 5 = (JIT decode + verify) the rebuilt
  *         rows stored and the next tile's first inputs loaded before the
  *         last input's CRC round
+ * key 25: fused kernels: stripe s starts its tile columns at (s * value) mod
+ *         the tiles per stripe (0 = default, no rotation; up to 4096)
  * Returns HEC_OK, or HEC_ERR_INVALID_ARG for an unknown key / value.
  */
 #ifndef HDFS_EC_AMD_EXP_H

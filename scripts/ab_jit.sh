@@ -7,7 +7,8 @@
 # empty code-object cache, jit8p4 / jit4p4 = expected sums loaded per tile,
 # jit4p5 / jit8p5 = rebuilt rows stored and the next tile's first inputs loaded
 # before the last CRC round, jitdef = the measurement build at its defaults,
-# s15 = the CRC tail through slicing-by-32 tables (key 11 = 12); the
+# s15 = the CRC tail through slicing-by-32 tables (key 11 = 12), rotN = the
+# per-stripe column rotation key 25 = N; the
 # encode + CRC leg follows keys 10 / 24 too) -- each variant
 # under rocprofv3 --kernel-trace --stats (no counters), alternated twice.
 # Usage: ab_jit.sh OUTDIR [extra bench args]
@@ -29,6 +30,7 @@ for rep in $(seq 1 ${AB_REPS:-2}); do
       jit4p5) E="HEC_JIT=async"; T="--tune 10=4,24=5";;
       jitdef) E="HEC_JIT=async"; T="--tune 11=0";;
       s15) E="HEC_JIT=async"; T="--tune 11=12";;
+      rot*) E="HEC_JIT=async"; T="--tune 25=${v#rot}";;
       jit8p5) E="HEC_JIT=async"; T="--tune 10=8,24=5";;
       jit4cold) E="HEC_JIT=async HEC_JIT_CACHE=$o/cache.$rep.$RANDOM"; T="--tune 10=4";;
     esac
