@@ -9,3 +9,6 @@ timeout -k 10 420 python3 -u -m pytest tests/test_gpu_experimental.py -m gpu -v 
 rc=$?; tail -3 $o/tests_new.txt; [ $rc -le 1 ] || exit 1
 AB_REPS=4 AB_VARIANTS="jitdef rot1 rot16 rot21" bash scripts/ab_jit.sh $o/ab > $o/ab_summary.txt 2>&1 || { tail -20 $o/ab_summary.txt; exit 1; }
 grep -E "6, 3, (8|4), 12, 0, (true|false)" $o/ab_summary.txt | cut -c1-110; grep " leg " $o/ab_summary.txt | cut -c1-40
+# the same kernels over five fresh buffer sets in one process (placement)
+PROBE_SETS=6 timeout -k 10 300 python3 -u scripts/probe_placement.py > $o/placement.txt 2>&1 || { tail $o/placement.txt; exit 2; }
+cat $o/placement.txt
