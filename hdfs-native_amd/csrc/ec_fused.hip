@@ -517,10 +517,12 @@ int launch_fused(const MatmulArgs& in, const FusedCrcArgs& cs, bool verify, int 
     tile_order(a.stripes, a.tiles_per_stripe, tn.group > 0 ? uint32_t(tn.group) : 4u, a.group, a.grouped_tiles);
     a.col_rot = uint32_t(tn.col_rot);  // measurement (key 25); 0 in the product
     // LDS: ~61 KiB per 256-thread block (two per CU) / ~131 KiB per 512-thread block (one)
-    // a grid of 8 blocks per CU (2 or 1 resident): finer-grained dynamic
+    // a grid of 16 blocks per CU (2 resident): finer-grained dynamic
     // scheduling beats exactly the resident blocks by 3 % (RS(6,3)) to 5 %
-    // (RS(10,4))
-    uint64_t grid = tn.grid ? uint64_t(tn.grid) : uint64_t(num_cus(device)) * ((split || wpe == 3) ? 4 : 8);
+    // (RS(10,4)) at 8 per CU, and 16 beats 8 by 1-2 % on the
+    // same buffers (profiles/r04n: decode + verify 1.728 vs 1.747 ms, encode +
+    // CRC 1.776 vs 1.803, mean of 3 placements x 2 rounds)
+    uint64_t grid = tn.grid ? uint64_t(tn.grid) : uint64_t(num_cus(device)) * ((split || wpe == 3) ? 4 : 16);
     if (grid > total) grid = total;
     FusedCrcArgs c = cs;
     void* args[] = {&a, &c};
