@@ -21,6 +21,13 @@ import hdfs_native_ec as H  # noqa: E402
 # name -> tune pairs; every key not named is reset to 0 before a configuration
 CONFIGS = {
     "default": [],
+    "grp16": [(8, 16)],
+    "grid32": [(7, 32 * 256)],
+    "grp8grid32": [(8, 8), (7, 32 * 256)],
+    "enc4": [(10, 4)],
+    "grid8": [(7, 8 * 256)],
+    "grid64": [(7, 64 * 256)],
+    "grp8grid16": [(8, 8), (7, 16 * 256)],
     "grp1": [(8, 1)],
     "grp2": [(8, 2)],
     "grp8": [(8, 8)],
