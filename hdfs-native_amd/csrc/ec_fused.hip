@@ -514,15 +514,20 @@ int launch_fused(const MatmulArgs& in, const FusedCrcArgs& cs, bool verify, int 
     a.chunks = uint32_t(chunks);
     a.tiles_per_stripe = uint32_t(tps);
     a.total_tiles = uint32_t(total);
-    tile_order(a.stripes, a.tiles_per_stripe, tn.group > 0 ? uint32_t(tn.group) : 4u, a.group, a.grouped_tiles);
+    // tile order: groups of 8 stripes (the register kernels keep 4); same
+    // buffers, 3 placements x 3 rounds (profiles/r04p): with 32 blocks per CU,
+    // encode + CRC 1.720 vs 1.727 ms for 4-stripe groups, 1.737-1.759 at 16
+    // blocks per CU; decode + verify level
+    tile_order(a.stripes, a.tiles_per_stripe, tn.group > 0 ? uint32_t(tn.group) : 8u, a.group, a.grouped_tiles);
     a.col_rot = uint32_t(tn.col_rot);  // measurement (key 25); 0 in the product
     // LDS: ~61 KiB per 256-thread block (two per CU) / ~131 KiB per 512-thread block (one)
-    // a grid of 16 blocks per CU (2 resident): finer-grained dynamic
+    // a grid of 32 blocks per CU (2 resident): finer-grained dynamic
     // scheduling beats exactly the resident blocks by 3 % (RS(6,3)) to 5 %
-    // (RS(10,4)) at 8 per CU, and 16 beats 8 by 1-2 % on the
-    // same buffers (profiles/r04n: decode + verify 1.728 vs 1.747 ms, encode +
-    // CRC 1.776 vs 1.803, mean of 3 placements x 2 rounds)
-    uint64_t grid = tn.grid ? uint64_t(tn.grid) : uint64_t(num_cus(device)) * ((split || wpe == 3) ? 4 : 16);
+    // (RS(10,4)) at 8 per CU; on the same buffers 16 beats 8
+    // by 1-2 % (profiles/r04n: decode + verify 1.728 vs 1.747 ms, encode +
+    // CRC 1.776 vs 1.803), 32 beats 8 by 1.5-2 % (r04o) and ties 16 (r04p;
+    // 64: 1-2 % slower)
+    uint64_t grid = tn.grid ? uint64_t(tn.grid) : uint64_t(num_cus(device)) * ((split || wpe == 3) ? 4 : 32);
     if (grid > total) grid = total;
     FusedCrcArgs c = cs;
     void* args[] = {&a, &c};
