@@ -4,6 +4,8 @@ RS(6,3) 1 MiB x 1024 data / parity / output tensors (the earlier sets stay
 allocated, so every set gets new memory), encode + CRC32C sums, the
 {0,1,2}-lost plan prepared (the specialised kernel), then the fused decode +
 verify and the fused encode + CRC timed with HIP events.  One line per set.
+PROBE_CROSS=1 then times decode + verify for every (input set, output set)
+pair: does the speed follow where the survivors or the rebuilt rows land?
   python3 scripts/probe_placement.py
 """
 import os
@@ -69,6 +71,33 @@ def main():
               f"med {res['decode_verify'][1]:.4f} ms  encode_crc min {res['encode_crc'][0]:.4f} "
               f"med {res['encode_crc'][1]:.4f} ms", flush=True)
         time.sleep(0.2)
+    if os.environ.get("PROBE_CROSS") == "1":
+        print("decode + verify, best of 8 (ms): rows = input set, columns = output set", flush=True)
+        for i, (d, p, _o, sums, bad) in enumerate(keep):
+            dp, ds = H.stripe_layout_ptrs(d, k)
+            pp, ps = H.stripe_layout_ptrs(p, m)
+            shard_ptrs = [None if x in miss else dp[x] for x in range(k)] + pp
+            row = []
+            for j in range(len(keep)):
+                op, os_ = H.stripe_layout_ptrs(keep[j][2], k)
+                vo = [op[x] if x in miss else dp[x] for x in range(k)]
+                vs = [os_[0] if x in miss else ds[x] for x in range(k)]
+
+                def dv():
+                    coder.decode_verify_device(H.CHECKSUM_CRC32C, shard_ptrs, ds + ps, vo, vs, cell, S, bpc,
+                                               sums.data_ptr(), bad.data_ptr(), sp)
+                dv()
+                torch.cuda.synchronize()
+                best = 1e9
+                for _ in range(reps):
+                    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    a.record(stream)
+                    dv()
+                    b.record(stream)
+                    torch.cuda.synchronize()
+                    best = min(best, a.elapsed_time(b))
+                row.append(best)
+            print(f"in {i}: " + "  ".join(f"{t:.4f}" for t in row), flush=True)
 
 
 if __name__ == "__main__":
