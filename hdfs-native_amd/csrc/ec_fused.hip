@@ -519,8 +519,7 @@ int launch_fused(const MatmulArgs& in, const FusedCrcArgs& cs, bool verify, int 
     // encode + CRC 1.720 vs 1.727 ms for 4-stripe groups, 1.737-1.759 at 16
     // blocks per CU; decode + verify level
     tile_order(a.stripes, a.tiles_per_stripe, tn.group > 0 ? uint32_t(tn.group) : 8u, a.group, a.grouped_tiles);
-    a.col_rot = uint32_t(tn.col_rot);      // measurement (key 25); 0 in the product
-    a.store_pol = uint32_t(tn.fused_store);  // measurement (key 26); 0 in the product
+    a.col_rot = uint32_t(tn.col_rot);  // measurement (key 25); 0 in the product
     // LDS: ~61 KiB per 256-thread block (two per CU) / ~131 KiB per 512-thread block (one)
     // a grid of 32 blocks per CU (2 resident): finer-grained dynamic
     // scheduling beats exactly the resident blocks by 3 % (RS(6,3)) to 5 %

@@ -356,13 +356,7 @@ __global__ __launch_bounds__(crcdev::sliced(SCHEME) ? 128 * WPE * (WPE - 1) : 51
                 }
 #pragma unroll
                 for (int u = 0; u < SLABS; u++) {
-                    if (live[u]) {
-                        uint8_t* dst = a.out[j] + (uint64_t(stripe) * a.out_stride[j] + wbyte) + voff[u];
-                        if (a.store_pol)
-                            store16<false>(dst, o[u]);
-                        else
-                            store16<true>(dst, o[u]);
-                    }
+                    if (live[u]) store16<true>(a.out[j] + (uint64_t(stripe) * a.out_stride[j] + wbyte) + voff[u], o[u]);
                     if constexpr (!VERIFY) stage_piece((K + j) % SPR, u, o[u]);
                 }
                 if constexpr (!VERIFY) after_stage(K + j);
@@ -607,13 +601,7 @@ __global__ __launch_bounds__(crcdev::sliced(SCHEME) ? 128 * WPE * (WPE - 1) : 51
                 }
 #pragma unroll
                 for (int u = 0; u < SLABS; u++) {
-                    if (live[u]) {
-                        uint8_t* dst = a.out[j] + (uint64_t(stripe) * a.out_stride[j] + wbyte) + voff[u];
-                        if (a.store_pol)
-                            store16<false>(dst, o[u]);
-                        else
-                            store16<true>(dst, o[u]);
-                    }
+                    if (live[u]) store16<true>(a.out[j] + (uint64_t(stripe) * a.out_stride[j] + wbyte) + voff[u], o[u]);
                     if constexpr (!VERIFY) stage_piece((K + j) % SPR, u, o[u]);
                 }
                 if constexpr (!VERIFY) after_stage(K + j);

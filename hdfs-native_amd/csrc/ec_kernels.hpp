@@ -37,7 +37,6 @@ struct MatmulArgs {
     uint32_t grouped_tiles;       // tiles of the whole G-stripe groups; the remainder stripes go stripe-major
     uint32_t drain;               // register kernel: 1 = wait for the tile's stores before the next tile's loads
     uint32_t col_rot = 0;         // tile order: stripe s starts its columns at (s * col_rot) % tiles (0 = none)
-    uint32_t store_pol = 0;       // fused kernels' row stores: 0 = non-temporal, 1 = default policy (measurement)
 };
 
 // One coefficient's v_perm_b32 product tables (see ec_kernels.hip): c*x =

@@ -15,7 +15,7 @@ namespace {
 std::atomic<int> g_cus[64];
 
 #ifdef HEC_EXPERIMENTAL
-constexpr int kKeys = 26;
+constexpr int kKeys = 25;
 std::atomic<int> g_knob[kKeys + 1];  // index = key; zero-initialised (static storage)
 std::atomic<int> g_nt{-1};           // key 2 defaults to -1 (non-temporal on)
 
@@ -52,7 +52,6 @@ Tune tune_snapshot() {
     t.matmul_bsl = load(23);
     t.jit_pfd = load(24);
     t.col_rot = load(25);
-    t.fused_store = load(26);
     return t;
 }
 
@@ -88,7 +87,6 @@ int tune_store(int key, int value) {
         case 23: ok = value == 0 || value == 1; break;
         case 24: ok = value >= 0 && value <= 5; break;
         case 25: ok = value >= 0 && value <= 4096; break;
-        case 26: ok = value == 0 || value == 1; break;
         default: ok = false;
     }
     if (!ok) return HEC_ERR_INVALID_ARG;

@@ -46,7 +46,6 @@ struct Tune {
     int fused_split = 0;        // key 21: fused kernels' wave roles: 0 default = 1 = every wave alternates (2 / 3 role-split)
     int fused_bsl = 0;          // key 22: fused encode parity: 0 default = bit-sliced for the RS matrix, 1 = v_perm tables
     int matmul_bsl = 0;         // key 23: register / LDS-DMA encode: 0 default = v_perm tables, 1 = bit-sliced RS parity (rejected)
-    int fused_store = 0;        // key 26: fused kernels' row stores: 0 default non-temporal, 1 default cache policy
     int col_rot = 0;            // key 25: fused kernels' per-stripe column rotation (tiles per stripe index; 0 = none)
     int jit_pfd = 0;            // key 24: fused load schedule (0 default, 2 = two pairs ahead at 4 slabs, 3 = early issue at 8, 4 = sums per tile, 5 = early outputs)
 };

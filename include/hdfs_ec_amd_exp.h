@@ -72,8 +72,6 @@
  *         last input's CRC round
  * key 25: fused kernels: stripe s starts its tile columns at (s * value) mod
  *         the tiles per stripe (0 = default, no rotation; up to 4096)
- * key 26: fused kernels' stores of the coded rows: 0 = default
- *         (non-temporal), 1 = the default cache policy
  * Returns HEC_OK, or HEC_ERR_INVALID_ARG for an unknown key / value.
  */
 #ifndef HDFS_EC_AMD_EXP_H

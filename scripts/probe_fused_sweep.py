@@ -27,7 +27,6 @@ CONFIGS = {
     "enc4": [(10, 4)],
     "grid8": [(7, 8 * 256)],
     "grid64": [(7, 64 * 256)],
-    "cached": [(26, 1)],
     "grp8grid16": [(8, 8), (7, 16 * 256)],
     "grp1": [(8, 1)],
     "grp2": [(8, 2)],
@@ -36,7 +35,7 @@ CONFIGS = {
     "grid16": [(7, 16 * 256)],
     "slabs8": [(10, 8)],
 }
-KEYS = (7, 8, 10, 26)
+KEYS = (7, 8, 10)
 
 
 def main():

@@ -148,7 +148,7 @@ FUSED_TUNES = [[(11, 2)], [(11, 6)], [(16, 3)], [(16, 3), (11, 1)]]
 
 @pytest.mark.parametrize("k,m,cell,S", [(6, 3, 1 << 16, 3), (10, 4, 1 << 15, 2), (3, 2, 8192 + 512, 4)])
 @pytest.mark.parametrize("tunes", FUSED_TUNES + [[(22, 1)], [(22, 1), (5, 0)], [(24, 3)], [(10, 4)], [(10, 4), (24, 2)],
-                                   [(25, 1)], [(25, 7), (10, 4)], [(26, 1)]])
+                                   [(25, 1)], [(25, 7), (10, 4)]])
 def test_fused_variants_encode_vs_oracle(xlib, dev, c_oracle, k, m, cell, S, tunes):
     """Fused encode + CRC32C with the rejected variants: bank-replicated
     slicing-by-1 / -by-2 tables (tune key 11 = 2 / 6), one 768-thread block
@@ -258,7 +258,6 @@ JIT_SHAPE_CASES = [
     (6, 3, (1 << 15) + 512, (0, 1, 2), [(25, 1)], H.CHECKSUM_CRC32C),
     (10, 4, (1 << 16) + 512, (0, 3), [(25, 7)], H.CHECKSUM_CRC32),
     (6, 3, (1 << 16) + 512, (2,), [(25, 5), (24, 3), (10, 8)], H.CHECKSUM_CRC32C),
-    (6, 3, (1 << 15) + 512, (0, 1, 2), [(26, 1)], H.CHECKSUM_CRC32C),
 ]
 
 
