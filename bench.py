@@ -91,6 +91,8 @@ def parse(argv=None):
                     help="also time the other multi-GPU BASELINE configs (RS(10,4) 1 MiB x 2048 and RS(6,3) "
                          "64 KiB x 65536, both split over the ranks): 1 = yes, 0 = no, -1 = default (yes for the "
                          "default RS(6,3) run)")
+    ap.add_argument("--rows-call-host", action="store_true",
+                    help="internal: the host-routine side of host_path.rows_call (child process, no GPU)")
     ap.add_argument("--verify", default="full", choices=["full", "sample"],
                     help="post-timing correctness gate: every stripe against the C oracle (full) or stripe 0")
     return ap.parse_args(argv)
@@ -188,16 +190,18 @@ def cpu_baseline(k, m, cell, seconds, threads=1):
     return res
 
 
-def cpu_config_batch(H, k, m, cell, stripes, threads):
-    """BASELINE.json configs[0] -- RS(3,2) 1 MiB cells, a 1024-stripe batch on
-    the CPU (the reference's rust/benches/ec.rs:16-33 path, no GPU): the
-    whole batch encoded, then decoded with data shards 0..m-1 missing, by the
-    C restatement of the reference loop (kind "port", orc_encode_batch /
+def cpu_config_batch(H, k, m, cell, stripes, threads, config_stripes=None, source="BASELINE.json configs[0]"):
+    """A BASELINE.json config on the CPU (the reference's rust/benches/ec.rs:
+    16-63 shape, no GPU): `stripes` stripes encoded, then decoded with data
+    shards 0..m-1 missing (the worst case each config names), by the C
+    restatement of the reference loop (kind "port", orc_encode_batch /
     orc_decode_batch over contiguous stripe slices) and by the engine's own
-    host routine (hec_encode / hec_decode per stripe on host-only coders,
-    as the per-row drop-in calls it without a GPU), each on 1 thread
-    and on the box's CPU share.  The engine's parity is checked against the
-    port's for every stripe."""
+    host routine (hec_encode / hec_decode per stripe on host-only coders, as
+    the per-row drop-in calls it without a GPU), each on 1 thread and on the
+    box's CPU share.  configs[0] (RS(3,2) 1 MiB x 1024) runs whole; for the
+    GPU configs `stripes` is a bounded sample of the config's
+    `config_stripes` (stated in the record).  The engine's parity is checked
+    against the port's for every stripe."""
     import ctypes
 
     import numpy as np
@@ -254,12 +258,17 @@ def cpu_config_batch(H, k, m, cell, stripes, threads):
             out[f"{kind}_{th}t"] = {"value": round(2 * stripes * k * cell / GIB / el, 4), "unit": "GiB/s",
                                     "cores": th, "seconds": round(el, 3),
                                     "kind": "port" if kind == "port" else "engine"}
+    whole = config_stripes is None or config_stripes == stripes
     return {"config": f"RS({k},{m}) {cell} B cells, {stripes}-stripe batch, encode + decode data 0..{m - 1} missing "
-                      f"(BASELINE.json configs[0], rust/benches/ec.rs:16-33)",
+                      f"({source}, rust/benches/ec.rs:16-63)",
+            "stripes_timed": stripes, "config_stripes": config_stripes or stripes,
+            "sample": "the whole batch" if whole else
+                      f"a bounded sample: {stripes} of the config's {config_stripes} stripes (same per-stripe work; "
+                      f"stripes are independent, so GiB/s is the config's rate on this host)",
             "legs": out, "host_isa": H.host_isa(), "host": host_info(),
             "note": "port = oracle/ec_oracle.c (restates matrix.rs:204-231; the Rust path is unbuildable here), "
-                    "engine = hec_encode / hec_decode per stripe on the host routine; the whole batch, not a "
-                    "sample; every stripe's engine parity == port parity, rebuilt cells == data"}
+                    "engine = hec_encode / hec_decode per stripe on the host routine; every timed stripe's "
+                    "engine parity == port parity, rebuilt cells == data"}
 
 
 def traffic_for(path, k, m, cell, stripes, mode):
@@ -274,6 +283,38 @@ def traffic_for(path, k, m, cell, stripes, mode):
         if (c["k"], c["m"], c["cell"], c["stripes"], c.get("decode_mode", "uniform")) == (k, m, cell, stripes, mode):
             return c["hbm_bytes_per_launch"], f"{os.path.relpath(path, ROOT)}:{c['config']} ({tr.get('tag')})"
     return None, None
+
+
+def rank_identity(rank, local, device, shared=False):
+    """(rank, device ordinal, PCI location, UUID) of this rank's GPU, so an
+    N-rank line shows that the ranks ran on N distinct cards (SURVEY §8e);
+    device None = no GPU (dry run)."""
+    ident = {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "device": device,
+             "host": socket.gethostname(), "pci_domain_id": None, "pci_bus_id": None, "pci_device_id": None,
+             "uuid": None, "shared_gpu": bool(shared)}
+    if device is not None:
+        import torch
+        p = torch.cuda.get_device_properties(device)
+        ident.update({"pci_domain_id": getattr(p, "pci_domain_id", None), "pci_bus_id": getattr(p, "pci_bus_id", None),
+                      "pci_device_id": getattr(p, "pci_device_id", None), "uuid": str(getattr(p, "uuid", "")) or None,
+                      "name": p.name})
+    return ident
+
+
+def gather_ranks(ident, world, dist):
+    """Every rank's identity, in rank order (all_gather_object over the
+    process group; the barrier / max-reduction group, no data)."""
+    if world == 1 or not dist.is_initialized():
+        return [ident]
+    out = [None] * world
+    dist.all_gather_object(out, ident)
+    return sorted(out, key=lambda r: r["rank"])
+
+
+def process_group_info(args, world, dist):
+    init = dist.is_available() and dist.is_initialized()
+    return {"backend": dist.get_backend() if init else None, "requested_backend": args.backend,
+            "world_size": dist.get_world_size() if init else 1, "env_world_size": world}
 
 
 def dry_run(args, world, rank):
@@ -293,6 +334,7 @@ def dry_run(args, world, rank):
         dist.barrier()
     el = max_over_ranks(time.perf_counter() - t0)
     total = sum_over_ranks(float(S))
+    ranks = gather_ranks(rank_identity(rank, int(os.environ.get("LOCAL_RANK", "0")), None), world, dist)
     extra = {}
     for cfg in EXTRA_CONFIGS:  # the same per-rank split extra_configs() runs
         _, share = shard_range(cfg["global_stripes"], world, rank)
@@ -304,7 +346,8 @@ def dry_run(args, world, rank):
                           "config": {"k": args.k, "m": args.m, "cell_bytes": args.cell, "stripes_per_gpu": S,
                                      "global_stripes": args.global_stripes or S * world,
                                      "stripes_summed_over_ranks": int(total)},
-                          "extra_configs": extra,
+                          "extra_configs": extra, "ranks": ranks,
+                          "process_group": process_group_info(args, world, dist),
                           "max_elapsed_s": el}), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -472,6 +515,144 @@ def per_call_sizes(H, k, m, oracle_lib):
                     "different row of a 1 GiB pool (4x the L3), device forced vs host routine forced"}
 
 
+ROWS_CALL_SHAPES = (1, 4)  # rows per call: the reference's per-row calls, the row-batched writer / reader's 4
+
+
+def _rows_pools(k, cell, rows, pool_bytes):
+    """Calls' worth of slots (one call's buffers each) so that the data of a
+    pass over them spans >= pool_bytes: every call's buffers are cold."""
+    return max(3, pool_bytes // (rows * k * cell))
+
+
+def rows_call_host(k, m, cell, seconds=0.4):
+    """Child process (no GPU): the engine's host routine on pageable buffers
+    at the writer's / reader's call shapes, cold, on however many threads
+    HEC_HOST_THREADS gives it.  Prints one JSON object."""
+    import ctypes
+
+    import numpy as np
+
+    import hdfs_native_ec as H
+    out = {}
+    coder = H.Coder(k, m, H.HEC_DEVICE_HOST)
+    for rows in ROWS_CALL_SHAPES:
+        n = rows * cell  # a vertical stripe: each shard's `rows` cells back to back
+        slots = _rows_pools(k, cell, rows, 1 << 30)
+        vert = np.frombuffer(np.random.default_rng(rows).bytes(slots * (k + m) * n), dtype=np.uint8).reshape(
+            slots, k + m, n)
+        rec = np.empty((slots, m, n), dtype=np.uint8)
+        rec[:, :, ::4096] = 0
+        res = {}
+        for op in ("encode", "decode"):
+            calls, t, r = 0, 0.0, 0
+            c0, t0 = time.process_time(), time.perf_counter()
+            while t < seconds or calls < 3:
+                v = vert[r]
+                if op == "encode":
+                    rc = H.lib.hec_encode(coder.handle, (ctypes.c_void_p * k)(*[v[i].ctypes.data for i in range(k)]),
+                                          n, (ctypes.c_void_p * m)(*[v[k + j].ctypes.data for j in range(m)]))
+                else:  # data shards 0..m-1 lost, rebuilt from the rest
+                    sh = (ctypes.c_void_p * (k + m))(*([0] * m + [v[i].ctypes.data for i in range(m, k + m)]))
+                    outs = (ctypes.c_void_p * (k + m))(*([rec[r, i].ctypes.data for i in range(m)] + [0] * k))
+                    rc = H.lib.hec_decode(coder.handle, sh, n, outs)
+                assert rc == 0, rc
+                r = (r + 1) % slots
+                calls += 1
+                t = time.perf_counter() - t0
+            cpu = time.process_time() - c0
+            gib = calls * k * n / GIB
+            res[op] = {"us_per_call": round(t / calls * 1e6, 1), "GiBps": round(gib / t, 2),
+                       "cpu_core_s_per_GiB": round(cpu / gib, 4), "calls": calls}
+        # slot 0 was encoded first: its rebuilt shards == the originals
+        assert np.array_equal(rec[0], vert[0, :m]), f"rows={rows}: host decode != data"
+        out[f"rows={rows}"] = res
+        del vert, rec
+    coder.close()
+    out["threads"] = int(os.environ.get("HEC_HOST_THREADS", "4"))
+    out["isa"] = H.host_isa()
+    print(json.dumps(out), flush=True)
+
+
+def rows_call_leg(H, k, m, cell, coder, torch):
+    """The striped writer's and reader's call shapes, cold (each call on a
+    different slice of a >= 1 GiB pool): `rows` rows per call, 1 (the
+    reference: block_writer.rs:838, ec/mod.rs:71-72) or 4 (the row-batched
+    writer / reader, rust/src/hdfs/ec_rows.rs).  device = the engine's pinned
+    pipeline on page-locked buffers (hec_encode_host_batch: file-order rows
+    in, parity out, one stripe per pipeline chunk; hec_decode_host_batch:
+    vertical shards in, file-order rows out, data shards 0..m-1 lost);
+    host_<T>t = the engine's host routine on pageable buffers (hec_encode /
+    hec_decode of the vertical stripes) on T threads, each in a child process
+    that never touches the GPU (HEC_HOST_THREADS=T).  Wall time per call and
+    CPU core-seconds per GiB of data (process CPU time over the calls: every
+    thread of the process, the HIP runtime's included)."""
+    import numpy as np
+    res = {}
+    dev_res = {}
+    for rows in ROWS_CALL_SHAPES:
+        slots = _rows_pools(k, cell, rows, 1 << 30)
+        d_bytes, p_bytes = rows * k * cell, rows * m * cell
+        hb_data = H.HostBuffer(slots * d_bytes)
+        hb_par = H.HostBuffer(slots * p_bytes)
+        hb_file = H.HostBuffer(slots * d_bytes)
+        data = hb_data.array().reshape(slots, rows, k, cell)
+        par = hb_par.array().reshape(slots, rows, m, cell)
+        filev = hb_file.array().reshape(slots, rows, k, cell)
+        data[:] = np.frombuffer(np.random.default_rng(7 + rows).bytes(slots * d_bytes), dtype=np.uint8).reshape(
+            data.shape)
+        filev[:, :, :, ::4096] = 0
+        par[:, :, :, ::4096] = 0
+        # the reader's vertical shards: [k+m][rows*cell] per slot, pinned
+        hb_vert = H.HostBuffer(slots * (k + m) * rows * cell)
+        vert = hb_vert.array().reshape(slots, k + m, rows * cell)
+        r_res = {}
+        for op in ("encode", "decode"):
+            calls, t, r = 0, 0.0, 0
+            fn = (lambda s: coder.encode_host_batch(data[s].ctypes.data, par[s].ctypes.data, cell, rows, 1)) \
+                if op == "encode" else \
+                (lambda s: coder.decode_host_batch([None] * m + [vert[s, i].ctypes.data for i in range(m, k + m)],
+                                                   cell, rows, filev[s].ctypes.data, 1))
+            if op == "decode":  # vertical shards of the encoded rows (untimed)
+                for s in range(slots):
+                    vert[s, :k] = data[s].transpose(1, 0, 2).reshape(k, rows * cell)
+                    vert[s, k:] = par[s].transpose(1, 0, 2).reshape(m, rows * cell)
+            fn(0)
+            c0, t0 = time.process_time(), time.perf_counter()
+            while t < 0.4 or calls < 3:
+                fn(r)
+                r = (r + 1) % slots
+                calls += 1
+                t = time.perf_counter() - t0
+            cpu = time.process_time() - c0
+            gib = calls * d_bytes / GIB
+            r_res[op] = {"us_per_call": round(t / calls * 1e6, 1), "GiBps": round(gib / t, 2),
+                         "cpu_core_s_per_GiB": round(cpu / gib, 4), "calls": calls}
+        # every slot's rows came back whole (data 0..m-1 rebuilt), and slot
+        # 0's parity matches the host routine's
+        assert np.array_equal(filev, data), f"rows={rows}: decode_host_batch file rows != data"
+        hc = H.Coder(k, m, H.HEC_DEVICE_HOST)
+        want = np.empty((rows, m, cell), dtype=np.uint8)
+        hc.encode_host_batch(data[0].ctypes.data, want.ctypes.data, cell, rows, 1)
+        hc.close()
+        assert np.array_equal(want, par[0]), f"rows={rows}: device parity != host routine parity"
+        dev_res[f"rows={rows}"] = r_res
+        for b in (hb_data, hb_par, hb_file, hb_vert):
+            b.close()
+    res["device_pinned"] = dev_res
+    for threads in (1, int(os.environ.get("HEC_HOST_THREADS", "4") or 4)):
+        env = dict(os.environ, HEC_HOST_THREADS=str(threads), HIP_VISIBLE_DEVICES="", ROCR_VISIBLE_DEVICES="")
+        out = subprocess.run([sys.executable, os.path.abspath(__file__), "--rows-call-host", "--k", str(k),
+                              "--m", str(m), "--cell", str(cell)], capture_output=True, text=True, env=env,
+                             timeout=300)
+        assert out.returncode == 0, out.stderr[-2000:]
+        res[f"host_{threads}t"] = json.loads(out.stdout.strip().splitlines()[-1])
+    res["note"] = (f"RS({k},{m}) {cell} B cells, rows per call 1 (reference) and 4 (row-batched writer / reader), "
+                   "cold pools; device_pinned = hec_encode_host_batch / hec_decode_host_batch on page-locked "
+                   "buffers (data shards 0..m-1 lost), host_<T>t = the host routine on pageable vertical stripes "
+                   "(hec_encode / hec_decode) on T threads; cpu_core_s_per_GiB = process CPU time / data GiB")
+    return res
+
+
 def ref_cases(args):
     """rust/benches/ec.rs:5-64 mirrored: matrix-inversion/invert (RS(6,3)
     rows 3..8), rs-encode/encode (one stripe of 6 x 16 MiB), and
@@ -588,6 +769,8 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     if args.dry_run:
         return dry_run(args, world, rank)
+    if args.rows_call_host:
+        return rows_call_host(args.k, args.m, args.cell)
     if args.ref_cases:
         return ref_cases(args)
 
@@ -600,7 +783,15 @@ def main():
 
     local = int(os.environ.get("LOCAL_RANK", "0"))
     ndev = torch.cuda.device_count()
-    local = local % max(1, ndev)  # rehearsal: several ranks may share one GPU (gloo only)
+    shared = local >= ndev
+    if shared:
+        if args.backend == "nccl" or ndev == 0:
+            # one rank per GPU is the contract: a world larger than the node's
+            # GPU count would fold ranks onto shared cards and over-report
+            log(f"refusing: LOCAL_RANK {local} but {ndev} GPU(s) visible (backend {args.backend}); "
+                "one rank per GPU")
+            sys.exit(3)
+        local %= ndev  # gloo rehearsal only: ranks share cards, flagged in the line
     if world > 1:
         torch.cuda.set_device(local)
         if args.backend == "nccl":
@@ -799,6 +990,8 @@ def main():
         log("host path legs")
         result["host_path"]["per_call_by_size"] = per_call_sizes(H, k, m, clib)
         log("per-call table")
+        result["host_path"]["rows_call"] = rows_call_leg(H, k, m, cell, coder, torch)
+        log("writer / reader call shapes")
 
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         log("cpu baseline")
@@ -808,6 +1001,14 @@ def main():
         if (k, m, cell) == (6, 3, 1 << 20) and args.codec == "rs" and not args.tune:
             log("cpu config RS(3,2) x 1024")
             result["cpu_baseline_configs"] = [cpu_config_batch(H, 3, 2, 1 << 20, 1024, args.cpu_threads)]
+            # the two other BASELINE configs with a device line in extra_configs
+            # (BASELINE.md:47-48): bounded stripe samples, ~2-5 s per 1-thread leg
+            log("cpu config RS(10,4) 1 MiB sample")
+            result["cpu_baseline_configs"].append(cpu_config_batch(
+                H, 10, 4, 1 << 20, 128, args.cpu_threads, config_stripes=2048, source="BASELINE.json configs[3]"))
+            log("cpu config RS(6,3) 64 KiB sample")
+            result["cpu_baseline_configs"].append(cpu_config_batch(
+                H, 6, 3, 1 << 16, 4096, args.cpu_threads, config_stripes=65536, source="BASELINE.json configs[4]"))
     elif rank == 0:
         result["cpu_baseline"] = None
 
@@ -819,6 +1020,10 @@ def main():
         torch.cuda.empty_cache()
         result["extra_configs"] = extra_configs(args, H, dist, world, rank, dev, max_over_ranks, shard_range)
 
+    result["process_group"] = process_group_info(args, world, dist)
+    result["ranks"] = gather_ranks(rank_identity(rank, local, dev.index, shared), world, dist)
+    result["distinct_gpus"] = len({(r["pci_domain_id"], r["pci_bus_id"], r["pci_device_id"], r["uuid"])
+                                   for r in result["ranks"]})
     if rank == 0:
         print(json.dumps(result), flush=True)
     coder.close()

@@ -5,6 +5,9 @@
 #include "host_gf.hpp"
 
 #include <immintrin.h>
+#include <pthread.h>
+#include <sys/types.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <condition_variable>
@@ -12,6 +15,7 @@
 #include <cstring>
 #include <functional>
 #include <mutex>
+#include <new>
 #include <thread>
 
 #include "gf256.hpp"
@@ -269,9 +273,34 @@ size_t split_threads() {
     return n;
 }
 
+// The process-wide pool, owned by the process that created it.  A fork()ed
+// child (Python multiprocessing's default start method) inherits the pool's
+// memory but not its worker threads, and a mutex another parent thread held
+// at fork time stays locked in the child: posting a job there would wait for
+// workers that do not exist.  So the child drops the inherited
+// pool (leaked, never touched) and builds its own on first use; the pid check
+// covers a fork before the handler was registered.
+std::mutex g_pool_mu;
+SplitPool* g_pool = nullptr;  // never destroyed: workers may outlive static destruction order
+pid_t g_pool_pid = 0;
+
+void pool_after_fork_child() {
+    new (&g_pool_mu) std::mutex();  // the child runs only the forking thread
+    g_pool = nullptr;
+    g_pool_pid = 0;
+}
+
 SplitPool* split_pool() {
-    static SplitPool* p = split_threads() > 1 ? new SplitPool(split_threads() - 1) : nullptr;  // never destroyed:
-    return p;  // workers may outlive static destruction order; the OS reaps them at exit
+    if (split_threads() <= 1) return nullptr;
+    static const int registered = pthread_atfork(nullptr, nullptr, pool_after_fork_child);
+    (void)registered;
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    const pid_t me = getpid();
+    if (!g_pool || g_pool_pid != me) {
+        g_pool = new SplitPool(split_threads() - 1);
+        g_pool_pid = me;
+    }
+    return g_pool;
 }
 
 }  // namespace
@@ -281,7 +310,12 @@ size_t split_min_bytes() { return size_t(256) << 10; }
 void gf_matmul_split(Isa isa, const uint8_t* mat, const uint64_t* aff, size_t rows, size_t cols,
                      const uint8_t* const* in, uint8_t* const* out, size_t n) {
     const size_t T = split_threads();
-    SplitPool* pool = n >= split_min_bytes() && T > 1 ? split_pool() : nullptr;
+    // the pieces' pointer arrays below hold up to kMaxSplitShards rows / cols
+    // (the C ABI bounds cols only): larger matrices run unsplit
+    constexpr size_t kMaxSplitShards = 64;
+    SplitPool* pool = n >= split_min_bytes() && T > 1 && rows <= kMaxSplitShards && cols <= kMaxSplitShards
+                          ? split_pool()
+                          : nullptr;
     std::unique_lock<std::mutex> own;
     if (pool) own = std::unique_lock<std::mutex>(pool->own, std::try_to_lock);
     if (!pool || !own.owns_lock()) {
@@ -294,8 +328,8 @@ void gf_matmul_split(Isa isa, const uint8_t* mat, const uint64_t* aff, size_t ro
         const size_t a = p * piece;
         if (a >= n) return;
         const size_t len = std::min(piece, n - a);
-        const uint8_t* pin[64];
-        uint8_t* pout[64];
+        const uint8_t* pin[kMaxSplitShards];
+        uint8_t* pout[kMaxSplitShards];
         for (size_t i = 0; i < cols; i++) pin[i] = in[i] + a;
         for (size_t j = 0; j < rows; j++) pout[j] = out[j] + a;
         gf_matmul(isa, mat, aff, rows, cols, pin, pout, len);

@@ -122,8 +122,8 @@ bool shape_ok(int k, int e, int kind, Shape sh) {
            (sh.scheme == 12 || (sh.scheme == 15 && kind == 0));
 }
 
-std::string entry_key(int k, int e, int kind, Shape sh, const uint8_t* matrix) {
-    std::string key = std::to_string(k) + "/" + std::to_string(e) + "/" + std::to_string(kind) + "/" +
+std::string entry_key(const std::string& arch, int k, int e, int kind, Shape sh, const uint8_t* matrix) {
+    std::string key = arch + "/" + std::to_string(k) + "/" + std::to_string(e) + "/" + std::to_string(kind) + "/" +
                       std::to_string(sh.slabs) + "/" + std::to_string(sh.wpe) + "/" + std::to_string(sh.pfd) + "/" +
                       std::to_string(sh.scheme) + "/";
     key.append(reinterpret_cast<const char*>(matrix), size_t(e) * k);
@@ -155,6 +155,8 @@ std::string make_source(int k, int e, int kind, const uint8_t* matrix) {
     return s;
 }
 
+constexpr uint32_t kCacheMagic = 0x32434548u;  // "HEC2": the checked disk-cache format
+
 uint64_t fnv1a(const std::string& s, uint64_t h = 1469598103934665603ull) {
     for (unsigned char c : s) {
         h ^= c;
@@ -177,10 +179,36 @@ void mkdirs(const std::string& d) {
         if (i == d.size() || d[i] == '/') (void)mkdir(d.substr(0, i).c_str(), 0755);
 }
 
+// The gfx target a device's code object is compiled for (its gcnArchName up
+// to the first ':'), cached per device; without a device (hec_jit_warm on a
+// build host) $HEC_JIT_ARCH, else gfx950.  Part of the entry and disk-cache
+// keys, so a code object is never loaded on a device of another target.
+std::string device_arch(int device) {
+    static std::mutex mu;
+    static std::map<int, std::string> cache;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find(device);
+    if (it != cache.end()) return it->second;
+    std::string arch;
+    hipDeviceProp_t p;
+    if (device >= 0 && hipGetDeviceProperties(&p, device) == hipSuccess) {
+        arch = p.gcnArchName;
+        arch = arch.substr(0, arch.find(':'));
+    } else {
+        (void)hipGetLastError();
+    }
+    if (arch.empty()) {
+        const char* v = std::getenv("HEC_JIT_ARCH");
+        arch = v && *v ? v : "gfx950";
+    }
+    return cache[device] = arch;
+}
+
 enum class State { kQueued, kCompiling, kReady, kFailed };
 
 struct Entry {
     int k = 0, e = 0, kind = 0;
+    std::string arch;  // gfx target (device_arch)
     Shape shape{8, 2, 1};
     std::vector<uint8_t> matrix;
     State state = State::kQueued;
@@ -237,26 +265,32 @@ struct Jit {
         int maj = 0, mnr = 0;
         if (r.ok) r.version(&maj, &mnr);
         const std::string dir = cache_dir();
-        const uint64_t h = fnv1a(name + "\n" + std::to_string(maj) + "." + std::to_string(mnr) + "\n" + src +
-                                 kHeaderDigest);
+        const uint64_t h = fnv1a(name + "\n" + en.arch + "\n" + std::to_string(maj) + "." + std::to_string(mnr) +
+                                 "\n" + src + kHeaderDigest);
         char hex[17];
         std::snprintf(hex, sizeof hex, "%016llx", static_cast<unsigned long long>(h));
         const std::string path = dir.empty() ? "" : dir + "/dv-" + hex + ".co";
         std::vector<char> code;
         std::string lowered;
-        if (!path.empty()) {  // disk cache: [name length u32][lowered name][code object]
+        // disk cache: [magic u32][name length u32][lowered name][code size u64]
+        // [fnv1a of the code u64][code object]; a file that does not check out
+        // (truncated by a full disk, another format) is ignored and rewritten
+        if (!path.empty()) {
             if (FILE* f = std::fopen(path.c_str(), "rb")) {
-                uint32_t n = 0;
-                if (std::fread(&n, 4, 1, f) == 1 && n < 4096) {
+                uint32_t magic = 0, n = 0;
+                uint64_t size = 0, sum = 0;
+                if (std::fread(&magic, 4, 1, f) == 1 && magic == kCacheMagic && std::fread(&n, 4, 1, f) == 1 &&
+                    n < 4096) {
                     lowered.resize(n);
-                    if (std::fread(&lowered[0], 1, n, f) == n) {
-                        char buf[1 << 16];
-                        size_t got;
-                        while ((got = std::fread(buf, 1, sizeof buf, f)) > 0) code.insert(code.end(), buf, buf + got);
+                    if (std::fread(&lowered[0], 1, n, f) == n && std::fread(&size, 8, 1, f) == 1 &&
+                        std::fread(&sum, 8, 1, f) == 1 && size >= 64 && size < (uint64_t(1) << 30)) {
+                        code.resize(size);
+                        if (std::fread(code.data(), 1, size, f) != size || std::fgetc(f) != EOF ||
+                            fnv1a(std::string(code.data(), code.size())) != sum)
+                            code.clear();
                     }
                 }
                 std::fclose(f);
-                if (code.size() < 64) code.clear();
             }
         }
         const bool disk = !code.empty();
@@ -267,7 +301,8 @@ struct Jit {
                 0) {
                 const std::string expr = "&" + name;
                 r.add_name(prog, expr.c_str());
-                const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
+                const std::string arch_opt = "--offload-arch=" + en.arch;
+                const char* opts[] = {arch_opt.c_str(), "-O3", "-std=c++17"};
                 if (r.compile(prog, 3, opts) == 0) {
                     size_t n = 0;
                     const char* low = nullptr;
@@ -291,10 +326,12 @@ struct Jit {
                 mkdirs(dir);
                 const std::string tmp = path + ".tmp" + std::to_string(getpid());
                 if (FILE* f = std::fopen(tmp.c_str(), "wb")) {
-                    const uint32_t n = uint32_t(lowered.size());
-                    const bool ok = std::fwrite(&n, 4, 1, f) == 1 && std::fwrite(lowered.data(), 1, n, f) == n &&
-                                    std::fwrite(code.data(), 1, code.size(), f) == code.size();
-                    std::fclose(f);
+                    const uint32_t magic = kCacheMagic, n = uint32_t(lowered.size());
+                    const uint64_t size = code.size(), sum = fnv1a(std::string(code.data(), code.size()));
+                    bool ok = std::fwrite(&magic, 4, 1, f) == 1 && std::fwrite(&n, 4, 1, f) == 1 &&
+                              std::fwrite(lowered.data(), 1, n, f) == n && std::fwrite(&size, 8, 1, f) == 1 &&
+                              std::fwrite(&sum, 8, 1, f) == 1 && std::fwrite(code.data(), 1, size, f) == size;
+                    ok = std::fclose(f) == 0 && ok;  // a short write surfaces at fclose (full disk)
                     if (!ok || std::rename(tmp.c_str(), path.c_str()) != 0) std::remove(tmp.c_str());
                 }
             }
@@ -326,7 +363,8 @@ bool verify_kernel(int device, int k, int e, int kind, int slabs, int wpe, int p
     if (mode() == Mode::kOff || !shape_ok(k, e, kind, sh)) return false;
     if (!rtc().ok && cache_dir().empty()) return false;
     wait = wait || mode() == Mode::kSync;
-    const std::string key = entry_key(k, e, kind, sh, matrix);
+    const std::string arch = device_arch(device);
+    const std::string key = entry_key(arch, k, e, kind, sh, matrix);
     Jit& J = jit();
     std::shared_ptr<Entry> en;
     {
@@ -337,6 +375,7 @@ bool verify_kernel(int device, int k, int e, int kind, int slabs, int wpe, int p
             en->k = k;
             en->e = e;
             en->kind = kind;
+            en->arch = arch;
             en->shape = sh;
             en->matrix.assign(matrix, matrix + size_t(e) * k);
             J.entries.emplace(key, en);
@@ -395,7 +434,8 @@ bool verify_kernel(int device, int k, int e, int kind, int slabs, int wpe, int p
 bool warm(int k, int e, int kind, int slabs, int wpe, int pfd, const uint8_t* matrix, int scheme) {
     const Shape sh{slabs, wpe, pfd, scheme};
     if (!shape_ok(k, e, kind, sh)) return false;
-    const std::string key = entry_key(k, e, kind, sh, matrix);
+    const std::string arch = device_arch(-1);  // no device: $HEC_JIT_ARCH or gfx950
+    const std::string key = entry_key(arch, k, e, kind, sh, matrix);
     Jit& J = jit();
     std::shared_ptr<Entry> en;
     {
@@ -418,6 +458,7 @@ bool warm(int k, int e, int kind, int slabs, int wpe, int pfd, const uint8_t* ma
             en->k = k;
             en->e = e;
             en->kind = kind;
+            en->arch = arch;
             en->shape = sh;
             en->matrix.assign(matrix, matrix + size_t(e) * k);
             J.entries.emplace(key, en);

@@ -193,6 +193,199 @@ static void replay_batched_reader(hec_coder_t *c, size_t cell, size_t R, int los
     for (int i = 0; i < K + M; i++) free(vert[i]);
 }
 
+/* block_reader.rs StripedBlockStream with the patch's row batching
+ * (rust/patches/ec_mi355x.patch: read_slice / read_row), modelled call for
+ * call over in-memory shard streams: cell_readers[] in shard order,
+ * start_next_reader() opens the next shard at current_block_start (or, for
+ * a shard in fail_open, records a failed reader), read_row() takes the first
+ * k good cells of a row -- a reader whose DataNode dies at row `die_row`
+ * errors there and is dropped -- and advances current_block_start past the
+ * row; read_slice() joins up to ROWS_PER_CALL rows with equal survivors into
+ * vertical stripes (a row with other survivors waits as pending_row) and
+ * decodes them in one hec_decode.  The file read back must equal the
+ * written one.  bug = 1 replays the round-4 patch instead (current_block_start
+ * advanced once per batch): a reader opened mid-batch then starts
+ * at the batch's first row and its cells are rows behind. */
+typedef struct {
+    int open;     /* a live reader */
+    size_t pos;   /* next cell's byte offset in its shard */
+} cell_reader;
+
+typedef struct {
+    const uint8_t *shard[K + M];
+    size_t rows;
+    int fail_open[K + M]; /* start_next_reader records a failed reader */
+    long die_row[K + M];  /* next_cell errors when asked for this row (-1: never) */
+    cell_reader rd[K + M];
+    size_t n_readers, current_block_start, cell;
+    int bug;
+} stripe_stream;
+
+static int start_next_reader(stripe_stream *st) {
+    if (st->n_readers >= K + M) return -1; /* "Not enough valid shards" */
+    const size_t i = st->n_readers++;
+    st->rd[i].open = !st->fail_open[i];
+    st->rd[i].pos = st->current_block_start;
+    return st->rd[i].open;
+}
+
+/* -> 0 and the row's first k good cells (pointers into the shards), or -1 */
+static int read_row(stripe_stream *st, const uint8_t **slice) {
+    size_t good = 0;
+    for (size_t i = 0; i < st->n_readers; i++) good += st->rd[i].open;
+    while (good < K) {
+        int r = start_next_reader(st);
+        if (r < 0) return -1;
+        good += (size_t)r;
+    }
+    for (int i = 0; i < K + M; i++) slice[i] = NULL;
+    size_t cells = 0, b = 0;
+    while (cells < K) {
+        if (b >= st->n_readers) {
+            int r = start_next_reader(st);
+            if (r < 0) return -1;
+            if (!r) {
+                b++;
+                continue;
+            }
+        }
+        cell_reader *rd = &st->rd[b];
+        if (rd->open) {
+            const size_t row = rd->pos / st->cell;
+            if (st->die_row[b] >= 0 && row >= (size_t)st->die_row[b]) {
+                rd->open = 0; /* "trying next replica" */
+            } else {
+                slice[b] = st->shard[b] + rd->pos;
+                rd->pos += st->cell;
+                cells++;
+            }
+        }
+        b++;
+    }
+    if (!st->bug) st->current_block_start += st->cell;
+    return 0;
+}
+
+/* the whole block group through read_slice: 1 = the file read back equals
+ * the written one, 0 = it differs, -1 = the read failed (not enough shards) */
+static int replay_reader_faults(hec_coder_t *c, size_t cell, size_t rows, const int *fail_open,
+                                const long *die_row, int bug) {
+    uint8_t *sh[K + M];
+    for (int i = 0; i < K + M; i++) sh[i] = malloc(rows * cell);
+    for (int i = 0; i < K; i++)
+        for (size_t b = 0; b < rows * cell; b++) sh[i][b] = next_byte();
+    for (size_t r = 0; r < rows; r++) {
+        const uint8_t *in[K];
+        uint8_t *out[M];
+        for (int i = 0; i < K; i++) in[i] = sh[i] + r * cell;
+        for (int j = 0; j < M; j++) out[j] = sh[K + j] + r * cell;
+        orc_encode(K, M, in, cell, out);
+    }
+    stripe_stream st;
+    memset(&st, 0, sizeof st);
+    for (int i = 0; i < K + M; i++) {
+        st.shard[i] = sh[i];
+        st.fail_open[i] = fail_open ? fail_open[i] : 0;
+        st.die_row[i] = die_row ? die_row[i] : -1;
+    }
+    st.rows = rows;
+    st.cell = cell;
+    st.bug = bug;
+    uint8_t *file = malloc(rows * K * cell), *vert[K + M];
+    for (int i = 0; i < K + M; i++) vert[i] = malloc(ROWS_PER_CALL * cell);
+    const uint8_t *pending[K + M];
+    int have_pending = 0;
+    size_t done = 0;
+    int ok = 1, failed = 0;
+    while (done < rows && ok) {
+        const size_t left = rows - (st.current_block_start / cell) + (size_t)have_pending;
+        size_t want = left < 1 ? 1 : left > ROWS_PER_CALL ? ROWS_PER_CALL : left;
+        if (st.bug) want = rows - done < ROWS_PER_CALL ? rows - done : ROWS_PER_CALL;
+        int present[K + M], got = 0;
+        size_t n = 0;
+        while (n < want) {
+            const uint8_t *slice[K + M];
+            if (have_pending) {
+                memcpy(slice, pending, sizeof slice);
+                have_pending = 0;
+            } else if (read_row(&st, slice) != 0) {
+                ok = 0;
+                failed = 1;
+                break;
+            }
+            int same = 1;
+            for (int i = 0; i < K + M; i++) same &= !got || present[i] == (slice[i] != NULL);
+            if (!same) {
+                memcpy(pending, slice, sizeof slice);
+                have_pending = 1;
+                break;
+            }
+            for (int i = 0; i < K + M; i++) {
+                present[i] = slice[i] != NULL;
+                if (slice[i]) memcpy(vert[i] + n * cell, slice[i], cell);
+            }
+            got = 1;
+            n++;
+        }
+        if (!ok || !n) break;
+        if (st.bug) st.current_block_start += n * cell;
+        /* ec_decode of the vertical stripes: rebuild missing data, split into rows */
+        const uint8_t *in[K + M];
+        uint8_t *out[K + M];
+        for (int i = 0; i < K + M; i++) {
+            in[i] = present[i] ? vert[i] : NULL;
+            out[i] = (i < K && !present[i]) ? vert[i] : NULL;
+        }
+        if (hec_decode(c, in, n * cell, out) != HEC_OK) {
+            ok = 0;
+            failed = 1;
+            break;
+        }
+        for (size_t r = 0; r < n; r++)
+            for (int i = 0; i < K; i++) memcpy(file + ((done + r) * K + i) * cell, vert[i] + r * cell, cell);
+        done += n;
+    }
+    for (size_t r = 0; ok && r < rows; r++)
+        for (int i = 0; i < K; i++) ok &= memcmp(file + (r * K + i) * cell, sh[i] + r * cell, cell) == 0;
+    for (int i = 0; i < K + M; i++) {
+        free(sh[i]);
+        free(vert[i]);
+    }
+    free(file);
+    return failed ? -1 : ok;
+}
+
+static void replay_reader_fault_cases(hec_coder_t *c) {
+    const size_t cell = 4096, rows = 9;
+    const long none[K + M] = {-1, -1, -1, -1, -1, -1, -1, -1, -1};
+    long die[K + M];
+    int fopen_[K + M] = {0};
+    CHECK(replay_reader_faults(c, cell, rows, NULL, none, 0) == 1, "batched reader, no faults");
+    /* shard 1's DataNode dies at row 2 (inside the first 4-row batch):
+     * rows 0-1 from shards 0..5, rows 2.. from 0,2..6 (parity 0 opened at
+     * row 2) -- the ADVICE r04 case */
+    memcpy(die, none, sizeof die);
+    die[1] = 2;
+    CHECK(replay_reader_faults(c, cell, rows, NULL, die, 0) == 1, "shard 1 dies at row 2 of a batch");
+    CHECK(replay_reader_faults(c, cell, rows, NULL, die, 1) == 0, "the round-4 patch misreads this case");
+    /* two deaths in different batches, and one at the batch boundary */
+    die[1] = 2;
+    die[4] = 5;
+    CHECK(replay_reader_faults(c, cell, rows, NULL, die, 0) == 1, "shards 1 and 4 die at rows 2 and 5");
+    memcpy(die, none, sizeof die);
+    die[0] = 4;
+    CHECK(replay_reader_faults(c, cell, rows, NULL, die, 0) == 1, "shard 0 dies at row 4 (a batch boundary)");
+    /* fault-injected open failures (EC_FAULT_INJECTOR fail_blocks) plus a death */
+    fopen_[2] = 1;
+    memcpy(die, none, sizeof die);
+    die[3] = 1;
+    CHECK(replay_reader_faults(c, cell, rows, fopen_, die, 0) == 1, "shard 2 never opens, shard 3 dies at row 1");
+    /* m + 1 lost: Not enough valid shards, never a wrong file */
+    die[4] = 6;
+    die[5] = 7;
+    CHECK(replay_reader_faults(c, cell, rows, fopen_, die, 0) == -1, "m + 1 lost shards: Not enough valid shards");
+}
+
 /* What needs no GPU: Coder::new's host-only fallback, decode over the first
  * k present shards only, and the batched writer / reader sequences on it. */
 static void host_only_replay(void) {
@@ -224,6 +417,7 @@ static void host_only_replay(void) {
     for (size_t t = 0; t < sizeof lens / sizeof lens[0]; t++) replay_batched_writer(h, cell, lens[t]);
     replay_batched_reader(h, cell, ROWS_PER_CALL, 0, 4);
     replay_batched_reader(h, cell, 3, 1, 2);
+    replay_reader_fault_cases(h);
     hec_coder_release(h);
     (void)hec_coder_pool_trim();
     printf("host-only replay %s\n", failures ? "FAILED" : "ok");

@@ -342,6 +342,14 @@ def test_jit_warm_compiles_and_caches(tmp_path):
     assert second.returncode == 0, second.stderr[-3000:]
     s2 = json.loads(second.stdout.strip().splitlines()[-1])
     assert s2["from_disk"] == 2 and s2["compiled"] == 0, s2
+    # a truncated cache file (a write cut short by a full disk) fails its size
+    # and checksum check and is recompiled, never loaded
+    victim = sorted(tmp_path.glob("dv-*.co"))[0]
+    victim.write_bytes(victim.read_bytes()[:-100])
+    third = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert third.returncode == 0, third.stderr[-3000:]
+    s3 = json.loads(third.stdout.strip().splitlines()[-1])
+    assert s3["from_disk"] == 1 and s3["compiled"] == 1 and s3["failed"] == 0, s3
     with pytest.raises(ValueError):
         H.jit_warm(5, 3, [0])  # k = 5: no fused decode + verify kernel
     with pytest.raises(ValueError):

@@ -136,3 +136,26 @@ def test_bench_gpus_flag_spawns_ranks(args, want_S, want_global, scaling):
     assert ex["rs63_64KiB_x65536"]["stripes_per_gpu_rank0"] == 32768
     assert ex["rs63_64KiB_x65536"]["stripes_summed_over_ranks"] == 65536
     assert all(v["scaling"] == "strong" and v["value_GiBps"] is None for v in ex.values())
+    # every rank reports its identity (device ordinal / PCI location / UUID on
+    # a GPU run; None here), gathered over the process group in rank order
+    assert d["process_group"]["world_size"] == 2 and d["process_group"]["backend"] == "gloo"
+    assert [r["rank"] for r in d["ranks"]] == [0, 1]
+    assert [r["local_rank"] for r in d["ranks"]] == [0, 1]
+    assert all(set(r) >= {"device", "pci_bus_id", "pci_domain_id", "uuid", "host", "shared_gpu"} for r in d["ranks"])
+
+
+def test_bench_refuses_more_nccl_ranks_than_gpus():
+    """One rank per GPU: an nccl world whose LOCAL_RANK has no GPU of its own
+    (here: no GPU at all) exits non-zero before anything is timed, instead of
+    folding ranks onto shared cards."""
+    import subprocess
+    from conftest import ROOT
+    if torch.cuda.device_count() >= 2:
+        pytest.skip("needs fewer GPUs than ranks")
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "nccl",
+                          "--steps", "1", "--warmup", "0", "--cpu-seconds", "0", "--host-path", "0"],
+                         capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert out.returncode != 0
+    assert "refusing" in out.stderr and "one rank per GPU" in out.stderr
+    assert not [ln for ln in out.stdout.splitlines() if ln.startswith("{")]

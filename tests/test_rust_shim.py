@@ -50,6 +50,18 @@ def test_forwarding_patch_applies_to_reference(tmp_path):
     rd = (hd / "block_reader.rs").read_text()
     assert rd.count("async fn read_slice") == 2 and "async fn read_row" in rd
     assert "super::ec_rows::ROWS_PER_CALL" in rd and "pending_row: None" in rd
+    # ONE copy of the reference's row loop and of its skip / trim, shared by
+    # both cfg variants of read_slice ...
+    assert rd.count("trying next replica") == 1
+    assert rd.count("async fn read_row") == 1 and rd.count("fn skip_and_trim") == 1
+    assert rd.count("Skip any bytes at the beginning") == 1
+    assert rd.count("self.read_row().await?") == 2 and rd.count("self.skip_and_trim(decoded)") == 2
+    # ... and current_block_start advances once per row read, inside
+    # read_row, so a reader opened for a later row of a batch starts at that
+    # row (replayed by tests/cpp/shim_replay.c)
+    row_fn = rd[rd.index("async fn read_row"):rd.index("fn skip_and_trim")]
+    assert "self.current_block_start += self.ec_schema.cell_size;" in row_fn
+    assert rd.count("self.current_block_start +=") == 1
     # the module the writer hunk imports exists and uses only the
     # reference's own Coder / EcSchema API
     rows = open(os.path.join(ROOT, "rust", "src", "hdfs", "ec_rows.rs")).read()
