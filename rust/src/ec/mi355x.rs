@@ -24,11 +24,11 @@
 //! pool (`hec_coder_acquire`) and gives it back on drop.  `Coder::new` stays
 //! infallible: without a GPU the pool hands out an engine host-only coder,
 //! and if even that fails the patched `Coder` keeps `None` and runs the
-//! reference CPU path.  The row-batched writer / reader of the same patch
-//! (`rust/src/hdfs/ec_rows.rs`, `block_reader.rs` `read_slice`) pass
-//! `ROWS_PER_CALL` rows per `encode` / `decode` as vertical stripes (shard i's
-//! cells back to back): GF(2^8) coding is bytewise, so that is one call of
-//! `ROWS_PER_CALL` times the cell length, bit-identical to the rows one by one.
+//! reference CPU path.  The striped writer and reader keep calling one row
+//! at a time on pageable cells, which the engine codes with its host routine
+//! (DESIGN.md §1 measures the device route at those call shapes: it loses).
+//! `GpuCoder::encode_rows` / `decode_rows` are the pinned-memory batched
+//! forms for callers that hold many rows at once (a reconstruct worker).
 
 use std::ffi::{c_char, c_int, c_void, CStr};
 

@@ -78,9 +78,15 @@ __device__ __forceinline__ void fold24(uint32_t (&w)[32]) {
     }
 }
 
+// cell (stripe s, shard i) at base[i] + s * stride[i]; sums [s][9][chunk]
+struct Cells {
+    const uint8_t* base[9];
+    uint64_t stride[9];
+};
+
 template <int WAVES, int NST, int TAIL>
-__global__ __launch_bounds__(WAVES * 64) void crc_dma(const uint8_t* __restrict__ base, uint32_t ncells,
-                                                      uint32_t* __restrict__ out) {
+__global__ __launch_bounds__(WAVES * 64) void crc_dma(Cells cs, uint32_t ncells, uint32_t* __restrict__ out,
+                                                      uint32_t inter) {
     using TW = TabW<TAIL>;
     constexpr int STAGE = 8192;
     // one LDS object: stages then tables
@@ -111,8 +117,18 @@ __global__ __launch_bounds__(WAVES * 64) void crc_dma(const uint8_t* __restrict_
         const uint32_t q = 8u * t + uint32_t(lane) / 8u;
         loff[t] = 1024u * t + 128u * (uint32_t(lane) / 8u) + 16u * ((uint32_t(lane) & 7u) ^ ((q >> 1) & 7u));
     }
+    // task order: `inter` cells interleaved -- consecutive tasks take group g
+    // of cells c0 .. c0+inter-1, then group g+1 (inter = 1: cell-major)
+    auto cell_of = [&](uint32_t tk, uint32_t& cell, uint32_t& g) {
+        const uint32_t span = inter * kGroups, blk = tk / span, r = tk - blk * span;
+        cell = blk * inter + r % inter;
+        g = r / inter;
+    };
     auto issue = [&](uint32_t tk, int s) {
-        const uint8_t* src = base + uint64_t(tk) * 8192u;
+        uint32_t cell, g;
+        cell_of(tk, cell, g);
+        const uint32_t stripe = cell / 9u, shard = cell % 9u;
+        const uint8_t* src = cs.base[shard] + uint64_t(stripe) * cs.stride[shard] + uint64_t(g) * 8192u;
 #pragma unroll
         for (int t = 0; t < 8; t++)
             __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + loff[t]),
@@ -163,7 +179,8 @@ __global__ __launch_bounds__(WAVES * 64) void crc_dma(const uint8_t* __restrict_
         }
         r ^= __shfl_xor(r, 1);
         r ^= __shfl_xor(r, 2);
-        const uint32_t cell = task / kGroups, g = task % kGroups;
+        uint32_t cell, g;
+        cell_of(task, cell, g);
         if (qi == 0) out[uint64_t(cell) * kNck + g * 16 + c] = __builtin_bswap32(r ^ kfinal);
         s = s == NST - 1 ? 0 : s + 1;
     }
@@ -171,16 +188,17 @@ __global__ __launch_bounds__(WAVES * 64) void crc_dma(const uint8_t* __restrict_
 
 struct Variant {
     std::string name;
-    const void* fn;
+    const void* fn;  // null: the product (hec_crc32c_device)
     int waves, per_cu;
     bool check;
+    uint32_t inter;
 };
 
 template <int W, int N, int T>
-Variant make(int per_cu) {
+Variant make(int per_cu, uint32_t inter) {
     return {"dma w" + std::to_string(W) + " st" + std::to_string(N) + (T == 2 ? " w11" : T == 1 ? " s8" : " mem") +
-                " x" + std::to_string(per_cu) + "/CU",
-            reinterpret_cast<const void*>(&crc_dma<W, N, T>), W, per_cu, T != 0};
+                " x" + std::to_string(per_cu) + "/CU inter " + std::to_string(inter),
+            reinterpret_cast<const void*>(&crc_dma<W, N, T>), W, per_cu, T != 0, inter};
 }
 
 static uint32_t host_crc32c(const uint8_t* p, size_t n) {
@@ -199,127 +217,147 @@ static uint32_t host_crc32c(const uint8_t* p, size_t n) {
     return r ^ 0xFFFFFFFFu;
 }
 
+static void fill(uint8_t* dst, size_t n, uint64_t x) {  // deterministic, 64 MiB at a time
+    std::vector<uint8_t> h(64u << 20);
+    for (size_t off = 0; off < n; off += h.size()) {
+        for (size_t i = 0; i < h.size(); i += 8) {
+            x ^= x << 13, x ^= x >> 7, x ^= x << 17;
+            std::memcpy(&h[i], &x, 8);
+        }
+        CK(hipMemcpy(dst + off, h.data(), std::min(h.size(), n - off), hipMemcpyHostToDevice));
+    }
+}
+
+// PROBE_SETS fresh buffer sets in one process (earlier sets stay allocated,
+// so each gets new memory); per set every variant, rounds alternated.
+// PROBE_LAYOUT: contig = one [S][9][cell] allocation; split = data
+// [S][6][cell] + parity [S][3][cell] (bench.py's layout).
 int main() {
     const uint32_t S = uint32_t(std::atoi(std::getenv("PROBE_STRIPES") ? std::getenv("PROBE_STRIPES") : "1024"));
-    const int rounds = std::atoi(std::getenv("PROBE_ROUNDS") ? std::getenv("PROBE_ROUNDS") : "5");
-    const int reps = std::atoi(std::getenv("PROBE_REPS") ? std::getenv("PROBE_REPS") : "10");
+    const int rounds = std::atoi(std::getenv("PROBE_ROUNDS") ? std::getenv("PROBE_ROUNDS") : "4");
+    const int reps = std::atoi(std::getenv("PROBE_REPS") ? std::getenv("PROBE_REPS") : "8");
+    const int nsets = std::atoi(std::getenv("PROBE_SETS") ? std::getenv("PROBE_SETS") : "3");
+    const std::string layout = std::getenv("PROBE_LAYOUT") ? std::getenv("PROBE_LAYOUT") : "contig";
     const uint32_t ncells = S * 9;
     const size_t bytes = size_t(ncells) * kCell;
     hipDeviceProp_t prop;
     CK(hipGetDeviceProperties(&prop, 0));
     const int cus = prop.multiProcessorCount;
-    uint8_t* d = nullptr;
-    uint32_t *o_ref = nullptr, *o = nullptr;
-    CK(hipMalloc(&d, bytes));
-    CK(hipMalloc(&o_ref, size_t(ncells) * kNck * 4));
-    CK(hipMalloc(&o, size_t(ncells) * kNck * 4));
-    {  // deterministic fill, 64 MiB at a time
-        std::vector<uint8_t> h(64u << 20);
-        uint64_t x = 0x9E3779B97F4A7C15ull;
-        for (size_t off = 0; off < bytes; off += h.size()) {
-            for (size_t i = 0; i < h.size(); i += 8) {
-                x ^= x << 13, x ^= x >> 7, x ^= x << 17;
-                std::memcpy(&h[i], &x, 8);
-            }
-            CK(hipMemcpy(d + off, h.data(), std::min(h.size(), bytes - off), hipMemcpyHostToDevice));
-        }
-    }
     hec_coder_t* coder = nullptr;
     if (hec_coder_create(6, 3, 0, &coder) != 0) {
         std::fprintf(stderr, "coder: %s\n", hec_last_error());
         return 1;
     }
-    std::vector<const uint8_t*> bases(9);
-    std::vector<size_t> strides(9, size_t(9) * kCell);
-    for (int i = 0; i < 9; i++) bases[i] = d + size_t(i) * kCell;
-    auto run_ref = [&](uint32_t* dst) {
-        const int rc = hec_crc32c_device(coder, bases.data(), strides.data(), 9, kCell, S, 512,
-                                         reinterpret_cast<uint8_t*>(dst), nullptr);
-        if (rc != 0) {
-            std::fprintf(stderr, "hec_crc32c_device %d %s\n", rc, hec_last_error());
-            std::exit(1);
-        }
-    };
-    run_ref(o_ref);
-    CK(hipDeviceSynchronize());
-    {  // the product against a host CRC on sampled chunks
-        std::vector<uint32_t> got(kNck);
-        std::vector<uint8_t> cellh(kCell);
-        for (uint32_t cidx : {0u, 1u, 7u, ncells / 2, ncells - 1}) {
-            CK(hipMemcpy(cellh.data(), d + size_t(cidx) * kCell, kCell, hipMemcpyDeviceToHost));
-            CK(hipMemcpy(got.data(), o_ref + size_t(cidx) * kNck, kNck * 4, hipMemcpyDeviceToHost));
-            for (uint32_t ch = 0; ch < kNck; ch += 37) {
-                const uint32_t want = __builtin_bswap32(host_crc32c(cellh.data() + ch * 512, 512));
-                if (got[ch] != want) {
-                    std::fprintf(stderr, "product mismatch cell %u chunk %u\n", cidx, ch);
-                    return 1;
-                }
-            }
-        }
-    }
+    uint32_t *o_ref = nullptr, *o = nullptr;
+    CK(hipMalloc(&o_ref, size_t(ncells) * kNck * 4));
+    CK(hipMalloc(&o, size_t(ncells) * kNck * 4));
     std::vector<Variant> vs = {
-        {"product hec_crc32c_device", nullptr, 0, 0, true},
-        make<4, 2, 1>(2), make<4, 2, 0>(2), make<8, 2, 1>(1), make<8, 2, 0>(1),
-        make<4, 3, 2>(1), make<4, 3, 1>(1), make<4, 3, 0>(1), make<4, 2, 2>(1),
+        {"product hec_crc32c_device", nullptr, 0, 0, true, 1},
+        make<4, 3, 1>(1, 1), make<4, 3, 1>(1, 2), make<4, 3, 1>(1, 4), make<4, 3, 1>(1, 8), make<4, 3, 1>(1, 16),
+        make<4, 4, 1>(1, 1), make<4, 4, 1>(1, 4), make<4, 4, 1>(1, 8), make<4, 4, 1>(1, 16),
+        make<4, 3, 0>(1, 8), make<4, 4, 0>(1, 8), make<4, 3, 2>(1, 8),
     };
-    const char* pick = std::getenv("PROBE_VARIANTS");  // comma list of indices
-    std::vector<int> idx;
-    if (pick) {
-        for (const char* p = pick; *p;) {
-            idx.push_back(std::atoi(p));
-            while (*p && *p != ',') p++;
-            if (*p) p++;
-        }
-    } else {
-        for (int i = 0; i < int(vs.size()); i++) idx.push_back(i);
-    }
-    std::vector<std::vector<float>> ms(vs.size());
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
     const uint32_t tasks = ncells * kGroups;
-    auto launch = [&](const Variant& v) {
-        if (!v.fn) return run_ref(o);
-        uint64_t grid = (tasks + v.waves - 1) / v.waves;
-        grid = std::min<uint64_t>(grid, uint64_t(cus) * v.per_cu);
-        void* args[] = {&d, const_cast<uint32_t*>(&ncells), &o};
-        CK(hipLaunchKernel(v.fn, dim3(uint32_t(grid)), dim3(v.waves * 64), args, 0, nullptr));
-    };
-    for (int i : idx) {  // correctness first
-        CK(hipMemset(o, 0, size_t(ncells) * kNck * 4));
-        launch(vs[i]);
+    for (int set = 0; set < nsets; set++) {
+        uint8_t* d = nullptr;
+        uint8_t* dpar = nullptr;
+        if (layout == "split") {
+            CK(hipMalloc(&d, size_t(S) * 6 * kCell));
+            CK(hipMalloc(&dpar, size_t(S) * 3 * kCell));
+            fill(d, size_t(S) * 6 * kCell, 0x9E3779B97F4A7C15ull + set);
+            fill(dpar, size_t(S) * 3 * kCell, 0x1234567887654321ull + set);
+        } else {
+            CK(hipMalloc(&d, bytes));
+            fill(d, bytes, 0x9E3779B97F4A7C15ull + set);
+        }
+        std::vector<const uint8_t*> bases(9);
+        std::vector<size_t> strides(9, size_t(9) * kCell);
+        Cells cs;
+        for (int i = 0; i < 9; i++) {
+            if (layout == "split") {
+                bases[i] = i < 6 ? d + size_t(i) * kCell : dpar + size_t(i - 6) * kCell;
+                strides[i] = (i < 6 ? 6 : 3) * size_t(kCell);
+            } else {
+                bases[i] = d + size_t(i) * kCell;
+            }
+            cs.base[i] = bases[i];
+            cs.stride[i] = strides[i];
+        }
+        auto run_ref = [&](uint32_t* dst) {
+            const int rc = hec_crc32c_device(coder, bases.data(), strides.data(), 9, kCell, S, 512,
+                                             reinterpret_cast<uint8_t*>(dst), nullptr);
+            if (rc != 0) {
+                std::fprintf(stderr, "hec_crc32c_device %d %s\n", rc, hec_last_error());
+                std::exit(1);
+            }
+        };
+        run_ref(o_ref);
         CK(hipDeviceSynchronize());
-        if (vs[i].check) {
-            std::vector<uint32_t> h1(size_t(ncells) * kNck), h2(size_t(ncells) * kNck);
-            CK(hipMemcpy(h1.data(), o_ref, h1.size() * 4, hipMemcpyDeviceToHost));
-            CK(hipMemcpy(h2.data(), o, h2.size() * 4, hipMemcpyDeviceToHost));
-            if (h1 != h2) {
-                size_t bad = 0;
-                while (h1[bad] == h2[bad]) bad++;
-                std::printf("%s: MISMATCH at sum %zu\n", vs[i].name.c_str(), bad);
-                return 2;
+        {  // the product against a host CRC on sampled chunks
+            std::vector<uint32_t> got(kNck);
+            std::vector<uint8_t> cellh(kCell);
+            for (uint32_t cidx : {0u, 1u, 7u, ncells / 2, ncells - 1}) {
+                CK(hipMemcpy(cellh.data(), bases[cidx % 9] + size_t(cidx / 9) * strides[cidx % 9], kCell,
+                             hipMemcpyDeviceToHost));
+                CK(hipMemcpy(got.data(), o_ref + size_t(cidx) * kNck, kNck * 4, hipMemcpyDeviceToHost));
+                for (uint32_t ch = 0; ch < kNck; ch += 37) {
+                    const uint32_t want = __builtin_bswap32(host_crc32c(cellh.data() + ch * 512, 512));
+                    if (got[ch] != want) {
+                        std::fprintf(stderr, "product mismatch cell %u chunk %u\n", cidx, ch);
+                        return 1;
+                    }
+                }
             }
         }
-    }
-    for (int r = 0; r < rounds; r++)
-        for (int i : idx) {
-            launch(vs[i]);
-            CK(hipEventRecord(a));
-            for (int k = 0; k < reps; k++) launch(vs[i]);
-            CK(hipEventRecord(b));
-            CK(hipEventSynchronize(b));
-            float t = 0;
-            CK(hipEventElapsedTime(&t, a, b));
-            ms[i].push_back(t / reps);
+        auto launch = [&](const Variant& v) {
+            if (!v.fn) return run_ref(o);
+            uint64_t grid = (tasks + v.waves - 1) / v.waves;
+            grid = std::min<uint64_t>(grid, uint64_t(cus) * v.per_cu);
+            uint32_t inter = v.inter;
+            void* args[] = {&cs, const_cast<uint32_t*>(&ncells), &o, &inter};
+            CK(hipLaunchKernel(v.fn, dim3(uint32_t(grid)), dim3(v.waves * 64), args, 0, nullptr));
+        };
+        for (const Variant& v : vs) {  // correctness first
+            CK(hipMemset(o, 0, size_t(ncells) * kNck * 4));
+            launch(v);
+            CK(hipDeviceSynchronize());
+            if (v.check) {
+                std::vector<uint32_t> h1(size_t(ncells) * kNck), h2(size_t(ncells) * kNck);
+                CK(hipMemcpy(h1.data(), o_ref, h1.size() * 4, hipMemcpyDeviceToHost));
+                CK(hipMemcpy(h2.data(), o, h2.size() * 4, hipMemcpyDeviceToHost));
+                if (h1 != h2) {
+                    size_t bad = 0;
+                    while (h1[bad] == h2[bad]) bad++;
+                    std::printf("%s: MISMATCH at sum %zu\n", v.name.c_str(), bad);
+                    return 2;
+                }
+            }
         }
-    const double algo = double(bytes) + double(ncells) * kNck * 4;
-    for (int i : idx) {
-        auto v = ms[i];
-        std::sort(v.begin(), v.end());
-        const double med = v[v.size() / 2];
-        std::printf("%-34s median %.4f ms (min %.4f max %.4f) %.1f GB/s = %.4f of 8 TB/s%s\n", vs[i].name.c_str(),
-                    med, v.front(), v.back(), algo / (med * 1e-3) / 1e9, algo / (med * 1e-3) / 8e12,
-                    vs[i].check ? "" : " [no CRC math]");
+        std::vector<std::vector<float>> ms(vs.size());
+        for (int r = 0; r < rounds; r++)
+            for (size_t i = 0; i < vs.size(); i++) {
+                launch(vs[i]);
+                CK(hipEventRecord(a));
+                for (int k = 0; k < reps; k++) launch(vs[i]);
+                CK(hipEventRecord(b));
+                CK(hipEventSynchronize(b));
+                float t = 0;
+                CK(hipEventElapsedTime(&t, a, b));
+                ms[i].push_back(t / reps);
+            }
+        const double algo = double(bytes) + double(ncells) * kNck * 4;
+        std::printf("set %d (%s, base %p):\n", set, layout.c_str(), static_cast<void*>(d));
+        for (size_t i = 0; i < vs.size(); i++) {
+            auto v = ms[i];
+            std::sort(v.begin(), v.end());
+            const double med = v[v.size() / 2];
+            std::printf("  %-40s median %.4f ms (min %.4f max %.4f) %.4f of 8 TB/s%s\n", vs[i].name.c_str(), med,
+                        v.front(), v.back(), algo / (med * 1e-3) / 8e12, vs[i].check ? "" : " [no CRC math]");
+        }
+        std::fflush(stdout);
     }
     hec_coder_destroy(coder);
     return 0;

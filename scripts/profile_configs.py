@@ -117,11 +117,24 @@ def bench_line(log):
     raise SystemExit(f"no bench line in {log}")
 
 
-def counter(d, name, match=lambda n: KERNEL_RE in n):
-    vals = [float(r["Counter_Value"]) for r in rows(d, "*counter_collection.csv")
-            if match(r.get("Kernel_Name", "")) and r.get("Counter_Name") == name]
+def counter(d, name, match=lambda n: KERNEL_RE in n, last=None):
+    """Counter value per dispatch (rows summed per Dispatch_Id: a dispatch may
+    report several rows), in dispatch order; `last` = keep only the last N
+    dispatches -- the bench's timed region.  The spin-up before it is
+    time-based, so a --pmc pass (slower kernels) runs fewer spin-up
+    dispatches than the trace pass: only the tail lines up across passes."""
+    got = {}
+    for r in rows(d, "*counter_collection.csv"):
+        if match(r.get("Kernel_Name", "")) and r.get("Counter_Name") == name:
+            i = int(r["Dispatch_Id"])
+            got[i] = got.get(i, 0.0) + float(r["Counter_Value"])
+    vals = [got[i] for i in sorted(got)]
     if not vals:
         raise SystemExit(f"no {name} rows under {d}")
+    if last is not None:
+        if len(vals) < last:
+            raise SystemExit(f"{name}: {len(vals)} dispatches under {d}, the timed region has {last}")
+        vals = vals[-last:]
     return vals
 
 
@@ -148,8 +161,8 @@ def profile(out, name):
     avg_all = sum(durs) / len(durs)
     stats = [r for r in rows(os.path.join(d, "trace"), "*kernel_stats.csv") if KERNEL_RE in r["Name"]]
     algo = (k + m) * cell * stripes  # per launch: k cells read + r = m written (uniform decode: e = m)
-    fetch = counter(os.path.join(d, "fetch_size"), "FETCH_SIZE")
-    write = counter(os.path.join(d, "write_size"), "WRITE_SIZE")
+    fetch = counter(os.path.join(d, "fetch_size"), "FETCH_SIZE", last=lps * steps)
+    write = counter(os.path.join(d, "write_size"), "WRITE_SIZE", last=lps * steps)
     fetch_b = 2.0 * 1024 * sum(fetch) / len(fetch)
     write_b = 1024.0 * sum(write) / len(write)
     res = {
@@ -263,10 +276,13 @@ def profile_mixed(out, name):
     avg = sum(timed) / len(timed)
     algo = dm["algorithmic_bytes_per_launch"]
     match = lambda n: MIXED_RE in n  # noqa: E731
-    fetch = counter(os.path.join(d, "fetch_size"), "FETCH_SIZE", match)
-    write = counter(os.path.join(d, "write_size"), "WRITE_SIZE", match)
+    # every dispatch of the timed region (the last `steps` decode launches of
+    # each pass), each dispatch's rows summed
+    fetch = counter(os.path.join(d, "fetch_size"), "FETCH_SIZE", match, last=line["steps"])
+    write = counter(os.path.join(d, "write_size"), "WRITE_SIZE", match, last=line["steps"])
     fetch_b = 2.0 * 1024 * sum(fetch) / len(fetch)
     write_b = 1024.0 * sum(write) / len(write)
+    per = [2.0 * 1024 * f_ + 1024.0 * w_ for f_, w_ in zip(fetch, write)]
     res = {
         "config": name, "args": " ".join(args + COMMON), "k": k, "m": m, "cell": cell, "stripes": stripes,
         "erased_cells": dm["erased_cells"], "kernel": sorted({r["Kernel_Name"] for r in trace}),
@@ -277,7 +293,10 @@ def profile_mixed(out, name):
         "fetch_bytes_per_launch": fetch_b, "write_bytes_per_launch": write_b,
         "hbm_bytes_per_launch": fetch_b + write_b,
         "traffic_over_algorithmic": round((fetch_b + write_b) / algo, 5),
-        "pmc_dispatches": {"fetch": len(fetch), "write": len(write)},
+        "pmc_dispatches": {"fetch": len(fetch), "write": len(write), "timed_region": line["steps"]},
+        # (max - min) / mean of the per-dispatch corrected HBM bytes: every
+        # timed launch decodes the same stripes, so this should be ~0
+        "traffic_per_dispatch_spread": round((max(per) - min(per)) / (sum(per) / len(per)), 6),
         "corrections": "FETCH_SIZE KiB x1024 x2 (gfx950 half-count on 16B/lane streaming reads); WRITE_SIZE KiB x1024",
         "bench_line": line,
     }

@@ -14,11 +14,11 @@
  *                        hec_coder_acquire / hec_coder_release: 10,000
  *                        acquire / encode / release cycles, timed against
  *                        create / destroy and against one device-routed call
- *   the patch's row batching (rust/src/hdfs/ec_rows.rs CellBuffer, and
- *                        block_reader.rs read_slice): ROWS_PER_CALL rows per
- *                        call as vertical stripes, then the short last row
- *                        zero-padded -- byte streams == the oracle's per-row
- *                        encode / decode
+ *   the reference's striped writer and reader (unchanged by the patch:
+ *                        CellBuffer::encode per row, the short last row
+ *                        zero-padded; read_slice per row with failed readers
+ *                        replaced) -- byte streams == the oracle's; and
+ *                        ec_decode's vertical stripes of several rows
  *   Coder::new without a GPU -> hec_coder_acquire(-1) = a host-only coder
  *                        (HEC_DEVICE_HOST); decode reads only the first k
  *                        present shards (a shorter shard past them is fine,
@@ -63,9 +63,11 @@ static uint8_t next_byte(void) {
     return (uint8_t)(rng >> 24);
 }
 
-enum { K = 6, M = 3, ROWS_PER_CALL = 4 };
+/* rows per Coder call in the reference's writer / reader: one (round 4's
+ * patch batched 4; measured and dropped) */
+enum { K = 6, M = 3, ROWS_PER_CALL = 1 };
 
-/* rust/src/hdfs/ec_rows.rs CellBuffer::write + encode over a file of `len`
+/* CellBuffer::write + encode (block_writer.rs:791-851) over a file of `len`
  * bytes: every batch of up to ROWS_PER_CALL rows is one encode of the
  * vertical stripes (whole rows) plus one of the zero-padded short row; the
  * k + m shard streams are compared with the oracle's row-by-row CellBuffer
@@ -104,7 +106,7 @@ static void replay_batched_writer(hec_coder_t *c, size_t cell, size_t len) {
             want_len[K + j] += n0;
         }
     }
-    /* the batched writer */
+    /* the writer, ROWS_PER_CALL rows per encode */
     size_t pos = 0;
     while (pos < len) {
         const size_t take = len - pos < ROWS_PER_CALL * row ? len - pos : ROWS_PER_CALL * row;
@@ -150,7 +152,7 @@ static void replay_batched_writer(hec_coder_t *c, size_t cell, size_t len) {
     }
     for (int i = 0; i < K + M; i++) {
         CHECK(got_len[i] == want_len[i] && memcmp(got[i], want[i], want_len[i]) == 0,
-              "batched writer stream %d (len %zu vs %zu, file %zu)", i, got_len[i], want_len[i], len);
+              "writer stream %d (len %zu vs %zu, file %zu)", i, got_len[i], want_len[i], len);
         free(want[i]);
         free(got[i]);
     }
@@ -159,10 +161,9 @@ static void replay_batched_writer(hec_coder_t *c, size_t cell, size_t len) {
     free(file);
 }
 
-/* block_reader.rs read_slice with row batching: R rows whose survivors are
- * the same are one ec_decode of vertical stripes (every present shard's R
- * cells back to back) -> one hec_decode of R * cell bytes; each rebuilt
- * cell == the original. */
+/* EcSchema::ec_decode of vertical stripes (ec/mod.rs:62-89): R rows whose
+ * survivors are the same, every present shard's R cells back to back -> one
+ * hec_decode of R * cell bytes; each rebuilt cell == the original. */
 static void replay_batched_reader(hec_coder_t *c, size_t cell, size_t R, int lost_a, int lost_b) {
     uint8_t *vert[K + M];
     for (int i = 0; i < K; i++) {
@@ -187,25 +188,24 @@ static void replay_batched_reader(hec_coder_t *c, size_t cell, size_t R, int los
     CHECK(rc == HEC_OK, "batched decode %s", hec_strerror(rc));
     for (int i = 0; i < K; i++)
         if (out[i]) {
-            CHECK(memcmp(out[i], vert[i], R * cell) == 0, "batched reader shard %d", i);
+            CHECK(memcmp(out[i], vert[i], R * cell) == 0, "vertical-stripe decode shard %d", i);
             free(out[i]);
         }
     for (int i = 0; i < K + M; i++) free(vert[i]);
 }
 
-/* block_reader.rs StripedBlockStream with the patch's row batching
- * (rust/patches/ec_mi355x.patch: read_slice / read_row), modelled call for
- * call over in-memory shard streams: cell_readers[] in shard order,
+/* block_reader.rs StripedBlockStream::read_slice (:480-554), modelled call
+ * for call over in-memory shard streams: cell_readers[] in shard order,
  * start_next_reader() opens the next shard at current_block_start (or, for
  * a shard in fail_open, records a failed reader), read_row() takes the first
  * k good cells of a row -- a reader whose DataNode dies at row `die_row`
- * errors there and is dropped -- and advances current_block_start past the
- * row; read_slice() joins up to ROWS_PER_CALL rows with equal survivors into
- * vertical stripes (a row with other survivors waits as pending_row) and
- * decodes them in one hec_decode.  The file read back must equal the
- * written one.  bug = 1 replays the round-4 patch instead (current_block_start
- * advanced once per batch): a reader opened mid-batch then starts
- * at the batch's first row and its cells are rows behind. */
+ * errors there and is dropped ("trying next replica") -- and advances
+ * current_block_start past the row; ROWS_PER_CALL rows with equal survivors
+ * go to one hec_decode (1: the reference's per-row ec_decode).  The file read
+ * back must equal the written one; m + 1 lost shards must end in "Not enough
+ * valid shards".  `bug` = 1 advances current_block_start once per call
+ * instead of per row (round 4's batched patch): with more than
+ * one row per call a reader opened mid-call starts rows behind. */
 typedef struct {
     int open;     /* a live reader */
     size_t pos;   /* next cell's byte offset in its shard */
@@ -360,14 +360,14 @@ static void replay_reader_fault_cases(hec_coder_t *c) {
     const long none[K + M] = {-1, -1, -1, -1, -1, -1, -1, -1, -1};
     long die[K + M];
     int fopen_[K + M] = {0};
-    CHECK(replay_reader_faults(c, cell, rows, NULL, none, 0) == 1, "batched reader, no faults");
-    /* shard 1's DataNode dies at row 2 (inside the first 4-row batch):
-     * rows 0-1 from shards 0..5, rows 2.. from 0,2..6 (parity 0 opened at
-     * row 2) -- the ADVICE r04 case */
+    CHECK(replay_reader_faults(c, cell, rows, NULL, none, 0) == 1, "striped reader, no faults");
+    /* shard 1's DataNode dies at row 2: rows 0-1 from shards 0..5, rows 2..
+     * from 0,2..6 (parity 0 opened at row 2) -- the ADVICE r04 case */
     memcpy(die, none, sizeof die);
     die[1] = 2;
-    CHECK(replay_reader_faults(c, cell, rows, NULL, die, 0) == 1, "shard 1 dies at row 2 of a batch");
-    CHECK(replay_reader_faults(c, cell, rows, NULL, die, 1) == 0, "the round-4 patch misreads this case");
+    CHECK(replay_reader_faults(c, cell, rows, NULL, die, 0) == 1, "shard 1 dies at row 2");
+    if (ROWS_PER_CALL > 1)
+        CHECK(replay_reader_faults(c, cell, rows, NULL, die, 1) == 0, "per-call advance misreads a mid-call death");
     /* two deaths in different batches, and one at the batch boundary */
     die[1] = 2;
     die[4] = 5;
@@ -387,7 +387,7 @@ static void replay_reader_fault_cases(hec_coder_t *c) {
 }
 
 /* What needs no GPU: Coder::new's host-only fallback, decode over the first
- * k present shards only, and the batched writer / reader sequences on it. */
+ * k present shards only, and the writer / reader sequences on it. */
 static void host_only_replay(void) {
     hec_coder_t *h = NULL;
     int rc = hec_coder_acquire("rs", K, M, HEC_DEVICE_HOST, &h);
@@ -410,7 +410,7 @@ static void host_only_replay(void) {
     for (int j = 0; j < M; j++) free(p[j]);
     free(rec);
     free(stub);
-    /* the patch's batched writer / reader on the host-only coder */
+    /* the reference's writer / reader sequences on the host-only coder */
     const size_t cell = 4096;
     const size_t lens[] = {1, 100, cell - 1, cell, K * cell - 4, K * cell, 3 * K * cell + 7, 4 * K * cell,
                            4 * K * cell + 1, 9 * K * cell + 2 * cell + 5};
@@ -607,8 +607,8 @@ int main(void) {
         }
     }
 
-    /* the batched writer / reader through the device (1 MiB cells: the
-     * ROWS_PER_CALL-row calls exceed the host limit) */
+    /* the writer / reader sequences through the device (1 MiB cells, host
+     * limit 256 KiB: every row takes the device route) */
     hec_coder_set_host_limit(c, 256 << 10);
     replay_batched_writer(c, 1 << 20, 4 * K * (1 << 20) + 3 * (1 << 20) + 11);
     replay_batched_reader(c, 1 << 20, ROWS_PER_CALL, 0, 1);
