@@ -100,6 +100,37 @@ struct Fold {
 // FD = folded dwords (24: default, 256-bit tail; 16 / 20: measurement
 // schemes 13 / 14, fewer v_alignbit, a 512- / 384-bit tail of lookups).  Any
 // FD <= 25 is valid: a bit is folded only at degree >= 1024 - 32 FD >= 224 > 209.
+// The quarter's 32 little-endian dwords, folded in place: dwords FD..31 then
+// hold a message with the quarter's remainder.
+template <int FD = Fold::kDwords>
+__device__ __forceinline__ void fold_in_place(uint32_t (&w)[32]) {
+    // target i takes (w[i-q] << s) | (w[i-q-1] >> (32-s)) from folded
+    // sources only (indices < FD); sources are at i-2 or earlier, so every
+    // source is final when a target reads it
+#pragma unroll
+    for (int i = 2; i < 32; i++) {
+        uint32_t acc = w[i], pend = 0;
+        bool has = false;
+#pragma unroll
+        for (int o = 0; o < Fold::kN; o++) {
+            const int hi = i - Fold::q[o], lo = hi - 1;
+            const bool h = hi >= 0 && hi < FD, l = lo >= 0 && lo < FD;
+            if (!h && !l) continue;
+            const uint32_t c = h && l ? __builtin_amdgcn_alignbit(w[hi], w[lo], 32 - Fold::s[o])
+                               : h    ? w[hi] << Fold::s[o]
+                                      : w[lo] >> (32 - Fold::s[o]);
+            if (has) {
+                acc = x3(acc, pend, c);
+                has = false;
+            } else {
+                pend = c;
+                has = true;
+            }
+        }
+        w[i] = has ? acc ^ pend : acc;
+    }
+}
+
 template <bool REFL, int FD = Fold::kDwords>
 __device__ __forceinline__ uint32_t quarter_fold(const uint32_t* t, const uint8_t* row) {
     static_assert(FD % 2 == 0 && FD >= 2 && FD <= 24, "even fold depth, 256-bit tail at least");
@@ -112,36 +143,23 @@ __device__ __forceinline__ uint32_t quarter_fold(const uint32_t* t, const uint8_
             const v4u v = *reinterpret_cast<const v4u*>(row + i * 16);
             w[4 * i] = v.x, w[4 * i + 1] = v.y, w[4 * i + 2] = v.z, w[4 * i + 3] = v.w;
         }
-        // target i takes (w[i-q] << s) | (w[i-q-1] >> (32-s)) from folded
-        // sources only (indices < 24); sources are at i-2 or earlier, so
-        // every source is final when a target reads it
-#pragma unroll
-        for (int i = 2; i < 32; i++) {
-            uint32_t acc = w[i], pend = 0;
-            bool has = false;
-#pragma unroll
-            for (int o = 0; o < Fold::kN; o++) {
-                const int hi = i - Fold::q[o], lo = hi - 1;
-                const bool h = hi >= 0 && hi < FD, l = lo >= 0 && lo < FD;
-                if (!h && !l) continue;
-                const uint32_t c = h && l ? __builtin_amdgcn_alignbit(w[hi], w[lo], 32 - Fold::s[o])
-                                   : h    ? w[hi] << Fold::s[o]
-                                          : w[lo] >> (32 - Fold::s[o]);
-                if (has) {
-                    acc = x3(acc, pend, c);
-                    has = false;
-                } else {
-                    pend = c;
-                    has = true;
-                }
-            }
-            w[i] = has ? acc ^ pend : acc;
-        }
+        fold_in_place<FD>(w);
         uint32_t r = 0;
 #pragma unroll
         for (int i = FD; i < 32; i += 2) r = step8_w11<REFL>(t, r, w[i], w[i + 1]);
         return r;
     }
+}
+
+// The fold of a quarter already in registers, its 32-B tail through the
+// slicing-by-8 tables t[8][256] (8 KiB: the LDS-DMA CRC kernel, whose stages
+// leave no room for the 40-KiB 11-bit tables at 3 stages per wave).  CRC32C.
+__device__ __forceinline__ uint32_t quarter_fold_regs_s8(uint32_t (&w)[32], const uint32_t (*t)[256]) {
+    fold_in_place(w);
+    uint32_t r = 0;
+#pragma unroll
+    for (int i = Fold::kDwords; i < 32; i += 2) r = step8<true>(t, r, w[i], w[i + 1]);
+    return r;
 }
 
 // Scheme 15 (CRC32C; measurement build): the same fold, then the 256-bit
@@ -158,28 +176,7 @@ __device__ __forceinline__ uint32_t quarter_fold32(const uint32_t* t, const uint
         const v4u v = *reinterpret_cast<const v4u*>(row + i * 16);
         w[4 * i] = v.x, w[4 * i + 1] = v.y, w[4 * i + 2] = v.z, w[4 * i + 3] = v.w;
     }
-#pragma unroll
-    for (int i = 2; i < 32; i++) {
-        uint32_t acc = w[i], pend = 0;
-        bool has = false;
-#pragma unroll
-        for (int o = 0; o < Fold::kN; o++) {
-            const int hi = i - Fold::q[o], lo = hi - 1;
-            const bool h = hi >= 0 && hi < Fold::kDwords, l = lo >= 0 && lo < Fold::kDwords;
-            if (!h && !l) continue;
-            const uint32_t c = h && l ? __builtin_amdgcn_alignbit(w[hi], w[lo], 32 - Fold::s[o])
-                               : h    ? w[hi] << Fold::s[o]
-                                      : w[lo] >> (32 - Fold::s[o]);
-            if (has) {
-                acc = x3(acc, pend, c);
-                has = false;
-            } else {
-                pend = c;
-                has = true;
-            }
-        }
-        w[i] = has ? acc ^ pend : acc;
-    }
+    fold_in_place(w);
     // tail byte i (0..31) of dwords 24..31 -> t[31 - i][byte]
     uint32_t v[32];
 #pragma unroll

@@ -186,6 +186,65 @@ __global__ __launch_bounds__(WAVES * 64) void crc_dma(Cells cs, uint32_t ncells,
     }
 }
 
+// The product's register-staged kernel (checksum.hip checksum_chunks512<
+// CRC32C, fold, one task of prefetch>: 256 threads, 2 blocks per CU, a
+// padded 9-KiB image per wave) restated over Cells with the task order
+// interleaved over `inter` cells, as crc_dma.
+__global__ __launch_bounds__(256) void crc_reg(Cells cs, uint32_t ncells, uint32_t* __restrict__ out,
+                                               uint32_t inter) {
+    constexpr int Q = 128, PITCH = Q + 16, STAGE = 64 * PITCH;
+    __shared__ uint32_t s_tab[10240 + 384];
+    __shared__ __attribute__((aligned(16))) uint8_t s_stage[4 * STAGE];
+    {
+        constexpr int off[6] = {0, 2048, 4096, 5120, 7168, 9216}, len[6] = {2048, 2048, 1024, 2048, 2048, 1024};
+#pragma unroll
+        for (int f = 0; f < 6; f++)
+            for (int t = threadIdx.x; t < len[f]; t += 256) s_tab[off[f] + t] = kT.w11[f][t];
+        for (int t = threadIdx.x; t < 384; t += 256) s_tab[10240 + t] = (&kT.shift_nib[0][0][0])[t];
+    }
+    __syncthreads();
+    const uint32_t kfinal = kT.final512;
+    const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x / 64)), lane = threadIdx.x & 63;
+    const int qi = lane & 3, c = lane >> 2;
+    uint8_t* stage = s_stage + wave * STAGE;
+    const uint32_t tasks = ncells * kGroups, step = gridDim.x * 4;
+    auto cell_of = [&](uint32_t tk, uint32_t& cell, uint32_t& g) {
+        const uint32_t span = inter * kGroups, blk = tk / span, r = tk - blk * span;
+        cell = blk * inter + r % inter;
+        g = r / inter;
+    };
+    auto load = [&](uint32_t tk, v4u (&v)[8]) {
+        uint32_t cell, g;
+        cell_of(tk, cell, g);
+        const uint8_t* b = cs.base[cell % 9u] + uint64_t(cell / 9u) * cs.stride[cell % 9u] + uint64_t(g) * 8192u;
+#pragma unroll
+        for (int t = 0; t < 8; t++)
+            v[t] = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(b + t * 1024 + lane * 16));
+    };
+    uint32_t task = blockIdx.x * 4 + wave;
+    v4u v[8];
+    if (task < tasks) load(task, v);
+    for (; task < tasks; task += step) {
+#pragma unroll
+        for (int t = 0; t < 8; t++) {
+            const uint32_t off = uint32_t(t) * 1024u + uint32_t(lane) * 16u;
+            *reinterpret_cast<v4u*>(stage + (off / Q) * PITCH + (off % Q)) = v[t];
+        }
+        if (task + step < tasks) load(task + step, v);
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("" ::: "memory");
+        uint32_t r = cd::quarter_fold<true>(s_tab, stage + lane * PITCH);
+        if (qi < 3) r = cd::apply_shift_nib(reinterpret_cast<const uint32_t(*)[8][16]>(s_tab + 10240)[qi], r);
+        r ^= __shfl_xor(r, 1);
+        r ^= __shfl_xor(r, 2);
+        uint32_t cell, g;
+        cell_of(task, cell, g);
+        if (qi == 0) out[uint64_t(cell) * kNck + g * 16 + c] = __builtin_bswap32(r ^ kfinal);
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("" ::: "memory");
+    }
+}
+
 struct Variant {
     std::string name;
     const void* fn;  // null: the product (hec_crc32c_device)
@@ -251,11 +310,14 @@ int main() {
     uint32_t *o_ref = nullptr, *o = nullptr;
     CK(hipMalloc(&o_ref, size_t(ncells) * kNck * 4));
     CK(hipMalloc(&o, size_t(ncells) * kNck * 4));
+    auto reg = [](uint32_t inter) {
+        return Variant{"reg (product restated) inter " + std::to_string(inter),
+                       reinterpret_cast<const void*>(&crc_reg), 4, 2, true, inter};
+    };
     std::vector<Variant> vs = {
         {"product hec_crc32c_device", nullptr, 0, 0, true, 1},
-        make<4, 3, 1>(1, 1), make<4, 3, 1>(1, 2), make<4, 3, 1>(1, 4), make<4, 3, 1>(1, 8), make<4, 3, 1>(1, 16),
-        make<4, 4, 1>(1, 1), make<4, 4, 1>(1, 4), make<4, 4, 1>(1, 8), make<4, 4, 1>(1, 16),
-        make<4, 3, 0>(1, 8), make<4, 4, 0>(1, 8), make<4, 3, 2>(1, 8),
+        reg(1), reg(2), reg(4), reg(8), reg(16),
+        make<4, 3, 1>(1, 1), make<4, 3, 1>(1, 8), make<4, 4, 1>(1, 8),
     };
     hipEvent_t a, b;
     CK(hipEventCreate(&a));

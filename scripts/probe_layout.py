@@ -9,6 +9,11 @@ alternated so drift hits every set alike (HIP events, median of REPS):
 Kernels: checksum_chunks512 (CRC32C of all k+m cells), gf_matmul_v16
 (encode), the fused encode + CRC32C and the plan-specialised fused decode
 {0,1,2} + verify.  Prints one line per (layout, set).
+PROBE_CRC_AB=1: the measurement build instead, CRC32C of all k+m cells by the
+LDS-DMA kernel (tune key 11 = 13) and by the default register-staged one,
+compute and verify mode, same buffers, rounds alternated (round 5 ran it with
+the DMA kernel as the default and the register one on the key: the figures in
+profiles/r05n are the same kernels).
   python3 scripts/probe_layout.py
 """
 import os
@@ -28,6 +33,7 @@ SETS = int(os.environ.get("PROBE_SETS", "2"))
 ROUNDS = int(os.environ.get("PROBE_ROUNDS", "4"))
 REPS = int(os.environ.get("PROBE_REPS", "6"))
 LAYOUTS = os.environ.get("PROBE_LAYOUTS", "split,stripe,shard").split(",")
+CRC_AB = os.environ.get("PROBE_CRC_AB") == "1"
 BPC, NCH = 512, CELL // 512
 MISS = [0, 1, 2]
 
@@ -73,7 +79,8 @@ def main():
     dev = torch.device("cuda:0")
     stream = torch.cuda.current_stream()
     sp = stream.cuda_stream
-    coder = H.Coder(K, M, 0)
+    lib = H.experimental_lib() if CRC_AB else None
+    coder = H.Coder(K, M, 0, lib=lib)
     print("jit prepared:", coder.prepare_decode(MISS, H.CHECKSUM_CRC32C), flush=True)
     g = torch.Generator(device=dev)
     g.manual_seed(5)
@@ -98,6 +105,21 @@ def main():
 
         enc_crc()
         torch.cuda.synchronize()
+        if CRC_AB:
+            def tuned(fn, v):
+                def run():
+                    H.tune_set(11, v, lib)
+                    fn()
+                    H.tune_set(11, 0, lib)
+                return run
+
+            def ver(st=st, cells=cells, cstr=cstr):
+                coder.checksum_verify_device(H.CHECKSUM_CRC32C, cells, cstr, CELL, S, BPC, st["sums"].data_ptr(),
+                                             st["bad"].data_ptr(), sp)
+
+            kernels[(lay, i)] = {"crc_dma": tuned(crc, 13), "crc_reg": crc, "verify_dma": tuned(ver, 13),
+                                 "verify_reg": ver}
+            continue
         kernels[(lay, i)] = {"crc_only": crc, "encode": enc, "encode_crc": enc_crc, "decode_verify": dec_ver}
     times = {key: {n: [] for n in fns} for key, fns in kernels.items()}
     for _ in range(ROUNDS):
@@ -116,6 +138,8 @@ def main():
     algo = {"crc_only": (K + M) * CELL * S + 4 * NCH * (K + M) * S, "encode": (K + M) * CELL * S,
             "encode_crc": (K + M) * CELL * S + 4 * NCH * (K + M) * S,
             "decode_verify": (K + len(MISS)) * CELL * S + 4 * NCH * K * S}
+    for n in ("crc_dma", "crc_reg", "verify_dma", "verify_reg"):
+        algo[n] = algo["crc_only"]
     for key, per in times.items():
         parts = []
         for name, ts in per.items():

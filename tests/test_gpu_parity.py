@@ -801,8 +801,9 @@ CRC32C_CASES = [(512 * 64, 512, 3), (512 * 70 + 256, 512, 2), (1 << 16, 512, 9),
 @pytest.mark.parametrize("cell,bpc,n", CRC32C_CASES)
 def test_crc32c_device_vs_oracle(dev, cell, bpc, n):
     """The default CRC32C kernel (each 128-B quarter folded by a sparse
-    multiple of the polynomial, 11-bit slicing of the tail) and the generic
-    byte kernel (other chunk sizes, unaligned cells) against the oracle."""
+    multiple of the polynomial, 11-bit slicing of the tail; partial last
+    tasks and short last chunks) and the generic byte kernel (other chunk
+    sizes, unaligned cells) against the oracle."""
     crc32c_body(dev, cell, bpc, n, coder(6, 3))
 
 
@@ -813,6 +814,48 @@ def crc32c_body(dev, cell, bpc, n, cod, knob_pairs=(), xlib=None):
         got = H.crc32c_batch(cod, torch.from_numpy(cells).to(dev), bpc)
         torch.cuda.synchronize()
     assert np.array_equal(got.cpu().numpy(), _oracle_sums(cells, bpc))
+
+
+def test_crc32c_pipelined_full_size_vs_byte_kernel(dev):
+    """The default CRC32C kernel at a size where its prefetch runs steady
+    (9 x 1 MiB x 64 cells, ~36 tasks per wave); the same bytes one byte off
+    the 16-B grid go through the generic byte kernel: two independent kernels
+    must agree (size-independent), and stripe 0 against the oracle."""
+    S, n, cell = 64, 9, 1 << 20
+    c = coder(6, 3)
+    g = torch.Generator(device=dev).manual_seed(11)
+    x = torch.empty((S, n, cell), dtype=torch.uint8, device=dev)
+    x.random_(0, 256, generator=g)
+    got = H.crc32c_batch(c, x, 512)
+    buf = torch.empty(S * n * cell + 16, dtype=torch.uint8, device=dev)
+    buf[1:1 + S * n * cell].copy_(x.flatten())
+    ref = torch.empty_like(got)
+    c.crc32c_device([buf.data_ptr() + 1 + i * cell for i in range(n)], [n * cell] * n, cell, S, 512, ref.data_ptr(),
+                    torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)
+    assert np.array_equal(got[:1].cpu().numpy(), _oracle_sums(x[:1].cpu().numpy(), 512))
+
+
+def test_crc32c_verify_pipelined_full_size(dev):
+    """Verify mode of the default CRC32C kernel at full size: exactly the
+    corrupted cells are flagged -- first byte, last byte, a middle byte, two
+    in one stripe."""
+    S, n, cell = 64, 9, 1 << 20
+    c = coder(6, 3)
+    g = torch.Generator(device=dev).manual_seed(12)
+    x = torch.empty((S, n, cell), dtype=torch.uint8, device=dev)
+    x.random_(0, 256, generator=g)
+    sums = H.crc32c_batch(c, x, 512)
+    hits = {(0, 0): 0, (5, 8): cell - 1, (31, 4): cell // 2 + 3, (63, 2): 8191, (63, 6): 8192}
+    for (s_, i), b in hits.items():
+        x[s_, i, b] ^= 0x41
+    bad = H.checksum_verify_batch(c, x, sums, H.CHECKSUM_CRC32C, 512)
+    torch.cuda.synchronize()
+    want = torch.zeros((S, n), dtype=torch.uint8)
+    for s_, i in hits:
+        want[s_, i] = 1
+    assert torch.equal(bad.cpu(), want)
 
 
 def test_crc32c_device_published_vector(dev):
