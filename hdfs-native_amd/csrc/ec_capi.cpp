@@ -788,10 +788,11 @@ size_t plan_bytes(size_t k, size_t m) {
     return sizeof(hec::DevPlanHeader) + std::min(k, m) * k * sizeof(hec::PermTable);
 }
 
-// [per-stripe plan offset: u32 x stripes][plan blob] (hec::MixedArgs)
+// [per-stripe plan offset: u32 x stripes][plan blob][launch tile counters]
+// (hec::MixedArgs)
 size_t mixed_workspace(size_t k, size_t m, size_t stripes) {
     const size_t p = max_plans(k, m, stripes);
-    return align_up(stripes * sizeof(uint32_t)) + p * plan_bytes(k, m);
+    return align_up(align_up(stripes * sizeof(uint32_t)) + p * plan_bytes(k, m)) + hec::kMixedQueueBytes;
 }
 
 
@@ -891,7 +892,8 @@ int mixed_decode_impl(hec_coder* c, const uint8_t* const* d_shards, const size_t
             plan_off[pi] = uint32_t(blob_bytes);
             blob_bytes += sizeof(hec::DevPlanHeader) + plans[pi]->missing.size() * k * sizeof(hec::PermTable);
         }
-        const size_t need = blob_pos + blob_bytes;
+        const size_t queue_pos = align_up(blob_pos + blob_bytes);
+        const size_t need = queue_pos + hec::kMixedQueueBytes;
         if (!d_workspace || workspace_bytes < need || blob_bytes > 0xFFFFFFF0ull) return HEC_ERR_INVALID_ARG;
         {
             // one of the coder's two pinned images, free once its last copy has run
@@ -923,6 +925,7 @@ int mixed_decode_impl(hec_coder* c, const uint8_t* const* d_shards, const size_t
                 std::memcpy(host + blob_pos + plan_off[pi] + sizeof(hec::DevPlanHeader), p.perm.data(),
                             p.perm.size() * sizeof(uint32_t));
             }
+            std::memset(host + blob_pos + blob_bytes, 0, need - (blob_pos + blob_bytes));  // pad + zeroed counters
             HEC_HIP(hipMemcpyAsync(d_workspace, host, need, hipMemcpyHostToDevice, stream), HEC_ERR_DEVICE);
             HEC_HIP(hipEventRecord(c->ev_mixed[b], stream), HEC_ERR_DEVICE);
         }
@@ -947,6 +950,8 @@ int mixed_decode_impl(hec_coder* c, const uint8_t* const* d_shards, const size_t
         a.stripes = stripes;
         for (size_t r0 = 0; r0 < max_e; r0 += hec::kMaxR) {
             a.row0 = int32_t(r0);
+            a.queue = reinterpret_cast<uint32_t*>(ws + queue_pos + (r0 / hec::kMaxR) * hec::kMixedQueues *
+                                                                          hec::kMixedQueueStride);
             const int rows = int(std::min(max_e - r0, size_t(hec::kMaxR)));
             const int rc = hec::launch_decode_mixed(a, rows, c->device, stream);
             if (rc != 0) return to_status(rc);

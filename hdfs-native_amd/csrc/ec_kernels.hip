@@ -30,6 +30,8 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <map>
+#include <mutex>
 
 #include "bitslice.hpp"
 #include "ec_kernels.hpp"
@@ -72,8 +74,18 @@ __device__ __forceinline__ void gstore16(gbyte* p, u32x4 v) {
 // of a tile is a contiguous BS-lane slab: a wave's U pieces are BS*16 B
 // apart).  K = compile-time input count (0 = runtime a.k), R = outputs (1..4).
 // ---------------------------------------------------------------------------
-template <int K, int R, int U, bool NT, int BS>
+// WQ > 0 (compile-time K; the default since round 5): the
+// tiles are wave-tiles (64 lanes x U chunks) dealt round-robin to
+// kMixedQueues launch counters (a.queue; block b takes from counter b %
+// kMixedQueues, i.e. one per XCD), WQ rounds per atomic, the next batch
+// fetched while the current one is coded.  Fast CUs take more tiles than slow
+// ones, and the waves still walk the tile order together.  The counters are
+// zero at rest: every wave makes exactly one fetch past the end, so a
+// counter's last value is known (its in-range batches + its waves) and the
+// wave that draws it resets the counter for the stream's next launch.
+template <int K, int R, int U, bool NT, int BS, int WQ = 0>
 __global__ __launch_bounds__(BS) void gf_matmul_v16(MatmulArgs a) {
+    static_assert(WQ == 0 || K > 0, "the work queue needs compile-time k");
     __shared__ PermTable s_tab[R][kMaxK];
     __shared__ uint8_t s_exp[512];
     __shared__ uint8_t s_log[256];
@@ -83,7 +95,9 @@ __global__ __launch_bounds__(BS) void gf_matmul_v16(MatmulArgs a) {
 
     const uint32_t chunks = a.chunks;  // 16-B chunks per cell
     const uint32_t total = a.total_tiles;
-    constexpr uint32_t TILE = BS * U;
+    constexpr uint32_t TILE = WQ ? 64 * U : BS * U;  // chunks per tile (WQ: a wave-tile)
+    constexpr uint32_t USTEP = WQ ? 64 : BS;          // chunks between a lane's U runs
+    const uint32_t lcol = WQ ? (threadIdx.x & 63u) : threadIdx.x;
 
     // Previous tile's store data (compile-time K).  Held live until the next
     // tile's loads are issued, and every accumulator is materialised before
@@ -97,7 +111,47 @@ __global__ __launch_bounds__(BS) void gf_matmul_v16(MatmulArgs a) {
     for (int u = 0; u < U; u++)
 #pragma unroll
         for (int j = 0; j < R; j++) acc[u][j] = u32x4{0, 0, 0, 0};
-    for (uint32_t tile = blockIdx.x; tile < total; tile += gridDim.x) {
+    // WQ: this wave's counter, its next batch (lane 0, in flight) and the
+    // rounds left of the current one; tile = round * wq_n + counter
+    // counters in use: one per block up to kMixedQueues (a grid smaller than
+    // that, tune key 7, must still reach every tile)
+    const uint32_t wq_n = gridDim.x < kMixedQueues ? gridDim.x : kMixedQueues;
+    const uint32_t wq_q = blockIdx.x % wq_n;
+    uint32_t* const wq_ctr = WQ ? a.queue + wq_q * (kMixedQueueStride / 4) : nullptr;
+    uint32_t wq_last = 0;  // the counter's last value this launch
+    if constexpr (WQ > 0) {
+        const uint32_t rounds = total > wq_q ? (total - 1 - wq_q) / wq_n + 1 : 0;
+        const uint32_t blocks = (gridDim.x - 1 - wq_q) / wq_n + 1;
+        wq_last = (rounds + WQ - 1) / WQ + blocks * (BS / 64) - 1;
+    }
+    uint32_t wq_next, wq_round = 0, wq_left = 0;
+    // Every fetch is read back, the one past the end included (a batch that
+    // runs out mid-way still reads the fetch issued behind it), so exactly
+    // one wave reads the counter's last value.
+    auto next_tile = [&]() -> uint32_t {
+        for (;;) {
+            if (wq_left == 0) {
+                const uint32_t v = uint32_t(__builtin_amdgcn_readfirstlane(int(wq_next)));
+                wq_round = v * uint32_t(WQ);
+                wq_left = WQ;
+                if (uint64_t(wq_round) * wq_n + wq_q >= total) {
+                    if ((threadIdx.x & 63u) == 0 && v == wq_last)
+                        (void)atomicExch(wq_ctr, 0u);  // every fetch of this counter is done
+                    return total;
+                }
+                if ((threadIdx.x & 63u) == 0) wq_next = atomicAdd(wq_ctr, 1u);
+            } else {
+                wq_round++;
+            }
+            wq_left--;
+            const uint64_t t = uint64_t(wq_round) * wq_n + wq_q;
+            if (t < total) return uint32_t(t);
+            wq_left = 0;  // past the end inside a batch: read the fetch behind it
+        }
+    };
+    if constexpr (WQ > 0)
+        if ((threadIdx.x & 63u) == 0) wq_next = atomicAdd(wq_ctr, 1u);
+    for (uint32_t tile = WQ ? next_tile() : blockIdx.x; tile < total; tile = WQ ? next_tile() : tile + gridDim.x) {
         uint32_t stripe, tcol;
         tile_coords(tile, a, stripe, tcol);
         // Keep the per-coefficient table reads inside the loop (LDS broadcast
@@ -114,7 +168,7 @@ __global__ __launch_bounds__(BS) void gf_matmul_v16(MatmulArgs a) {
             uint32_t offs[U];
 #pragma unroll
             for (int u = 0; u < U; u++) {
-                const uint32_t col = tcol * TILE + u * BS + threadIdx.x;
+                const uint32_t col = tcol * TILE + u * USTEP + lcol;
                 live[u] = col < chunks;
                 offs[u] = (live[u] ? col : 0u) * 16u;
             }
@@ -497,8 +551,20 @@ __global__ __launch_bounds__(BS) void gf_matmul_dma(MatmulArgs a) {
 //  otherwise: blocks walk contiguous runs of whole stripes and restage the
 //    plan into LDS once per stripe.
 // ---------------------------------------------------------------------------
-template <int K, int R, int U, int BS, bool RESIDENT, bool MIXED_SKIP = true>
+//  WQ > 0 (measurement build, tune key 26; RESIDENT only): a work queue of
+//    wave-tiles (64 lanes x U chunks of one stripe) instead of block tiles in
+//    a fixed order.  The tile order is dealt round-robin to kMixedQueues
+//    launch counters (a.queue, zeroed by the workspace upload; block b takes
+//    from counter b % kMixedQueues, i.e. one per XCD), each atomic hands a
+//    wave WQ rounds of its counter's tiles, and a wave fetches its next batch
+//    while it codes the current one.  So the unequal stripes (k reads + e
+//    writes each) even out at wave-tile grain, a grid of one block per CU
+//    stages the plans once per CU, and the waves still walk the tile order
+//    together (the DRAM window stays a few stripes wide).
+// ---------------------------------------------------------------------------
+template <int K, int R, int U, int BS, bool RESIDENT, bool MIXED_SKIP = true, int WQ = 0>
 __global__ __launch_bounds__(BS) void gf_decode_mixed(MixedArgs a) {
+    static_assert(WQ == 0 || RESIDENT, "the work queue needs resident plans");
     static_assert(K > 0, "compile-time k");
     __shared__ PermTable s_tab[RESIDENT ? 1 : R][K];  // non-resident: the current plan's rows
     __shared__ DevPlanHeader s_hdr;
@@ -525,7 +591,9 @@ __global__ __launch_bounds__(BS) void gf_decode_mixed(MixedArgs a) {
     __syncthreads();
     const uint32_t chunks = a.chunks;
     const uint32_t total = a.total_tiles;
-    constexpr uint32_t TILE = BS * U;
+    constexpr uint32_t TILE = WQ ? 64 * U : BS * U;  // chunks per tile (WQ: a wave-tile)
+    constexpr uint32_t USTEP = WQ ? 64 : BS;          // chunks between a lane's U runs
+    const uint32_t lcol = WQ ? (threadIdx.x & 63u) : threadIdx.x;
     MatmulArgs order;  // tile_coords reads tiles_per_stripe / group only
     order.tiles_per_stripe = a.tiles_per_stripe;
     order.group = a.group;
@@ -550,14 +618,14 @@ __global__ __launch_bounds__(BS) void gf_decode_mixed(MixedArgs a) {
     for (int u = 0; u < U; u++)
 #pragma unroll
         for (int j = 0; j < R; j++) acc[u][j] = u32x4{0, 0, 0, 0};
-    for (uint32_t tile = t_begin; tile < t_end; tile += t_step) {
+    auto run_tile = [&](uint32_t tile) {
         uint32_t stripe, tcol;
         tile_coords(tile, order, stripe, tcol);
         const DevPlanHeader* hdr = &s_hdr;
         const PermTable* tabs = &s_tab[0][0];  // row r, input i at tabs[r * K + i]
         if constexpr (RESIDENT) {
             const uint32_t off = __builtin_amdgcn_readfirstlane(reinterpret_cast<const uint32_t*>(s_dyn)[stripe]);
-            if (off == kNoPlan) continue;
+            if (off == kNoPlan) return;
             hdr = reinterpret_cast<const DevPlanHeader*>(s_dyn + off_bytes + off);
             tabs = reinterpret_cast<const PermTable*>(s_dyn + off_bytes + off + sizeof(DevPlanHeader)) + a.row0 * K;
         } else {
@@ -580,7 +648,7 @@ __global__ __launch_bounds__(BS) void gf_decode_mixed(MixedArgs a) {
                 __syncthreads();
                 cur_stripe = stripe;
             }
-            if (cur_none) continue;
+            if (cur_none) return;
         }
         // The tile's metadata in three dependent LDS round trips, whatever K:
         // the header words (e, survivor and missing shard bytes), then every
@@ -614,14 +682,14 @@ __global__ __launch_bounds__(BS) void gf_decode_mixed(MixedArgs a) {
 #pragma unroll
         for (int i = 0; i < K; i++) asm volatile("" : "+v"(v_base[i]), "+v"(v_stride[i]), "+v"(w_e2));
         const int nrows = int(__builtin_amdgcn_readfirstlane(w_e2)) - a.row0;  // rows of this launch in the plan
-        if (nrows <= 0) continue;
+        if (nrows <= 0) return;
         asm volatile("" ::: "memory");
 
         bool live[U];
         uint32_t offs[U];
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            const uint32_t col = tcol * TILE + u * BS + threadIdx.x;
+            const uint32_t col = tcol * TILE + u * USTEP + lcol;
             live[u] = col < chunks;
             offs[u] = (live[u] ? col : 0u) * 16u;
         }
@@ -674,7 +742,7 @@ __global__ __launch_bounds__(BS) void gf_decode_mixed(MixedArgs a) {
         for (int u = 0; u < U; u++)
 #pragma unroll
             for (int j = 0; j < R; j++) asm volatile("" : "+v"(acc[u][j]));
-        const bool full = (tcol + 1) * TILE <= chunks;  // block-uniform
+        const bool full = (tcol + 1) * TILE <= chunks;  // block-uniform (WQ: wave-uniform)
 #pragma unroll
         for (int j = 0; j < R; j++) {
             if (j >= nrows) break;  // block-uniform
@@ -684,6 +752,27 @@ __global__ __launch_bounds__(BS) void gf_decode_mixed(MixedArgs a) {
                 if (full || live[u]) gstore16(ob + offs[u], acc[u][j]);
         }
         if (a.drain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // as gf_matmul_v16
+    };
+    if constexpr (WQ > 0) {
+        // lane 0 holds the next batch index; the other lanes' copies are
+        // never read (readfirstlane), so the atomic's result needs no merge
+        // and is first waited for at the next batch, behind the tile drains
+        const uint32_t nq = gridDim.x < kMixedQueues ? gridDim.x : kMixedQueues;  // every tile has a block
+        const uint32_t q = blockIdx.x % nq;
+        uint32_t* ctr = a.queue + q * (kMixedQueueStride / 4);
+        uint32_t v_next;
+        if ((threadIdx.x & 63u) == 0) v_next = atomicAdd(ctr, 1u);
+        for (;;) {
+            const uint32_t r0 = uint32_t(__builtin_amdgcn_readfirstlane(int(v_next))) * uint32_t(WQ);
+            if (uint64_t(r0) * nq + q >= total) break;  // 64-bit: no wrap past 2^32 tiles
+            if ((threadIdx.x & 63u) == 0) v_next = atomicAdd(ctr, 1u);
+            for (uint32_t r = r0; r < r0 + uint32_t(WQ); r++) {
+                if (uint64_t(r) * nq + q >= total) break;
+                run_tile(r * nq + q);
+            }
+        }
+    } else {
+        for (uint32_t tile = t_begin; tile < t_end; tile += t_step) run_tile(tile);
     }
 }
 
@@ -900,6 +989,70 @@ const void* pick_dma(int k, int r, int unroll, int bs) {
 #endif
 }
 
+// register kernel with the work queue, default shapes only
+template <int WQ, int R>
+const void* wq_vec_k(int k) {
+    switch (k) {
+        case 2: return reinterpret_cast<const void*>(&gf_matmul_v16<2, R, 4, true, 256, WQ>);
+        case 3: return reinterpret_cast<const void*>(&gf_matmul_v16<3, R, 4, true, 256, WQ>);
+        case 6: return reinterpret_cast<const void*>(&gf_matmul_v16<6, R, 4, true, 256, WQ>);
+        case 10: return reinterpret_cast<const void*>(&gf_matmul_v16<10, R, 2, true, 512, WQ>);
+        default: return nullptr;
+    }
+}
+template <int WQ>
+const void* wq_vec(int k, int r) {
+    switch (r) {
+        case 1: return wq_vec_k<WQ, 1>(k);
+        case 2: return wq_vec_k<WQ, 2>(k);
+        case 3: return wq_vec_k<WQ, 3>(k);
+        default: return wq_vec_k<WQ, 4>(k);
+    }
+}
+const void* pick_wq(int k, int r, int wq) {
+#ifdef HEC_EXPERIMENTAL
+    return wq == 2 ? wq_vec<2>(k, r) : wq_vec<1>(k, r);
+#else
+    // the product compiles the default batch per k (default_wq)
+    if (k == 2 || k == 3) return wq == 2 ? wq_vec<2>(k, r) : nullptr;
+    return wq == 1 ? wq_vec<1>(k, r) : nullptr;
+#endif
+}
+
+// Rounds of wave-tiles per atomic: same process, same buffers, 2 sets x 5
+// alternated rounds of the bench step (encode + decode of data 0..m-1;
+// scripts/probe_matmul_wq.py, profiles/r05t): RS(6,3) x 1024 0.795-0.798 of
+// HBM peak at 1 vs 0.739-0.747 for the fixed order (0.780-0.782 at 2),
+// RS(3,2) x 1024 0.775-0.776 at 2 (0.752-0.753 at 1) vs 0.711-0.713,
+// RS(10,4) x 256 0.740 at 1 vs 0.729-0.732.
+int default_wq(int k) { return k == 2 || k == 3 ? 2 : (k == 6 || k == 10) ? 1 : 0; }
+
+// The work-queue counters of (device, stream): kMixedQueues of them,
+// kMixedQueueStride apart, zero at rest (each launch leaves them zero, see
+// gf_matmul_v16), zeroed on the stream when first made.  Launches on one
+// stream run in order, so they share a set; launches on different streams
+// get different sets.  Never freed (2 KiB per stream that ever launched).
+uint32_t* stream_counters(int device, hipStream_t stream) {
+    static std::mutex mu;
+    static std::map<std::pair<int, uintptr_t>, uint32_t*> sets;
+    std::lock_guard<std::mutex> lk(mu);
+    uint32_t*& c = sets[{device, reinterpret_cast<uintptr_t>(stream)}];
+    if (!c) {
+        const size_t bytes = size_t(kMixedQueues) * kMixedQueueStride;
+        if (hipMalloc(reinterpret_cast<void**>(&c), bytes) != hipSuccess) {
+            (void)hipGetLastError();
+            c = nullptr;
+            return nullptr;
+        }
+        if (hipMemsetAsync(c, 0, bytes, stream) != hipSuccess) {
+            (void)hipGetLastError();
+            (void)hipFree(c);
+            c = nullptr;
+        }
+    }
+    return c;
+}
+
 #ifdef HEC_EXPERIMENTAL
 // Bit-sliced encode for the (K, R) pairs with a generated network (K > 2:
 // RS(2,1)'s network is no shorter than its tables); nullptr otherwise.
@@ -1024,9 +1177,24 @@ int launch_gf_matmul(const MatmulArgs& in, int device, hipStream_t stream) {
         if (!fn && tn.matmul_bsl == 1 && sh.unroll % 2 == 0 && rs_parity_matrix(a))
             fn = sh.dma ? pick_dma_bsl(a.k, a.r, sh.unroll, sh.block) : pick_bsl(a.k, a.r, sh);
 #endif
+        // the register kernel's default shapes take the work queue (tune key
+        // 27, measurement build: 1 / 2 rounds per atomic, 3 = the fixed order)
+        int wq = 0;
+        if (!fn && !sh.dma && sh.nt && sh.unroll == (sh.block == 512 ? 2 : 4) && (sh.block == 512) == (a.k == 10)) {
+            wq = default_wq(a.k);
+            if (kExperimental && tn.matmul_wq) wq = tn.matmul_wq == 3 ? 0 : tn.matmul_wq;
+            const void* f = wq ? pick_wq(a.k, a.r, wq) : nullptr;
+            a.queue = f ? stream_counters(device, stream) : nullptr;
+            if (a.queue) {
+                fn = f;
+                if (!tn.blocks_per_cu) sh.blocks_per_cu = 1;  // resident blocks only: each one drains the queue
+            } else {
+                wq = 0;
+            }
+        }
         if (!fn) fn = sh.dma ? pick_dma(a.k, a.r, sh.unroll, sh.block) : pick_vec(a.k, a.r, sh);
         if (!fn) return -1;
-        const uint64_t tile = uint64_t(sh.block) * sh.unroll * tile_mult;
+        const uint64_t tile = uint64_t(wq ? 64 : sh.block) * sh.unroll * tile_mult;
         const uint64_t tps = (chunks + tile - 1) / tile;
         const uint64_t total = tps * a.stripes;
         if (chunks > 0xFFFFFFFFull || total > 0xFFF00000ull) return -1;  // tile indices (+ a prefetch stride) in 32 bits
@@ -1081,19 +1249,22 @@ int launch_gf_matmul(const MatmulArgs& in, int device, hipStream_t stream) {
 
 namespace {
 
-template <int K, int R, bool RES, bool SKIP>
+template <int K, int R, bool RES, bool SKIP, int WQ = 0>
 const void* mixed_fn() {
     if constexpr (K > 6)
-        return reinterpret_cast<const void*>(&gf_decode_mixed<K, R, 2, 512, RES, SKIP>);
+        return reinterpret_cast<const void*>(&gf_decode_mixed<K, R, 2, 512, RES, SKIP, WQ>);
     else
-        return reinterpret_cast<const void*>(&gf_decode_mixed<K, R, 4, 256, RES, SKIP>);
+        return reinterpret_cast<const void*>(&gf_decode_mixed<K, R, 4, 256, RES, SKIP, WQ>);
 }
 
 // The product library compiles the default row policy only (rows past a
 // stripe's e skipped); the measurement build both (tune key 20).
 template <int K, int R>
-const void* mixed_sel(bool res, bool skip) {
+const void* mixed_sel(bool res, bool skip, int wq) {
+    if (res && skip && wq == 1) return mixed_fn<K, R, true, true, 1>();
+    if (res && skip && wq == 4) return mixed_fn<K, R, true, true, 4>();
 #ifdef HEC_EXPERIMENTAL
+    if (res && skip && wq == 2) return mixed_fn<K, R, true, true, 2>();
     return res ? (skip ? mixed_fn<K, R, true, true>() : mixed_fn<K, R, true, false>())
                : (skip ? mixed_fn<K, R, false, true>() : mixed_fn<K, R, false, false>());
 #else
@@ -1103,12 +1274,12 @@ const void* mixed_sel(bool res, bool skip) {
 }
 
 template <int K>
-const void* mixed_pick_r(int r, bool res, bool skip) {
+const void* mixed_pick_r(int r, bool res, bool skip, int wq) {
     switch (r) {
-        case 1: return mixed_sel<K, 1>(res, skip);
-        case 2: return mixed_sel<K, 2>(res, skip);
-        case 3: return mixed_sel<K, 3>(res, skip);
-        default: return mixed_sel<K, 4>(res, skip);
+        case 1: return mixed_sel<K, 1>(res, skip, wq);
+        case 2: return mixed_sel<K, 2>(res, skip, wq);
+        case 3: return mixed_sel<K, 3>(res, skip, wq);
+        default: return mixed_sel<K, 4>(res, skip, wq);
     }
 }
 
@@ -1136,12 +1307,26 @@ int launch_decode_mixed(const MixedArgs& in, int rows, int device, hipStream_t s
     // with the serial metadata and flat loads, skipping lost 3.5-4 % there).
     // Tune key 20: 1 = compute every row (measurement), 0 / 2 = skip.
     const bool skip = tn.mixed_skip != 1;
+    // Work queue of wave-tiles over kMixedQueues counters (round 5), one
+    // round per atomic for k >= 6, four below (more atomics per byte there).
+    // Same process and buffers, 2 sets x 5 alternated rounds
+    // (scripts/probe_mixed_wq.py, profiles/r05r): RS(10,4) x 256 0.658-0.662
+    // vs 0.639-0.642 for the fixed order, RS(6,3) x 1024 0.744-0.755 vs
+    // 0.683-0.699, RS(3,2) x 1024 (4 per atomic) 0.708-0.712 vs 0.674-0.715.
+    // One counter measured 2-4x slower at one round per atomic (device-scope
+    // atomics on one address top out near 85 M/s) and 16 or 64 per atomic
+    // widened the DRAM window (slower again).  Tune key 26 (measurement
+    // build): 1 / 2 / 4 rounds per atomic, 3 = the fixed order.  Needs the
+    // launch counters (a.queue) and resident plans.
+    int wq = (a.queue && skip) ? (a.k >= 6 ? 1 : 4) : 0;
+    if (kExperimental && tn.mixed_wq) wq = tn.mixed_wq == 3 ? 0 : tn.mixed_wq;
     auto pick = [&](bool resident) -> const void* {
+        const int w = resident ? wq : 0;
         switch (a.k) {
-            case 2: return mixed_pick_r<2>(rows, resident, skip);
-            case 3: return mixed_pick_r<3>(rows, resident, skip);
-            case 6: return mixed_pick_r<6>(rows, resident, skip);
-            case 10: return mixed_pick_r<10>(rows, resident, skip);
+            case 2: return mixed_pick_r<2>(rows, resident, skip, w);
+            case 3: return mixed_pick_r<3>(rows, resident, skip, w);
+            case 6: return mixed_pick_r<6>(rows, resident, skip, w);
+            case 10: return mixed_pick_r<10>(rows, resident, skip, w);
             default: return nullptr;
         }
     };
@@ -1156,12 +1341,13 @@ int launch_decode_mixed(const MixedArgs& in, int rows, int device, hipStream_t s
         res = false;  // the runtime refused the LDS: restage per stripe instead
         fn = pick(false);
     }
+    if (!res) wq = 0;
     const int U = a.k > 6 ? 2 : 4, BS = a.k > 6 ? 512 : 256;
     // K > 6: a grid of 8 per CU (one resident): RS(10,4) mixed decode 3216-3234
     // -> 3524-3621 GiB/s against 2 per CU
     const int bpc = tn.blocks_per_cu ? tn.blocks_per_cu : (a.k > 6 ? 8 : 1);
     const uint64_t chunks = a.cell_len / 16;
-    const uint64_t tile = uint64_t(BS) * U;
+    const uint64_t tile = uint64_t(wq ? 64 : BS) * U;  // WQ: wave-tiles
     const uint64_t tps = (chunks + tile - 1) / tile;
     const uint64_t total = tps * a.stripes;
     if (total > 0xFFFFFFFFull) return -1;
@@ -1171,7 +1357,9 @@ int launch_decode_mixed(const MixedArgs& in, int rows, int device, hipStream_t s
     a.total_tiles = uint32_t(total);
     tile_order(a.stripes, a.tiles_per_stripe, tn.group > 0 ? uint32_t(tn.group) : 4u, a.group, a.grouped_tiles);
     a.drain = tn.drain == 1 ? 0u : 1u;
-    uint64_t grid = uint64_t(num_cus(device)) * bpc;
+    // WQ: one block per CU unless key 3 says otherwise (resident plans are
+    // staged once per block)
+    uint64_t grid = uint64_t(num_cus(device)) * (wq && !tn.blocks_per_cu ? 1 : bpc);
     if (grid > total) grid = total;
     void* args[] = {&a};
     const hipError_t e = hipLaunchKernel(fn, dim3(uint32_t(grid)), dim3(BS), args, res ? uint32_t(dyn) : 0u, stream);

@@ -37,6 +37,7 @@ struct MatmulArgs {
     uint32_t grouped_tiles;       // tiles of the whole G-stripe groups; the remainder stripes go stripe-major
     uint32_t drain;               // register kernel: 1 = wait for the tile's stores before the next tile's loads
     uint32_t col_rot = 0;         // tile order: stripe s starts its columns at (s * col_rot) % tiles (0 = none)
+    uint32_t* queue = nullptr;    // work-queue register kernel: the stream's launch counters (zero at rest)
 };
 
 // One coefficient's v_perm_b32 product tables (see ec_kernels.hip): c*x =
@@ -59,8 +60,12 @@ static_assert(sizeof(DevPlanHeader) == 64, "plan header is 64 B");
 
 constexpr uint32_t kNoPlan = 0xFFFFFFFFu;  // stripe with no missing data shard
 
-// Workspace (device): [per-stripe plan offset: u32 x stripes][plan blob];
+// Workspace (device): [per-stripe plan offset: u32 x stripes][plan blob]
+// [kMixedQueueBytes: zeroed tile counters, kMixedQueues per launch, one per
+// kMixedQueueStride bytes];
 // plan = DevPlanHeader + e x k PermTables (row r, input i at r*k + i).
+constexpr uint32_t kMixedQueues = 8, kMixedQueueStride = 256;
+constexpr size_t kMixedQueueBytes = size_t(16) * kMixedQueues * kMixedQueueStride;  // up to 16 launches (64 rows)
 struct MixedArgs {
     const uint8_t* base[kMaxShards];  // all k+m shard bases
     uint64_t stride[kMaxShards];
@@ -75,6 +80,7 @@ struct MixedArgs {
     uint64_t stripes;
     uint32_t chunks, tiles_per_stripe, total_tiles, group, grouped_tiles;
     uint32_t drain;                   // 1 = wait for a tile's stores before the next tile (tune key 6)
+    uint32_t* queue;                  // this launch's zeroed tile counters (work-queue variant, key 26)
 };
 
 // Mixed-pattern decode of one group of missing rows row0 .. row0+rows-1

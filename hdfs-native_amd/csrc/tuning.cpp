@@ -15,7 +15,7 @@ namespace {
 std::atomic<int> g_cus[64];
 
 #ifdef HEC_EXPERIMENTAL
-constexpr int kKeys = 25;
+constexpr int kKeys = 27;
 std::atomic<int> g_knob[kKeys + 1];  // index = key; zero-initialised (static storage)
 std::atomic<int> g_nt{-1};           // key 2 defaults to -1 (non-temporal on)
 
@@ -52,6 +52,8 @@ Tune tune_snapshot() {
     t.matmul_bsl = load(23);
     t.jit_pfd = load(24);
     t.col_rot = load(25);
+    t.mixed_wq = load(26);
+    t.matmul_wq = load(27);
     return t;
 }
 
@@ -87,6 +89,8 @@ int tune_store(int key, int value) {
         case 23: ok = value == 0 || value == 1; break;
         case 24: ok = value >= 0 && value <= 5; break;
         case 25: ok = value >= 0 && value <= 4096; break;
+        case 26: ok = value >= 0 && value <= 4; break;
+        case 27: ok = value >= 0 && value <= 3; break;
         default: ok = false;
     }
     if (!ok) return HEC_ERR_INVALID_ARG;

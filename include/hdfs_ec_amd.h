@@ -209,7 +209,9 @@ int hec_decode_device(hec_coder_t *coder, const uint8_t *const *d_shards, const 
  * missing.  One plan per distinct pattern (first-k-present survivors, as
  * gf256.rs:84-126) is built on the host, cached in the coder and uploaded to
  * d_workspace (hec_decode_mixed_workspace_size bytes; keep it untouched
- * until the stream reaches the work).  If any stripe lacks data shards and
+ * until the stream reaches the work: the launch also keeps its tile-queue
+ * counters there, so calls in flight on different streams need different
+ * workspaces).  If any stripe lacks data shards and
  * has fewer than k present, HEC_ERR_NOT_ENOUGH_SHARDS is returned and
  * nothing is launched. */
 size_t hec_decode_mixed_workspace_size(const hec_coder_t *coder, size_t stripes);

@@ -1,0 +1,81 @@
+"""Measurement probe (GPU box): the register kernel's fixed tile order (tune
+key 27 = 3; the default before round 5) against its work queue of wave-tiles
+(key 27 = 1 / 2 rounds per atomic over 8 launch counters; the default is 2 for
+k <= 3, 1 for k = 6, 10), measurement build, on the bench's uniform step: encode, then decode with data shards 0..m-1 lost.  Same process, same
+buffers, rounds alternated, HIP events around REPS back-to-back steps
+(median); two fresh buffer sets per config; outputs checked against the
+fixed order's.
+  python3 scripts/probe_matmul_wq.py
+"""
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "hdfs-native_amd"))
+
+import torch  # noqa: E402
+
+import hdfs_native_ec as H  # noqa: E402
+
+CELL = 1 << 20
+CONFIGS = [(6, 3, 1024), (10, 4, 256), (3, 2, 1024)]
+SETS = int(os.environ.get("PROBE_SETS", "2"))
+ROUNDS = int(os.environ.get("PROBE_ROUNDS", "5"))
+REPS = int(os.environ.get("PROBE_REPS", "6"))
+VARIANTS = [("fixed order", 3), ("queue x1", 1), ("queue x2", 2)]
+
+
+def main():
+    dev = torch.device("cuda:0")
+    stream = torch.cuda.current_stream()
+    lib = H.experimental_lib()
+    g = torch.Generator(device=dev)
+    g.manual_seed(9)
+    cases = []
+    for k, m, S in CONFIGS:
+        coder = H.Coder(k, m, 0, lib=lib)
+        for si in range(SETS):
+            d = torch.empty((S, k, CELL), dtype=torch.uint8, device=dev)
+            d.random_(0, 256, generator=g)
+            ps = [torch.empty((S, m, CELL), dtype=torch.uint8, device=dev) for _ in VARIANTS]
+            rs = [torch.empty((S, k, CELL), dtype=torch.uint8, device=dev) for _ in VARIANTS]
+            cases.append(dict(name=f"RS({k},{m}) x {S} set {si}", coder=coder, d=d, ps=ps, rs=rs, m=m,
+                              bytes=2 * (k + m) * S * CELL, t={v: [] for v, _ in VARIANTS}))
+    torch.cuda.synchronize()
+
+    def step(c, i, wq):
+        H.tune_set(27, wq, lib)
+        H.encode_batch(c["coder"], c["d"], c["ps"][i], stream)
+        H.decode_batch(c["coder"], c["d"], c["ps"][i], list(range(c["m"])), c["rs"][i], stream)
+        H.tune_set(27, 0, lib)
+
+    for c in cases:
+        for i, (_, wq) in enumerate(VARIANTS):
+            step(c, i, wq)
+        torch.cuda.synchronize()
+        m = c["m"]
+        for i in range(len(VARIANTS)):
+            assert torch.equal(c["ps"][i], c["ps"][0]), (c["name"], VARIANTS[i][0])
+            assert torch.equal(c["rs"][i][:, :m], c["d"][:, :m]), (c["name"], VARIANTS[i][0])
+    for _ in range(ROUNDS):
+        for c in cases:
+            for i, (v, wq) in enumerate(VARIANTS):
+                step(c, i, wq)
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record(stream)
+                for _ in range(REPS):
+                    step(c, i, wq)
+                b.record(stream)
+                torch.cuda.synchronize()
+                c["t"][v].append(a.elapsed_time(b) / REPS)
+    for c in cases:
+        parts = []
+        for v, ts in c["t"].items():
+            med = statistics.median(ts)
+            parts.append(f"{v} {med:.4f} ms/step ({c['bytes'] / (med * 1e-3) / 8e12:.3f})")
+        print(f"{c['name']:22s} " + "  ".join(parts), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -405,7 +405,7 @@ def test_tune_set_concurrent_with_launches(xlib, dev, c_oracle):
 
 
 def test_tune_set_rejects_unknown_values(xlib):
-    for key, value in [(3, 99), (1, 5), (5, 6), (11, 8), (16, 1), (17, 6), (19, 3), (20, 3), (21, 4), (22, 2), (23, 2), (24, 6), (25, 4097), (26, 2), (27, 0), (0, 0)]:
+    for key, value in [(3, 99), (1, 5), (5, 6), (11, 8), (16, 1), (17, 6), (19, 3), (20, 3), (21, 4), (22, 2), (23, 2), (24, 6), (25, 4097), (26, 5), (27, 4), (28, 0), (0, 0)]:
         with pytest.raises(ValueError):
             H.tune_set(key, value, xlib)
 
@@ -426,6 +426,48 @@ def test_mixed_row_policies(xlib, dev, c_oracle, k, m, cell, skip):
 
 def test_mixed_many_plans_skipped_rows(xlib, dev):
     P.mixed_many_plans_body(dev, P.coder(10, 4, xlib), [(20, 2)], xlib)
+
+
+@pytest.mark.parametrize("k,m,cell", [(6, 3, 4096), (6, 3, 65536 + 64), (10, 4, 8192), (3, 2, 4096 + 16),
+                                      (2, 1, 1024), (6, 3, 1 << 20)])
+@pytest.mark.parametrize("wq", [2, 3])
+def test_mixed_work_queue(xlib, dev, c_oracle, k, m, cell, wq):
+    """Tune key 26: the mixed decode's work queue at 2 rounds of wave-tiles
+    per atomic (the product runs 1 and 4) and the fixed tile order it
+    replaced (3), against the oracle."""
+    for _ in range(2):
+        P.mixed_patterns_body(dev, c_oracle, k, m, cell, P.coder(k, m, xlib), [(26, wq)], xlib)
+
+
+@pytest.mark.parametrize("k,m,cell,S", [(6, 3, 1 << 20, 24), (10, 4, 1 << 20, 12), (3, 2, 1 << 20, 24),
+                                        (2, 1, 65536 * 8, 9), (10, 4, 65536, 40), (6, 3, 1 << 20, 1)])
+@pytest.mark.parametrize("wq", [1, 2, 3])
+def test_matmul_work_queue(xlib, dev, c_oracle, k, m, cell, S, wq):
+    """Tune key 27: the register kernel's work queue at 1 and 2 rounds of
+    wave-tiles per atomic (the product runs 2 for k <= 3, 1 for k = 6, 10)
+    and the fixed tile order it replaced (3): encode and decode of data
+    0..m-1 against the oracle, three launches in a row (the counters must
+    come back to zero)."""
+    d = P._device_random((S, k, cell), dev, seed=k * 100 + S + wq)
+    c = P.coder(k, m, xlib)
+    with P.knobs([(27, wq)], xlib):
+        for _ in range(3):
+            p = torch.empty((S, m, cell), dtype=torch.uint8, device=dev)
+            H.encode_batch(c, d, p)
+            out = torch.zeros_like(d)
+            H.decode_batch(c, d, p, list(range(m)), out)
+            torch.cuda.synchronize()
+            assert torch.equal(out[:, :m], d[:, :m])
+    O.c_check_batch(c_oracle, k, m, d.cpu().numpy(), p.cpu().numpy(), threads=4)
+
+
+@pytest.mark.parametrize("S", [24, 256])
+@pytest.mark.parametrize("wq", [2, 3])
+def test_mixed_work_queue_resident_plans(xlib, dev, S, wq):
+    """RS(10,4) random losses of any shards, key 26 = 2 / 3: plans under and
+    past 64 KiB of LDS (S = 512 restages per stripe: no queue there)."""
+    P.mixed_many_plans_body(dev, P.coder(10, 4, xlib), [(26, wq)], xlib, S=S)
+    P.mixed_many_plans_body(dev, P.coder(10, 4, xlib), [(26, wq)], xlib, S=512)
 
 
 @pytest.mark.parametrize("cell,bpc,n", P.CRC32C_CASES)

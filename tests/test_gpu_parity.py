@@ -436,6 +436,39 @@ def test_full_size_roundtrip_and_oracle(dev, c_oracle, k, m, cell, S):
                     np.ascontiguousarray(out[:, :m].cpu().numpy()), threads=_cpu_share())
 
 
+def test_work_queue_counters_reset_across_launches(dev, c_oracle):
+    """The register kernel deals wave-tiles from per-stream launch counters
+    that each launch leaves at zero (ec_kernels.hip gf_matmul_v16): launches
+    of different tile counts back to back on one stream (fewer tiles than
+    counters, fewer than CUs, many), then two streams at once -- a counter
+    left non-zero would skip tiles of the next launch."""
+    k, m = 6, 3
+    cod = coder(k, m)
+    for S, cell in [(1, 1 << 20), (3, 1 << 20), (1, 4096), (200, 1 << 20), (5, 8192 + 16), (64, 1 << 20)]:
+        d = _device_random((S, k, cell), dev, seed=S * 7 + cell)
+        p = torch.empty((S, m, cell), dtype=torch.uint8, device=dev)
+        H.encode_batch(cod, d, p)
+        out = torch.zeros_like(d)
+        H.decode_batch(cod, d, p, [0, 1, 2], out)
+        torch.cuda.synchronize()
+        assert torch.equal(out[:, :3], d[:, :3]), (S, cell)
+        O.c_check_batch(c_oracle, k, m, d[:2].cpu().numpy(), p[:2].cpu().numpy(), threads=1)
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    S, cell = 96, 1 << 20
+    ds = [_device_random((S, k, cell), dev, seed=50 + i) for i in range(3)]
+    ps = [torch.empty((S, m, cell), dtype=torch.uint8, device=dev) for _ in range(3)]
+    want = [torch.empty_like(x) for x in ps]
+    for i in range(3):
+        H.encode_batch(cod, ds[i], want[i])
+    torch.cuda.synchronize()
+    for rep in range(3):
+        for i, st in enumerate(streams):
+            H.encode_batch(cod, ds[i], ps[i], st)
+        torch.cuda.synchronize()
+        for i in range(3):
+            assert torch.equal(ps[i], want[i]), (rep, i)
+
+
 def test_linearity(dev):
     k, m, S, cell = 6, 3, 16, 1 << 18
     a = _device_random((S, k, cell), dev, 1)
@@ -655,6 +688,38 @@ def test_device_decode_mixed_matches_uniform_decode(dev, c_oracle):
     torch.cuda.synchronize()
     assert torch.equal(o1, o2)
     assert torch.equal(o1[:, 0], d[:, 0]) and torch.equal(o1[:, 2], d[:, 2])
+
+
+@pytest.mark.parametrize("k,m,S", [(6, 3, 64), (10, 4, 32), (3, 2, 64)])
+def test_device_decode_mixed_full_size_workspace_reuse(dev, c_oracle, k, m, S):
+    """Full-size cells through the mixed decode's work queue (wave-tiles
+    dealt by the launch counters the workspace upload zeroes): three calls in
+    a row on ONE workspace with different patterns -- a counter left at its
+    end value would skip every tile of the next call -- each checked against
+    the original data, and the last call's stripe 0 against the oracle's
+    decode."""
+    cell = 1 << 20
+    g = torch.Generator(device=dev)
+    g.manual_seed(900 + k)
+    d = torch.randint(0, 256, (S, k, cell), dtype=torch.uint8, device=dev, generator=g)
+    p = torch.empty((S, m, cell), dtype=torch.uint8, device=dev)
+    H.encode_batch(coder(k, m), d, p)
+    ws = None
+    full = (1 << (k + m)) - 1
+    for call in range(3):
+        masks = _random_masks(k, m, S, seed=31 * call + k)
+        out = torch.full_like(d, 0x5A)
+        ws = H.decode_batch_mixed(coder(k, m), d, p, masks, out, workspace=ws)
+        torch.cuda.synchronize()
+        lost = torch.tensor([[not (mk >> i) & 1 for i in range(k)] for mk in masks], device=dev)
+        assert bool(((out == d) | ~lost[:, :, None]).all()), call
+        assert bool(((out == 0x5A) | lost[:, :, None]).all()), call
+    miss0 = [i for i in range(k + m) if not (masks[0] >> i) & 1]
+    if any(i < k for i in miss0) and len(miss0) <= m:
+        present = full & masks[0]
+        d0 = d[:1].cpu().numpy()
+        O.c_check_batch(c_oracle, k, m, d0, p[:1].cpu().numpy(), present,
+                        np.ascontiguousarray(out[:1, [i for i in miss0 if i < k]].cpu().numpy()), threads=1)
 
 
 # ---- rs-legacy codec (SURVEY §8f row 4; parity unpinned, see oracle) -----
