@@ -293,6 +293,18 @@ const void* encode_bsl(bool bsl) {
     return reinterpret_cast<const void*>(&gf_fused_crc<K, R, SL, SCHEME, crc::kCrc32c, false, 2, PAIR>);
 }
 
+// encode + CRC with the work queue of wave-tiles (gf_device.hpp WaveQueue),
+// the default bit-sliced shape; the product compiles it for k = 3 and 10
+// (launch_fused: the k it wins at)
+template <int K, int R>
+const void* encode_wq_fn() {
+    constexpr int SL = fused_slabs(K, R);
+    if constexpr (bsl_shape<K, R>() && (kExperimental || K != 6))
+        return reinterpret_cast<const void*>(
+            &gf_fused_crc<K, R, SL, 12, crc::kCrc32c, false, 2, SL == 4, RsNet<K, R>, 1, true>);
+    return nullptr;
+}
+
 template <int K, int R>
 const void* encode_fn(int slabs, int scheme, int wpe, bool pair, bool bsl) {
 #ifndef HEC_EXPERIMENTAL
@@ -503,10 +515,35 @@ int launch_fused(const MatmulArgs& in, const FusedCrcArgs& cs, bool verify, int 
         // `waves` and grid already follow wpe)
         if (jit::verify_kernel(device, a.k, a.r, cs.kind, js, wpe, jp, mat, false, &vk, scheme)) use_slabs = js;
     }
+    // Encode + CRC with the work queue of wave-tiles at k = 3 and 10; k = 6
+    // keeps the block tiles.  Same process and buffers, 2 sets x 5 alternated
+    // rounds (scripts/probe_fused_wq.py, profiles/r05z): RS(10,4) x 256
+    // 0.675-0.683 of HBM peak vs 0.627-0.628, RS(3,2) x 1024 0.721-0.724 vs
+    // 0.697-0.698, RS(6,3) x 1024 0.697-0.709 vs 0.703-0.712.  Tune key 28
+    // (measurement build): 1 = the queue at k = 3, 6, 10; 2 = block tiles.
+    bool wq = false;
+    const bool wq_want = kExperimental && tn.fused_wq ? tn.fused_wq == 1 : (a.k == 3 || a.k == 10);
+    if (wq_want && !verify && !split && fn && scheme == 12 && wpe == 2 && !vk.fn && slabs == fused_slabs(a.k, a.r) &&
+        rs_parity_matrix(a) && tn.fused_bsl != 1) {
+        const void* f = nullptr;
+        switch (a.k * 16 + a.r) {
+            case 3 * 16 + 2: f = encode_wq_fn<3, 2>(); break;
+            case 6 * 16 + 3: f = encode_wq_fn<6, 3>(); break;
+            case 10 * 16 + 4: f = encode_wq_fn<10, 4>(); break;
+            default: break;
+        }
+        a.queue = f ? stream_counters(device, stream) : nullptr;
+        if (a.queue) {
+            fn = f;
+            wq = true;
+        }
+    }
     if (!fn && !vk.fn) return -1;
     const uint64_t chunks = a.cell_len / 16;
-    // split: 4 GF waves x 8 KiB per tile; else waves x slabs x 1 KiB
-    const uint64_t tile_bytes = split ? 4u * 8192u : 1024u * uint64_t(use_slabs) * uint64_t(waves);
+    // split: 4 GF waves x 8 KiB per tile; else waves x slabs x 1 KiB (work
+    // queue: one wave's slabs)
+    const uint64_t tile_bytes =
+        split ? 4u * 8192u : 1024u * uint64_t(use_slabs) * uint64_t(wq ? 1 : waves);
     const uint64_t tps = (a.cell_len + tile_bytes - 1) / tile_bytes;
     const uint64_t total = tps * a.stripes;
     if (chunks > 0xFFFFFFFFull || total > 0xFFFFFFFFull) return -1;
@@ -528,6 +565,7 @@ int launch_fused(const MatmulArgs& in, const FusedCrcArgs& cs, bool verify, int 
     // CRC 1.776 vs 1.803), 32 beats 8 by 1.5-2 % (r04o) and ties 16 (r04p;
     // 64: 1-2 % slower)
     uint64_t grid = tn.grid ? uint64_t(tn.grid) : uint64_t(num_cus(device)) * ((split || wpe == 3) ? 4 : 32);
+    if (wq && !tn.grid) grid = uint64_t(num_cus(device)) * 2;  // the resident blocks drain the queue
     if (grid > total) grid = total;
     FusedCrcArgs c = cs;
     void* args[] = {&a, &c};

@@ -83,8 +83,11 @@ __device__ __forceinline__ const uint32_t* fused_slice32() {
 // transposed back at the end -- instead of through the v_perm product
 // tables: RS(6,3) 650 instead of 960 VALU per 8 dwords of every shard,
 // RS(10,4) 1155 instead of 2000.  The kernel is VALU-issue bound.
+// WQ: tiles are wave-tiles (SLABS KiB of one stripe's cells per wave) from
+// the work queue (gf_device.hpp WaveQueue, a.queue) instead of block tiles in
+// a fixed order.
 template <int K, int R, int SLABS, int SCHEME, int KIND, bool VERIFY, int WPE = 2, bool PAIR = false,
-          class NET = PermNet, int PFD = 1>
+          class NET = PermNet, int PFD = 1, bool WQ = false>
 __global__ __launch_bounds__(crcdev::sliced(SCHEME) ? 128 * WPE * (WPE - 1) : 512)
     __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void gf_fused_crc(
     MatmulArgs a, FusedCrcArgs cs) {
@@ -110,7 +113,7 @@ __global__ __launch_bounds__(crcdev::sliced(SCHEME) ? 128 * WPE * (WPE - 1) : 51
     // behind this tile's stores (vmcnt retires in order) with nothing to do
     constexpr bool EARLY_OUT = VERIFY && PFD == 5;
     constexpr int CPS = SLABS * 2, NWANT = WANT_PF ? (NSUM * CPS + 63) / 64 : 1;
-    constexpr uint32_t WAVE_BYTES = SLABS * 1024u, TILE_BYTES = WAVES * WAVE_BYTES;
+    constexpr uint32_t WAVE_BYTES = SLABS * 1024u, TILE_BYTES = WQ ? WAVE_BYTES : WAVES * WAVE_BYTES;
     constexpr bool PF = R * SLABS <= 24;  // register prefetch of the next shard
     __shared__ PermTable s_tab[R][K];  // K columns: scheme 11 needs 2 x 79 KiB per CU
     __shared__ uint8_t s_exp[512];
@@ -156,10 +159,14 @@ __global__ __launch_bounds__(crcdev::sliced(SCHEME) ? 128 * WPE * (WPE - 1) : 51
     // previous tile's outputs)
     bool have_next = false;
     u32x4 x[SLABS], xn[SLABS];
-    for (uint32_t tile = blockIdx.x; tile < total; tile += gridDim.x) {
+    WaveQueue wq;
+    if constexpr (WQ) wq.init(a.queue, total, WAVES);
+    // the wave's byte offset inside a block tile (WQ: a wave-tile is the wave's own)
+    const uint32_t wave_off = WQ ? 0u : uint32_t(wave) * WAVE_BYTES;
+    for (uint32_t tile = WQ ? wq.next() : blockIdx.x; tile < total; tile = WQ ? wq.next() : tile + gridDim.x) {
         uint32_t stripe, tcol;
         coords(tile, stripe, tcol);
-        const uint64_t wbyte = uint64_t(tcol) * TILE_BYTES + uint64_t(wave) * WAVE_BYTES;  // wave's first byte
+        const uint64_t wbyte = uint64_t(tcol) * TILE_BYTES + wave_off;  // wave's first byte
         if (wbyte >= cell_len) continue;  // wave-uniform (never a prefetched tile: those are full)
         // 32-bit lane offsets from a wave-uniform per-shard base (saddr +
         // voffset addressing); dead slabs of a short last tile read slab 0
@@ -323,11 +330,11 @@ __global__ __launch_bounds__(crcdev::sliced(SCHEME) ? 128 * WPE * (WPE - 1) : 51
         // the next tile's input 0 (and 1: `two`) into x (xn) when that tile is
         // full for this wave (its lane offsets are then the constant ones)
         auto prefetch_next = [&](bool two) {
-            const uint32_t nt = tile + gridDim.x;
+            const uint32_t nt = WQ ? wq.peek() : tile + gridDim.x;
             if (nt < total) {
                 uint32_t ns, ncol;
                 coords(nt, ns, ncol);
-                const uint64_t nw = uint64_t(ncol) * TILE_BYTES + uint64_t(wave) * WAVE_BYTES;
+                const uint64_t nw = uint64_t(ncol) * TILE_BYTES + wave_off;
                 if (nw + WAVE_BYTES <= cell_len) {  // wave-uniform
 #pragma unroll
                     for (int u = 0; u < SLABS; u++)

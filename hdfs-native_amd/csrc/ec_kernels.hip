@@ -1027,32 +1027,6 @@ const void* pick_wq(int k, int r, int wq) {
 // RS(10,4) x 256 0.740 at 1 vs 0.729-0.732.
 int default_wq(int k) { return k == 2 || k == 3 ? 2 : (k == 6 || k == 10) ? 1 : 0; }
 
-// The work-queue counters of (device, stream): kMixedQueues of them,
-// kMixedQueueStride apart, zero at rest (each launch leaves them zero, see
-// gf_matmul_v16), zeroed on the stream when first made.  Launches on one
-// stream run in order, so they share a set; launches on different streams
-// get different sets.  Never freed (2 KiB per stream that ever launched).
-uint32_t* stream_counters(int device, hipStream_t stream) {
-    static std::mutex mu;
-    static std::map<std::pair<int, uintptr_t>, uint32_t*> sets;
-    std::lock_guard<std::mutex> lk(mu);
-    uint32_t*& c = sets[{device, reinterpret_cast<uintptr_t>(stream)}];
-    if (!c) {
-        const size_t bytes = size_t(kMixedQueues) * kMixedQueueStride;
-        if (hipMalloc(reinterpret_cast<void**>(&c), bytes) != hipSuccess) {
-            (void)hipGetLastError();
-            c = nullptr;
-            return nullptr;
-        }
-        if (hipMemsetAsync(c, 0, bytes, stream) != hipSuccess) {
-            (void)hipGetLastError();
-            (void)hipFree(c);
-            c = nullptr;
-        }
-    }
-    return c;
-}
-
 #ifdef HEC_EXPERIMENTAL
 // Bit-sliced encode for the (K, R) pairs with a generated network (K > 2:
 // RS(2,1)'s network is no shorter than its tables); nullptr otherwise.
@@ -1113,6 +1087,32 @@ Shape default_shape(int k, uint64_t cell_len) {
 }
 
 }  // namespace
+
+// The work-queue counters of (device, stream): kMixedQueues of them,
+// kMixedQueueStride apart, zero at rest (each launch leaves them zero, see
+// gf_matmul_v16), zeroed on the stream when first made.  Launches on one
+// stream run in order, so they share a set; launches on different streams
+// get different sets.  Never freed (2 KiB per stream that ever launched).
+uint32_t* stream_counters(int device, hipStream_t stream) {
+    static std::mutex mu;
+    static std::map<std::pair<int, uintptr_t>, uint32_t*> sets;
+    std::lock_guard<std::mutex> lk(mu);
+    uint32_t*& c = sets[{device, reinterpret_cast<uintptr_t>(stream)}];
+    if (!c) {
+        const size_t bytes = size_t(kMixedQueues) * kMixedQueueStride;
+        if (hipMalloc(reinterpret_cast<void**>(&c), bytes) != hipSuccess) {
+            (void)hipGetLastError();
+            c = nullptr;
+            return nullptr;
+        }
+        if (hipMemsetAsync(c, 0, bytes, stream) != hipSuccess) {
+            (void)hipGetLastError();
+            (void)hipFree(c);
+            c = nullptr;
+        }
+    }
+    return c;
+}
 
 bool rs_parity_matrix(const MatmulArgs& a) {
     if (a.k < 1 || a.k > kMaxK || a.r < 1 || a.r > kMaxR) return false;

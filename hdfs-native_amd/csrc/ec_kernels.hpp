@@ -83,6 +83,10 @@ struct MixedArgs {
     uint32_t* queue;                  // this launch's zeroed tile counters (work-queue variant, key 26)
 };
 
+// The work-queue launch counters of (device, stream) (ec_kernels.hip): zero
+// at rest, made and zeroed on the stream on first use; nullptr on failure.
+uint32_t* stream_counters(int device, hipStream_t stream);
+
 // Mixed-pattern decode of one group of missing rows row0 .. row0+rows-1
 // (rows <= kMaxR).  Requires k in {2,3,6,10}, 16-B aligned bases/strides
 // and cell_len % 16 == 0.  0 ok, -1 unsupported, >0 hipError_t.

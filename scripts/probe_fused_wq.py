@@ -1,0 +1,85 @@
+"""Measurement probe (GPU box): the fused encode + CRC32C kernel with its
+block tiles (tune key 28 = 2; the default at k = 6) against the work queue
+of wave-tiles (key 28 = 1; the default at k = 3 and 10), measurement build.  Same process, same buffers, rounds
+alternated, HIP events around REPS back-to-back launches (median), two fresh
+buffer sets per config; parity and sums checked equal.
+  python3 scripts/probe_fused_wq.py
+"""
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "hdfs-native_amd"))
+
+import torch  # noqa: E402
+
+import hdfs_native_ec as H  # noqa: E402
+
+CELL = 1 << 20
+CONFIGS = [(6, 3, 1024), (10, 4, 256), (3, 2, 1024)]
+SETS = int(os.environ.get("PROBE_SETS", "2"))
+ROUNDS = int(os.environ.get("PROBE_ROUNDS", "5"))
+REPS = int(os.environ.get("PROBE_REPS", "6"))
+VARIANTS = [("block tiles", 2), ("queue", 1)]
+
+
+def main():
+    dev = torch.device("cuda:0")
+    stream = torch.cuda.current_stream()
+    sp = stream.cuda_stream
+    lib = H.experimental_lib()
+    g = torch.Generator(device=dev)
+    g.manual_seed(11)
+    cases = []
+    for k, m, S in CONFIGS:
+        coder = H.Coder(k, m, 0, lib=lib)
+        nck = CELL // 512
+        for si in range(SETS):
+            d = torch.empty((S, k, CELL), dtype=torch.uint8, device=dev)
+            d.random_(0, 256, generator=g)
+            dp, ds = H.stripe_layout_ptrs(d, k)
+            outs = []
+            for _ in VARIANTS:
+                p = torch.empty((S, m, CELL), dtype=torch.uint8, device=dev)
+                sums = torch.empty((S, k + m, nck, 4), dtype=torch.uint8, device=dev)
+                pp, ps = H.stripe_layout_ptrs(p, m)
+                outs.append((p, sums, pp, ps))
+            cases.append(dict(name=f"RS({k},{m}) x {S} set {si}", coder=coder, d=d, dp=dp, ds=ds, outs=outs, S=S,
+                              bytes=(k + m) * S * CELL + 4 * nck * (k + m) * S, t={v: [] for v, _ in VARIANTS}))
+    torch.cuda.synchronize()
+
+    def run(c, i, wq):
+        p, sums, pp, ps = c["outs"][i]
+        H.tune_set(28, wq, lib)
+        c["coder"].encode_crc_device(c["dp"], c["ds"], pp, ps, CELL, c["S"], 512, sums.data_ptr(), sp)
+        H.tune_set(28, 0, lib)
+
+    for c in cases:
+        for i, (_, wq) in enumerate(VARIANTS):
+            run(c, i, wq)
+        torch.cuda.synchronize()
+        for i in range(1, len(VARIANTS)):
+            assert torch.equal(c["outs"][i][0], c["outs"][0][0]), (c["name"], "parity")
+            assert torch.equal(c["outs"][i][1], c["outs"][0][1]), (c["name"], "sums")
+    for _ in range(ROUNDS):
+        for c in cases:
+            for i, (v, wq) in enumerate(VARIANTS):
+                run(c, i, wq)
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record(stream)
+                for _ in range(REPS):
+                    run(c, i, wq)
+                b.record(stream)
+                torch.cuda.synchronize()
+                c["t"][v].append(a.elapsed_time(b) / REPS)
+    for c in cases:
+        parts = []
+        for v, ts in c["t"].items():
+            med = statistics.median(ts)
+            parts.append(f"{v} {med:.4f} ms ({c['bytes'] / (med * 1e-3) / 8e12:.3f})")
+        print(f"{c['name']:22s} " + "  ".join(parts), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -405,7 +405,7 @@ def test_tune_set_concurrent_with_launches(xlib, dev, c_oracle):
 
 
 def test_tune_set_rejects_unknown_values(xlib):
-    for key, value in [(3, 99), (1, 5), (5, 6), (11, 8), (16, 1), (17, 6), (19, 3), (20, 3), (21, 4), (22, 2), (23, 2), (24, 6), (25, 4097), (26, 5), (27, 4), (28, 0), (0, 0)]:
+    for key, value in [(3, 99), (1, 5), (5, 6), (11, 8), (16, 1), (17, 6), (19, 3), (20, 3), (21, 4), (22, 2), (23, 2), (24, 6), (25, 4097), (26, 5), (27, 4), (28, 3), (29, 0), (0, 0)]:
         with pytest.raises(ValueError):
             H.tune_set(key, value, xlib)
 
@@ -459,6 +459,15 @@ def test_matmul_work_queue(xlib, dev, c_oracle, k, m, cell, S, wq):
             torch.cuda.synchronize()
             assert torch.equal(out[:, :m], d[:, :m])
     O.c_check_batch(c_oracle, k, m, d.cpu().numpy(), p.cpu().numpy(), threads=4)
+
+
+@pytest.mark.parametrize("codec,k,m,cell,S", [c for c in P.ENCODE_CRC_CASES if c[1] in (3, 6, 10) and c[0] == "rs"])
+@pytest.mark.parametrize("wq", [1, 2])
+def test_encode_crc_work_queue(xlib, dev, c_oracle, codec, k, m, cell, S, wq):
+    """Tune key 28: fused encode + CRC with the work queue at k = 3, 6, 10 (1)
+    and with the block tiles it replaced at k = 3, 10 (2), against the
+    oracle's parity and sums."""
+    P.encode_crc_body(dev, c_oracle, codec, k, m, cell, S, xlib, [(28, wq)])
 
 
 @pytest.mark.parametrize("S", [24, 256])

@@ -968,10 +968,13 @@ def encode_crc_body(dev, c_oracle, codec, k, m, cell, S, xlib, knob_pairs=()):
     assert np.array_equal(sums.cpu().numpy(), want)
 
 
-def test_encode_crc_full_size_properties(dev):
-    """RS(6,3) 1 MiB x 64 fused: parity equals a plain encode and sums equal
-    a standalone CRC pass over the same k+m cells (size-independent)."""
-    k, m, cell, S = 6, 3, 1 << 20, 64
+@pytest.mark.parametrize("k,m,S", [(6, 3, 64), (10, 4, 24), (3, 2, 64)])
+def test_encode_crc_full_size_properties(dev, k, m, S):
+    """1 MiB cells fused (RS(6,3) block tiles; RS(10,4) and RS(3,2) through
+    the work queue of wave-tiles, twice in a row on one stream): parity
+    equals a plain encode and sums equal a standalone CRC pass over the same
+    k+m cells (size-independent)."""
+    cell = 1 << 20
     c = coder(k, m)
     d = torch.empty((S, k, cell), dtype=torch.uint8, device=dev)
     g = torch.Generator(device=dev).manual_seed(7)
@@ -982,11 +985,14 @@ def test_encode_crc_full_size_properties(dev):
     sums = torch.empty((S, k + m, cell // 512, 4), dtype=torch.uint8, device=dev)
     dp, ds = H.stripe_layout_ptrs(d, k)
     pp, ps = H.stripe_layout_ptrs(p2, m)
-    c.encode_crc_device(dp, ds, pp, ps, cell, S, 512, sums.data_ptr(), torch.cuda.current_stream().cuda_stream)
-    ref = H.crc32c_batch(c, torch.cat([d, p1], dim=1), 512)
-    torch.cuda.synchronize()
-    assert torch.equal(p1, p2)
-    assert torch.equal(sums, ref)
+    for _ in range(2):
+        p2.zero_()
+        sums.zero_()
+        c.encode_crc_device(dp, ds, pp, ps, cell, S, 512, sums.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        ref = H.crc32c_batch(c, torch.cat([d, p1], dim=1), 512)
+        torch.cuda.synchronize()
+        assert torch.equal(p1, p2)
+        assert torch.equal(sums, ref)
 
 
 # ---- Chunk checksums on the read path: CRC32 / CRC32C verify and the ----
