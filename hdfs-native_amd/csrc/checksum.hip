@@ -43,6 +43,7 @@
 #include "checksum_device.hpp"
 #include "checksum_tables.hpp"
 #include "ec_kernels.hpp"
+#include "work_queue.hpp"
 
 namespace hec {
 
@@ -110,8 +111,12 @@ struct CrcShape : crcdev::TableLayout<SCHEME> {
     static constexpr int kWaves = kBlock / 64;
 };
 
-template <int KIND, int SCHEME, int PF>
+// WQ > 0 (PF = 1 only): tasks come from the work queue of wave-tiles
+// (work_queue.hpp, a.queue) in units of WQ consecutive tasks of one cell,
+// one unit per atomic; the next task is still loaded during this one.
+template <int KIND, int SCHEME, int PF, int WQ = 0>
 __global__ __launch_bounds__(CrcShape<SCHEME>::kBlock) void checksum_chunks512(CrcArgs a) {
+    static_assert(WQ == 0 || PF == 1, "the queue runs one task of prefetch");
     using Sh = CrcShape<SCHEME>;
     using Spec = crc::Spec<KIND>;
     constexpr bool REFL = Spec::kReflected;
@@ -174,6 +179,22 @@ __global__ __launch_bounds__(CrcShape<SCHEME>::kBlock) void checksum_chunks512(C
         asm volatile("" ::: "memory");
     };
 
+    if constexpr (WQ > 0) {
+        // units of WQ tasks; the launcher keeps the unit count below 2^32
+        const uint32_t units = uint32_t((tasks + WQ - 1) / WQ);
+        WaveQueue q;
+        q.init(a.queue, units, Sh::kWaves);
+        auto task_of = [&](uint32_t u) { return u < units ? uint64_t(u) * WQ : tasks; };
+        uint64_t task = task_of(q.next());
+        u32x4 v[8];
+        if (task < tasks) load_task(a, groups, task, lane, v);
+        while (task < tasks) {
+            const bool unit_end = (task % WQ) == WQ - 1 || task + 1 >= tasks;
+            run_task(task, v, unit_end ? task_of(q.peek()) : task + 1);
+            task = unit_end ? task_of(q.next()) : task + 1;
+        }
+        return;
+    }
     // PF register sets in flight: task t's loads are issued while task t-PF
     // is checksummed
     uint64_t task = uint64_t(blockIdx.x) * Sh::kWaves + wave;
@@ -454,6 +475,17 @@ const void* crc_pick(int scheme, int pf) {
         return crc_fn<KIND, 12>(pf);
     }
 #endif
+#ifdef HEC_EXPERIMENTAL
+    // the fold with the work queue (tune key 29 = 1 / 2 / 4 tasks per unit)
+    if (scheme == 12 && pf < 0) {
+        if constexpr (KIND == crc::kCrc32c) {
+            if (pf == -1) return reinterpret_cast<const void*>(&checksum_chunks512<KIND, 12, 1, 1>);
+            if (pf == -2) return reinterpret_cast<const void*>(&checksum_chunks512<KIND, 12, 1, 2>);
+            if (pf == -4) return reinterpret_cast<const void*>(&checksum_chunks512<KIND, 12, 1, 4>);
+        }
+        return nullptr;
+    }
+#endif
 #ifndef HEC_EXPERIMENTAL
     // product: the fold (CRC32C, one task of prefetch) / 11-bit slicing inside
     // scheme 12 (CRC32, two tasks)
@@ -540,6 +572,21 @@ int launch_checksum(const CrcArgs& in, int device, hipStream_t stream) {
         const uint64_t cap = tn.grid ? uint64_t(tn.grid) : uint64_t(cus) * per_cu;
         if (grid > cap) grid = cap;
         const void* fn = a.kind == crc::kCrc32c ? crc_pick<crc::kCrc32c>(scheme, pf) : crc_pick<crc::kCksum>(scheme, pf);
+#ifdef HEC_EXPERIMENTAL
+        // tune key 29: the fold kernel with the work queue, 1 / 2 / 4 tasks per
+        // unit, the resident blocks only
+        if (tn.crc_wq && scheme == 12 && a.kind == crc::kCrc32c && pf == 1 &&
+            (tasks + uint64_t(tn.crc_wq) - 1) / uint64_t(tn.crc_wq) < (uint64_t(1) << 32)) {
+            const void* f = crc_pick<crc::kCrc32c>(12, -tn.crc_wq);
+            a.queue = f ? stream_counters(device, stream) : nullptr;
+            if (a.queue) {
+                fn = f;
+                grid = uint64_t(cus) * per_cu;
+                const uint64_t units = (tasks + uint64_t(tn.crc_wq) - 1) / uint64_t(tn.crc_wq);
+                if (grid > units) grid = units;
+            }
+        }
+#endif
         e = hipLaunchKernel(fn, dim3(uint32_t(grid)), dim3(uint32_t(waves * 64)), args, 0, stream);
     } else {
         const uint64_t total = a.chunks_per_cell * a.n_shards * a.stripes;

@@ -38,6 +38,7 @@ struct CrcArgs {
     uint64_t bytes_per_checksum;
     uint64_t chunks_per_cell;  // filled by the launcher
     uint64_t groups_per_cell;  // filled by the launcher (fast path)
+    uint32_t* queue;           // work-queue variant (measurement build, key 29): the stream's launch counters
 };
 
 // 0 ok, -1 invalid sizes, >0 hipError_t.

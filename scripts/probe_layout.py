@@ -10,10 +10,11 @@ Kernels: checksum_chunks512 (CRC32C of all k+m cells), gf_matmul_v16
 (encode), the fused encode + CRC32C and the plan-specialised fused decode
 {0,1,2} + verify.  Prints one line per (layout, set).
 PROBE_CRC_AB=1: the measurement build instead, CRC32C of all k+m cells by the
-LDS-DMA kernel (tune key 11 = 13) and by the default register-staged one,
-compute and verify mode, same buffers, rounds alternated (round 5 ran it with
-the DMA kernel as the default and the register one on the key: the figures in
-profiles/r05n are the same kernels).
+default register-staged kernel and by the same kernel on the work queue (tune
+key 29 = 1 / 2 / 4 tasks per unit), compute and verify mode, same buffers,
+rounds alternated; PROBE_CRC_DMA=1 adds the LDS-DMA kernel (key 11 = 13;
+profiles/r05n ran it with the DMA kernel as the default and the register one
+on the key: the same kernels).
   python3 scripts/probe_layout.py
 """
 import os
@@ -106,19 +107,21 @@ def main():
         enc_crc()
         torch.cuda.synchronize()
         if CRC_AB:
-            def tuned(fn, v):
+            def tuned(fn, v, key=11):
                 def run():
-                    H.tune_set(11, v, lib)
+                    H.tune_set(key, v, lib)
                     fn()
-                    H.tune_set(11, 0, lib)
+                    H.tune_set(key, 0, lib)
                 return run
 
             def ver(st=st, cells=cells, cstr=cstr):
                 coder.checksum_verify_device(H.CHECKSUM_CRC32C, cells, cstr, CELL, S, BPC, st["sums"].data_ptr(),
                                              st["bad"].data_ptr(), sp)
 
-            kernels[(lay, i)] = {"crc_dma": tuned(crc, 13), "crc_reg": crc, "verify_dma": tuned(ver, 13),
-                                 "verify_reg": ver}
+            kernels[(lay, i)] = {"crc_reg": crc, "crc_wq1": tuned(crc, 1, 29), "crc_wq2": tuned(crc, 2, 29),
+                                 "crc_wq4": tuned(crc, 4, 29), "verify_reg": ver, "verify_wq2": tuned(ver, 2, 29)}
+            if os.environ.get("PROBE_CRC_DMA") == "1":
+                kernels[(lay, i)].update({"crc_dma": tuned(crc, 13), "verify_dma": tuned(ver, 13)})
             continue
         kernels[(lay, i)] = {"crc_only": crc, "encode": enc, "encode_crc": enc_crc, "decode_verify": dec_ver}
     times = {key: {n: [] for n in fns} for key, fns in kernels.items()}
@@ -138,7 +141,7 @@ def main():
     algo = {"crc_only": (K + M) * CELL * S + 4 * NCH * (K + M) * S, "encode": (K + M) * CELL * S,
             "encode_crc": (K + M) * CELL * S + 4 * NCH * (K + M) * S,
             "decode_verify": (K + len(MISS)) * CELL * S + 4 * NCH * K * S}
-    for n in ("crc_dma", "crc_reg", "verify_dma", "verify_reg"):
+    for n in ("crc_dma", "crc_reg", "verify_dma", "verify_reg", "crc_wq1", "crc_wq2", "crc_wq4", "verify_wq2"):
         algo[n] = algo["crc_only"]
     for key, per in times.items():
         parts = []

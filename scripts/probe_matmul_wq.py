@@ -24,6 +24,13 @@ SETS = int(os.environ.get("PROBE_SETS", "2"))
 ROUNDS = int(os.environ.get("PROBE_ROUNDS", "5"))
 REPS = int(os.environ.get("PROBE_REPS", "6"))
 VARIANTS = [("fixed order", 3), ("queue x1", 1), ("queue x2", 2)]
+# PROBE_K10=1: RS(10,4) only, its 512-thread shape against 256-thread blocks
+# (tune keys 4 = 256, 1 = 2) at 1 and 2 blocks per CU (key 3), all on the queue
+K10 = os.environ.get("PROBE_K10") == "1"
+if K10:
+    CONFIGS = [(10, 4, 256), (10, 4, 1024)]
+    VARIANTS = [("512 x1/CU", [(27, 1)]), ("256 x1/CU", [(27, 1), (4, 256), (1, 2)]),
+                ("256 x2/CU", [(27, 1), (4, 256), (1, 2), (3, 2)]), ("fixed 512 x8/CU", [(27, 3)])]
 
 
 def main():
@@ -45,10 +52,13 @@ def main():
     torch.cuda.synchronize()
 
     def step(c, i, wq):
-        H.tune_set(27, wq, lib)
+        pairs = wq if isinstance(wq, list) else [(27, wq)]
+        for key, val in pairs:
+            H.tune_set(key, val, lib)
         H.encode_batch(c["coder"], c["d"], c["ps"][i], stream)
         H.decode_batch(c["coder"], c["d"], c["ps"][i], list(range(c["m"])), c["rs"][i], stream)
-        H.tune_set(27, 0, lib)
+        for key, _ in pairs:
+            H.tune_set(key, -1 if key == 2 else 0, lib)
 
     for c in cases:
         for i, (_, wq) in enumerate(VARIANTS):

@@ -144,6 +144,43 @@ def test_crc_schemes_vs_oracle(xlib, dev, ctype, cell, bpc, n, variant, pf):
     assert np.array_equal(got.cpu().numpy(), _oracle_sums(cells, bpc, ctype))
 
 
+@pytest.mark.parametrize("cell,bpc,n", [c for c in P.CRC32C_CASES if c[1] == 512])
+@pytest.mark.parametrize("wq", [1, 2, 4])
+def test_crc_wq_vs_oracle(xlib, dev, cell, bpc, n, wq):
+    """Tune key 29: the CRC32C fold kernel on the work queue, 1 / 2 / 4 tasks
+    per unit (partial last tasks, short last chunks, units that run past the
+    last task), against the oracle."""
+    P.crc32c_body(dev, cell, bpc, n, P.coder(6, 3, xlib), [(29, wq)], xlib)
+
+
+@pytest.mark.parametrize("wq", [1, 2, 4])
+def test_crc_wq_full_size_compute_and_verify(xlib, dev, wq):
+    """Key 29 at full size (9 x 1 MiB x 64 cells), three launches in a row
+    on one stream (the counters must come back to zero): sums equal the
+    default kernel's, and verify mode flags exactly the corrupted cells."""
+    S, n, cell = 64, 9, 1 << 20
+    c = xcoder(xlib, 6, 3)
+    g = torch.Generator(device=dev).manual_seed(29 + wq)
+    x = torch.empty((S, n, cell), dtype=torch.uint8, device=dev)
+    x.random_(0, 256, generator=g)
+    want = H.crc32c_batch(c, x, 512)
+    hits = {(0, 0): 0, (5, 8): cell - 1, (31, 4): cell // 2 + 3, (63, 2): 8191, (63, 6): 8192}
+    with P.knobs([(29, wq)], xlib):
+        for _ in range(3):
+            got = H.crc32c_batch(c, x, 512)
+            torch.cuda.synchronize()
+            assert torch.equal(got, want)
+        y = x.clone()
+        for (s_, i), b in hits.items():
+            y[s_, i, b] ^= 0x41
+        bad = H.checksum_verify_batch(c, y, want, H.CHECKSUM_CRC32C, 512)
+        torch.cuda.synchronize()
+    flags = torch.zeros((S, n), dtype=torch.uint8)
+    for s_, i in hits:
+        flags[s_, i] = 1
+    assert torch.equal(bad.cpu(), flags)
+
+
 @pytest.mark.parametrize("verify", [False, True])
 def test_crc_dma_full_size_vs_default(xlib, dev, verify):
     """The LDS-DMA CRC32C kernel (key 11 = 13: three tasks in flight per wave,
@@ -405,7 +442,7 @@ def test_tune_set_concurrent_with_launches(xlib, dev, c_oracle):
 
 
 def test_tune_set_rejects_unknown_values(xlib):
-    for key, value in [(3, 99), (1, 5), (5, 6), (11, 8), (16, 1), (17, 6), (19, 3), (20, 3), (21, 4), (22, 2), (23, 2), (24, 6), (25, 4097), (26, 5), (27, 4), (28, 3), (29, 0), (0, 0)]:
+    for key, value in [(3, 99), (1, 5), (5, 6), (11, 8), (16, 1), (17, 6), (19, 3), (20, 3), (21, 4), (22, 2), (23, 2), (24, 6), (25, 4097), (26, 5), (27, 4), (28, 3), (29, 3), (30, 0), (0, 0)]:
         with pytest.raises(ValueError):
             H.tune_set(key, value, xlib)
 
