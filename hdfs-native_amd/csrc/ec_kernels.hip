@@ -761,6 +761,7 @@ __global__ __launch_bounds__(BS) void gf_decode_mixed(MixedArgs a) {
         const uint32_t q = blockIdx.x % nq;
         uint32_t* ctr = a.queue + q * (kMixedQueueStride / 4);
         uint32_t v_next;
+        asm volatile("" : "=v"(v_next));  // defined, unread outside lane 0: no merge with the atomic's result
         if ((threadIdx.x & 63u) == 0) v_next = atomicAdd(ctr, 1u);
         for (;;) {
             const uint32_t r0 = uint32_t(__builtin_amdgcn_readfirstlane(int(v_next))) * uint32_t(WQ);
@@ -971,9 +972,13 @@ const void* dma_pick(int k, int r) {
 // (10 x 2 x 4 waves x 1 KiB = 80 KiB of LDS).
 const void* pick_dma(int k, int r, int unroll, int bs) {
 #ifndef HEC_EXPERIMENTAL
+    // the product runs the register kernel on the work queue at every cell
+    // size (default_shape); the LDS-DMA kernel is measurement-only
+    (void)k;
+    (void)r;
     (void)unroll;
     (void)bs;
-    return dma_pick<4, 256>(k, r);
+    return nullptr;
 #else
     if (k == 10) {
         switch (r) {
@@ -1090,15 +1095,20 @@ Shape default_shape(int k, uint64_t cell_len) {
     // at 256-512 stripes and ties at 2048 (profiles/r01f_probe_bpc_k10_*.log)
     if (k > 6) return {2, 512, 8, true, false};
     // RS(3,2), RS(6,3): one wave per SIMD, 4 x 1 KiB per stream per wave.
-    // Small cells (many short stripes) gain 2-3 % from the LDS-DMA prefetch;
-    // 1 MiB cells lose ~5 % with it (profiles/r01_probe_dma_pipeline.log).
-    // The LDS-DMA kernel (one block resident per CU) runs a grid of 2 per CU:
-    // +3.3 % at 64 KiB x 16384 stripes, +1 % at x 65536, against 1 per CU
-    // (profiles/r01f_probe_grid_64k_*.log); the register kernel keeps exactly
-    // the resident blocks (2 per CU: -9 % at 1 MiB).
-    const bool small = cell_len <= (256u << 10);
-    const bool dma = small && (k == 2 || k == 3 || k == 6);
-    return {4, 256, dma ? 2 : 1, true, dma};
+    // Every cell size takes the register kernel on the work queue since round
+    // 5.  Before, cells <= 256 KiB took the LDS-DMA kernel (2-3 % over the
+    // register kernel in the fixed order, profiles/r01_probe_dma_pipeline.log);
+    // the queue's wave-tiles (4 KiB per cell) beat it at every small size:
+    // same process and buffers, encode + decode of data 0..2, RS(6,3)
+    // (scripts/probe_matmul_wq.py PROBE_C64K=1, profiles/r05ac, r05ad): 64 KiB
+    // x 65536 0.785-0.788 of HBM peak vs 0.766-0.774 for the LDS-DMA kernel;
+    // 4 / 8 / 16 / 128 / 256 KiB 0.758 / 0.775 / 0.803 / 0.787 / 0.778 vs
+    // 0.256 / 0.500 / 0.748 / 0.691 / 0.710 (the fixed order's 16-KiB block
+    // tiles left most lanes of a small cell idle).  Measurement build: tune
+    // key 5 = 2 for the LDS-DMA kernel.
+    (void)k;
+    (void)cell_len;
+    return {4, 256, 1, true, false};
 }
 
 }  // namespace

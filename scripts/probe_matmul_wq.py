@@ -24,6 +24,16 @@ SETS = int(os.environ.get("PROBE_SETS", "2"))
 ROUNDS = int(os.environ.get("PROBE_ROUNDS", "5"))
 REPS = int(os.environ.get("PROBE_REPS", "6"))
 VARIANTS = [("fixed order", 3), ("queue x1", 1), ("queue x2", 2)]
+# PROBE_C64K=1: RS(6,3) 64 KiB cells x 65536 (BASELINE configs[4]): the LDS-DMA
+# kernel (the small-cell default, fixed order) against the register kernel on the
+# queue (tune key 5 = 1) and in the fixed order (5 = 1, 27 = 3)
+C64K = os.environ.get("PROBE_C64K") == "1"
+if C64K:
+    CONFIGS = [(6, 3, 65536, 1 << 16)]
+    if os.environ.get("PROBE_CELLS"):  # e.g. "8192:131072,262144:8192": cell:stripes, one set each
+        CONFIGS = [(6, 3, int(x.split(":")[1]), int(x.split(":")[0])) for x in os.environ["PROBE_CELLS"].split(",")]
+        SETS = 1
+    VARIANTS = [("LDS-DMA", [(5, 0)]), ("register queue", [(5, 1)]), ("register fixed", [(5, 1), (27, 3)])]
 # PROBE_K10=1: RS(10,4) only, its 512-thread shape against 256-thread blocks
 # (tune keys 4 = 256, 1 = 2) at 1 and 2 blocks per CU (key 3), all on the queue
 K10 = os.environ.get("PROBE_K10") == "1"
@@ -40,15 +50,17 @@ def main():
     g = torch.Generator(device=dev)
     g.manual_seed(9)
     cases = []
-    for k, m, S in CONFIGS:
+    for cfg in CONFIGS:
+        k, m, S = cfg[:3]
+        cell = cfg[3] if len(cfg) > 3 else CELL
         coder = H.Coder(k, m, 0, lib=lib)
         for si in range(SETS):
-            d = torch.empty((S, k, CELL), dtype=torch.uint8, device=dev)
+            d = torch.empty((S, k, cell), dtype=torch.uint8, device=dev)
             d.random_(0, 256, generator=g)
-            ps = [torch.empty((S, m, CELL), dtype=torch.uint8, device=dev) for _ in VARIANTS]
-            rs = [torch.empty((S, k, CELL), dtype=torch.uint8, device=dev) for _ in VARIANTS]
-            cases.append(dict(name=f"RS({k},{m}) x {S} set {si}", coder=coder, d=d, ps=ps, rs=rs, m=m,
-                              bytes=2 * (k + m) * S * CELL, t={v: [] for v, _ in VARIANTS}))
+            ps = [torch.empty((S, m, cell), dtype=torch.uint8, device=dev) for _ in VARIANTS]
+            rs = [torch.empty((S, k, cell), dtype=torch.uint8, device=dev) for _ in VARIANTS]
+            cases.append(dict(name=f"RS({k},{m}) {cell >> 10} KiB x {S} set {si}", coder=coder, d=d, ps=ps, rs=rs,
+                              m=m, bytes=2 * (k + m) * S * cell, t={v: [] for v, _ in VARIANTS}))
     torch.cuda.synchronize()
 
     def step(c, i, wq):
