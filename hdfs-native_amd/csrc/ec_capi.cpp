@@ -1527,8 +1527,10 @@ int hec_coder_prepare_decode(hec_coder_t* c, const uint8_t* present, int checksu
         const int pfd = hec::jit::pick_pfd(tn.jit_pfd, slabs, int(c->k), e);
         const int wpe = tn.fused_wpe == 3 && slabs == 4 ? 3 : 2;
         const int scheme = tn.crc_variant == 12 && kind == 0 ? 15 : 12;  // measurement: slicing-by-32 tail
-        const bool ok =
-            hec::jit::verify_kernel(c->device, int(c->k), e, kind, slabs, wpe, pfd, p.matrix.data(), true, &vk, scheme);
+        // the launch's choice (ec_fused.hip launch_fused; measurement: tune key 28)
+        const bool wq = (hec::kExperimental && tn.fused_wq) ? tn.fused_wq == 1 : hec::jit::default_wq(int(c->k), e);
+        const bool ok = hec::jit::verify_kernel(c->device, int(c->k), e, kind, slabs, wpe, pfd, p.matrix.data(), true,
+                                                &vk, scheme, wq);
         if (specialised) *specialised = ok ? 1 : 0;
         return int(HEC_OK);
     });
@@ -1548,7 +1550,8 @@ int hec_jit_warm(size_t data_units, size_t parity_units, const uint8_t* present,
         const size_t k = data_units;
         if (e == 0 || e > size_t(hec::kMaxR) || !(k == 2 || k == 3 || k == 6 || k == 10)) return int(HEC_ERR_INVALID_ARG);
         return hec::jit::warm(int(k), int(e), kind, hec::jit::default_slabs(int(k), int(e)), 2,
-                              hec::jit::default_pfd(int(k), int(e)), mat) ? int(HEC_OK)
+                              hec::jit::default_pfd(int(k), int(e)), mat, 12,
+                              hec::jit::default_wq(int(k), int(e))) ? int(HEC_OK)
                                                          : fail(HEC_ERR_DEVICE, "hiprtc compile", hipErrorNotSupported);
     });
 }

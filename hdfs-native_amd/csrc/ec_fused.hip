@@ -505,6 +505,7 @@ int launch_fused(const MatmulArgs& in, const FusedCrcArgs& cs, bool verify, int 
     // tile geometry below follows it
     jit::VerifyKernel vk;
     int use_slabs = slabs;
+    bool vwq = false;  // the specialised kernel takes the work queue (tune key 28 / jit::default_wq)
     if (verify && !split && (scheme == 12 || (scheme == 15 && cs.kind == crc::kCrc32c))) {
         uint8_t mat[kMaxR * kMaxK];
         for (int j = 0; j < a.r; j++)
@@ -513,10 +514,12 @@ int launch_fused(const MatmulArgs& in, const FusedCrcArgs& cs, bool verify, int 
         const int jp = jit::pick_pfd(tn.jit_pfd, js, a.k, a.r);
         // (3 waves per SIMD: tune key 16 = 3 with key 10 = 4; the launch's
         // `waves` and grid already follow wpe)
-        if (jit::verify_kernel(device, a.k, a.r, cs.kind, js, wpe, jp, mat, false, &vk, scheme)) use_slabs = js;
+        vwq = (kExperimental && tn.fused_wq) ? tn.fused_wq == 1 : jit::default_wq(a.k, a.r);
+        if (jit::verify_kernel(device, a.k, a.r, cs.kind, js, wpe, jp, mat, false, &vk, scheme, vwq)) use_slabs = js;
     }
     // Encode + CRC with the work queue of wave-tiles at k = 3 and 10; k = 6
-    // keeps the block tiles.  Same process and buffers, 2 sets x 5 alternated
+    // keeps the block tiles (decode + verify: the queue at every k,
+    // jit::default_wq).  Same process and buffers, 2 sets x 5 alternated
     // rounds (scripts/probe_fused_wq.py, profiles/r05z): RS(10,4) x 256
     // 0.675-0.683 of HBM peak vs 0.627-0.628, RS(3,2) x 1024 0.721-0.724 vs
     // 0.697-0.698, RS(6,3) x 1024 0.697-0.709 vs 0.703-0.712.  Tune key 28
@@ -537,6 +540,14 @@ int launch_fused(const MatmulArgs& in, const FusedCrcArgs& cs, bool verify, int 
             fn = f;
             wq = true;
         }
+    }
+    if (vk.fn && vwq) {
+        a.queue = stream_counters(device, stream);
+        if (a.queue)
+            wq = true;
+        else
+            vk.fn = nullptr;  // no counters: the generic kernel (below) instead
+        if (!vk.fn) use_slabs = slabs;
     }
     if (!fn && !vk.fn) return -1;
     const uint64_t chunks = a.cell_len / 16;
@@ -565,7 +576,7 @@ int launch_fused(const MatmulArgs& in, const FusedCrcArgs& cs, bool verify, int 
     // CRC 1.776 vs 1.803), 32 beats 8 by 1.5-2 % (r04o) and ties 16 (r04p;
     // 64: 1-2 % slower)
     uint64_t grid = tn.grid ? uint64_t(tn.grid) : uint64_t(num_cus(device)) * ((split || wpe == 3) ? 4 : 32);
-    if (wq && !tn.grid) grid = uint64_t(num_cus(device)) * 2;  // the resident blocks drain the queue
+    if (wq && !tn.grid) grid = uint64_t(num_cus(device)) * (wpe == 3 ? 1 : 2);  // the resident blocks drain the queue
     if (grid > total) grid = total;
     FusedCrcArgs c = cs;
     void* args[] = {&a, &c};

@@ -107,12 +107,14 @@ Mode mode() {
 struct Shape {
     int slabs, wpe, pfd;
     int scheme = 12;  // CRC lookup scheme: 12 (the fold + 11-bit tail), 15 (slicing-by-32 tail; CRC32C)
+    bool wq = false;  // tiles from the work queue of wave-tiles (work_queue.hpp)
 };
 
 std::string kernel_name(int k, int e, int kind, Shape sh) {
     return "hec::gf_fused_crc<" + std::to_string(k) + ", " + std::to_string(e) + ", " + std::to_string(sh.slabs) +
            ", " + std::to_string(sh.scheme) + ", " + std::to_string(kind) + ", true, " + std::to_string(sh.wpe) + ", " +
-           (sh.slabs == 4 ? "true" : "false") + ", hec::jit_plan::Net, " + std::to_string(sh.pfd) + ">";
+           (sh.slabs == 4 ? "true" : "false") + ", hec::jit_plan::Net, " + std::to_string(sh.pfd) +
+           (sh.wq ? ", true>" : ">");
 }
 
 bool shape_ok(int k, int e, int kind, Shape sh) {
@@ -125,7 +127,7 @@ bool shape_ok(int k, int e, int kind, Shape sh) {
 std::string entry_key(const std::string& arch, int k, int e, int kind, Shape sh, const uint8_t* matrix) {
     std::string key = arch + "/" + std::to_string(k) + "/" + std::to_string(e) + "/" + std::to_string(kind) + "/" +
                       std::to_string(sh.slabs) + "/" + std::to_string(sh.wpe) + "/" + std::to_string(sh.pfd) + "/" +
-                      std::to_string(sh.scheme) + "/";
+                      std::to_string(sh.scheme) + (sh.wq ? "/q/" : "/");
     key.append(reinterpret_cast<const char*>(matrix), size_t(e) * k);
     return key;
 }
@@ -358,8 +360,8 @@ Jit& jit() {
 }  // namespace
 
 bool verify_kernel(int device, int k, int e, int kind, int slabs, int wpe, int pfd, const uint8_t* matrix, bool wait,
-                   VerifyKernel* out, int scheme) {
-    const Shape sh{slabs, wpe, pfd, scheme};
+                   VerifyKernel* out, int scheme, bool wq) {
+    const Shape sh{slabs, wpe, pfd, scheme, wq};
     if (mode() == Mode::kOff || !shape_ok(k, e, kind, sh)) return false;
     if (!rtc().ok && cache_dir().empty()) return false;
     wait = wait || mode() == Mode::kSync;
@@ -431,8 +433,8 @@ bool verify_kernel(int device, int k, int e, int kind, int slabs, int wpe, int p
     return true;
 }
 
-bool warm(int k, int e, int kind, int slabs, int wpe, int pfd, const uint8_t* matrix, int scheme) {
-    const Shape sh{slabs, wpe, pfd, scheme};
+bool warm(int k, int e, int kind, int slabs, int wpe, int pfd, const uint8_t* matrix, int scheme, bool wq) {
+    const Shape sh{slabs, wpe, pfd, scheme, wq};
     if (!shape_ok(k, e, kind, sh)) return false;
     const std::string arch = device_arch(-1);  // no device: $HEC_JIT_ARCH or gfx950
     const std::string key = entry_key(arch, k, e, kind, sh, matrix);
@@ -480,6 +482,13 @@ void count_launch() { jit().launches++; }
 // 4 slabs with the inputs in pairs: RS(6,3) {0,1,2} 1.747-1.774 ms against
 // 1.804-1.809 at 8 slabs, same box, 3 alternations (profiles/r04h/)
 int default_slabs(int, int) { return 4; }
+// The specialised decode + verify takes the work queue of wave-tiles (round
+// 5).  Same process and buffers, decode of data 0..m-1 + verify of the k
+// survivors, 2 sets x 5 alternated rounds (scripts/probe_fused_wq.py,
+// profiles/r05af): RS(6,3) x 1024 0.728-0.740 of HBM peak vs 0.685-0.725 in
+// block tiles, RS(10,4) x 256 0.667-0.669 vs 0.619-0.620, RS(3,2) x 1024
+// 0.691-0.701 vs 0.648-0.674.
+bool default_wq(int, int) { return true; }
 int default_pfd(int, int) { return 1; }
 
 int pick_pfd(int key, int slabs, int k, int e) {

@@ -48,8 +48,13 @@ struct VerifyKernel {
 // pfd = load schedule (1 default; measurement shapes: pick_pfd).
 // scheme = the CRC lookup scheme (12 default; 15 = slicing-by-32 tail,
 // CRC32C only, measurement build)
+// wq = tiles from the work queue of wave-tiles (work_queue.hpp): the
+// launch then needs a.queue and the per-wave tile geometry (ec_fused.hip)
 bool verify_kernel(int device, int k, int e, int kind, int slabs, int wpe, int pfd, const uint8_t* matrix, bool wait,
-                   VerifyKernel* out, int scheme = 12);
+                   VerifyKernel* out, int scheme = 12, bool wq = false);
+// whether the specialised decode + verify of (k, e) takes the work queue
+// (launch and prepare must agree: ec_fused.hip, hec_coder_prepare_decode)
+bool default_wq(int k, int e);
 int default_slabs(int k, int e);
 int default_pfd(int k, int e);
 // the pfd a measurement-build tune key 24 value asks for at this slab count
@@ -59,7 +64,7 @@ int pick_pfd(int key, int slabs, int k, int e);
 // Compiles (or loads from the disk cache) the specialised kernel's code
 // object without a device: warms the caches ahead of use.  False when the
 // shape is not covered or the compile failed.
-bool warm(int k, int e, int kind, int slabs, int wpe, int pfd, const uint8_t* matrix, int scheme = 12);
+bool warm(int k, int e, int kind, int slabs, int wpe, int pfd, const uint8_t* matrix, int scheme = 12, bool wq = false);
 
 // Counters for tests and the bench line: kernels compiled (or loaded from
 // the disk cache), compiles failed, launches that used a specialised kernel.

@@ -1,6 +1,9 @@
 """Measurement probe (GPU box): the fused encode + CRC32C kernel with its
 block tiles (tune key 28 = 2; the default at k = 6) against the work queue
-of wave-tiles (key 28 = 1; the default at k = 3 and 10), measurement build.  Same process, same buffers, rounds
+of wave-tiles (key 28 = 1; the default at k = 3 and 10), measurement build;
+and the plan-specialised decode {0..m-1} + verify the same two ways (key 28
+= 1 compiles its work-queue form, the default since round 5; 2 its block-tile
+form).  Same process, same buffers, rounds
 alternated, HIP events around REPS back-to-back launches (median), two fresh
 buffer sets per config; parity and sums checked equal.
   python3 scripts/probe_fused_wq.py
@@ -45,8 +48,14 @@ def main():
                 sums = torch.empty((S, k + m, nck, 4), dtype=torch.uint8, device=dev)
                 pp, ps = H.stripe_layout_ptrs(p, m)
                 outs.append((p, sums, pp, ps))
+            rec = torch.empty((S, m, CELL), dtype=torch.uint8, device=dev)
+            rp, rsd = H.stripe_layout_ptrs(rec, m)
+            bad = torch.zeros((S, k + m), dtype=torch.uint8, device=dev)
             cases.append(dict(name=f"RS({k},{m}) x {S} set {si}", coder=coder, d=d, dp=dp, ds=ds, outs=outs, S=S,
-                              bytes=(k + m) * S * CELL + 4 * nck * (k + m) * S, t={v: [] for v, _ in VARIANTS}))
+                              k=k, m=m, rec=rec, rp=rp, rsd=rsd, bad=bad,
+                              bytes=(k + m) * S * CELL + 4 * nck * (k + m) * S,
+                              vbytes=(k + m) * S * CELL + 4 * nck * k * S,
+                              t={v: [] for v, _ in VARIANTS}, tv={v: [] for v, _ in VARIANTS}))
     torch.cuda.synchronize()
 
     def run(c, i, wq):
@@ -55,10 +64,33 @@ def main():
         c["coder"].encode_crc_device(c["dp"], c["ds"], pp, ps, CELL, c["S"], 512, sums.data_ptr(), sp)
         H.tune_set(28, 0, lib)
 
+    def run_verify(c, wq):
+        # decode data 0..m-1 + verify the k survivors against the sums the
+        # default encode + CRC wrote (outs[0]); rebuilt rows into rec
+        k, m = c["k"], c["m"]
+        p, sums, pp, ps = c["outs"][0]
+        surv = [None] * m + c["dp"][m:] + pp
+        out = [c["rp"][i] if i < m else c["dp"][i] for i in range(k)]
+        ost = [c["rsd"][0] if i < m else c["ds"][i] for i in range(k)]
+        H.tune_set(28, wq, lib)
+        c["coder"].decode_verify_device(H.CHECKSUM_CRC32C, surv, c["ds"] + ps, out, ost, CELL, c["S"], 512,
+                                        sums.data_ptr(), c["bad"].data_ptr(), sp)
+        H.tune_set(28, 0, lib)
+
     for c in cases:
+        for _, wq in VARIANTS:  # compile both specialised decode + verify kernels now
+            H.tune_set(28, wq, lib)
+            assert c["coder"].prepare_decode(list(range(c["m"])), H.CHECKSUM_CRC32C)
+            H.tune_set(28, 0, lib)
         for i, (_, wq) in enumerate(VARIANTS):
             run(c, i, wq)
         torch.cuda.synchronize()
+        for _, wq in VARIANTS:
+            c["rec"].zero_()
+            run_verify(c, wq)
+            torch.cuda.synchronize()
+            assert torch.equal(c["rec"], c["d"][:, :c["m"]]), (c["name"], "rebuilt", wq)
+            assert not bool(c["bad"].any()), (c["name"], "flagged", wq)
         for i in range(1, len(VARIANTS)):
             assert torch.equal(c["outs"][i][0], c["outs"][0][0]), (c["name"], "parity")
             assert torch.equal(c["outs"][i][1], c["outs"][0][1]), (c["name"], "sums")
@@ -73,11 +105,21 @@ def main():
                 b.record(stream)
                 torch.cuda.synchronize()
                 c["t"][v].append(a.elapsed_time(b) / REPS)
+                run_verify(c, wq)
+                a.record(stream)
+                for _ in range(REPS):
+                    run_verify(c, wq)
+                b.record(stream)
+                torch.cuda.synchronize()
+                c["tv"][v].append(a.elapsed_time(b) / REPS)
     for c in cases:
         parts = []
         for v, ts in c["t"].items():
             med = statistics.median(ts)
-            parts.append(f"{v} {med:.4f} ms ({c['bytes'] / (med * 1e-3) / 8e12:.3f})")
+            parts.append(f"enc+crc {v} {med:.4f} ms ({c['bytes'] / (med * 1e-3) / 8e12:.3f})")
+        for v, ts in c["tv"].items():
+            med = statistics.median(ts)
+            parts.append(f"dec+verify {v} {med:.4f} ms ({c['vbytes'] / (med * 1e-3) / 8e12:.3f})")
         print(f"{c['name']:22s} " + "  ".join(parts), flush=True)
 
 

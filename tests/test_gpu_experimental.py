@@ -330,6 +330,15 @@ JIT_SHAPE_CASES = [
     (6, 3, (1 << 15) + 512, (0, 1, 2), [(25, 1)], H.CHECKSUM_CRC32C),
     (10, 4, (1 << 16) + 512, (0, 3), [(25, 7)], H.CHECKSUM_CRC32),
     (6, 3, (1 << 16) + 512, (2,), [(25, 5), (24, 3), (10, 8)], H.CHECKSUM_CRC32C),
+    # tune key 28 = 1: the specialised kernel on the work queue of wave-tiles
+    (6, 3, (1 << 15) + 512, (0, 1, 2), [(28, 1)], H.CHECKSUM_CRC32C),
+    (6, 3, 1 << 15, (1,), [(28, 1)], H.CHECKSUM_CRC32),
+    (10, 4, (1 << 14) + 512, (0, 1, 2, 3), [(28, 1)], H.CHECKSUM_CRC32C),
+    (10, 4, (1 << 16) + 512, (0, 5), [(28, 1)], H.CHECKSUM_CRC32),
+    (3, 2, 8192 + 512, (0, 1), [(28, 1)], H.CHECKSUM_CRC32C),
+    (2, 1, 8192, (0,), [(28, 1)], H.CHECKSUM_CRC32C),
+    (6, 3, (1 << 15) + 512, (0, 2), [(28, 1), (16, 3), (10, 4)], H.CHECKSUM_CRC32C),
+    (6, 3, (1 << 15) + 512, (0, 1, 2), [(28, 1), (24, 5)], H.CHECKSUM_CRC32C),
 ]
 
 
