@@ -297,8 +297,17 @@ const void* encode_bsl(bool bsl) {
 // the default bit-sliced shape; the product compiles it for k = 3 and 10
 // (launch_fused: the k it wins at)
 template <int K, int R>
-const void* encode_wq_fn() {
+const void* encode_wq_fn(int slabs = 0) {
     constexpr int SL = fused_slabs(K, R);
+#ifdef HEC_EXPERIMENTAL
+    // measurement: 4 slabs with the inputs in pairs where the default is 8
+    // (tune keys 28 = 1, 10 = 4)
+    if constexpr (bsl_shape<K, R>() && SL == 8)
+        if (slabs == 4)
+            return reinterpret_cast<const void*>(
+                &gf_fused_crc<K, R, 4, 12, crc::kCrc32c, false, 2, true, RsNet<K, R>, 1, true>);
+#endif
+    (void)slabs;
     if constexpr (bsl_shape<K, R>() && (kExperimental || K != 6))
         return reinterpret_cast<const void*>(
             &gf_fused_crc<K, R, SL, 12, crc::kCrc32c, false, 2, SL == 4, RsNet<K, R>, 1, true>);
@@ -526,13 +535,14 @@ int launch_fused(const MatmulArgs& in, const FusedCrcArgs& cs, bool verify, int 
     // (measurement build): 1 = the queue at k = 3, 6, 10; 2 = block tiles.
     bool wq = false;
     const bool wq_want = kExperimental && tn.fused_wq ? tn.fused_wq == 1 : (a.k == 3 || a.k == 10);
-    if (wq_want && !verify && !split && fn && scheme == 12 && wpe == 2 && !vk.fn && slabs == fused_slabs(a.k, a.r) &&
+    const bool wq_shape = slabs == fused_slabs(a.k, a.r) || (kExperimental && slabs == 4);
+    if (wq_want && !verify && !split && fn && scheme == 12 && wpe == 2 && !vk.fn && wq_shape &&
         rs_parity_matrix(a) && tn.fused_bsl != 1) {
         const void* f = nullptr;
         switch (a.k * 16 + a.r) {
-            case 3 * 16 + 2: f = encode_wq_fn<3, 2>(); break;
-            case 6 * 16 + 3: f = encode_wq_fn<6, 3>(); break;
-            case 10 * 16 + 4: f = encode_wq_fn<10, 4>(); break;
+            case 3 * 16 + 2: f = encode_wq_fn<3, 2>(slabs); break;
+            case 6 * 16 + 3: f = encode_wq_fn<6, 3>(slabs); break;
+            case 10 * 16 + 4: f = encode_wq_fn<10, 4>(slabs); break;
             default: break;
         }
         a.queue = f ? stream_counters(device, stream) : nullptr;

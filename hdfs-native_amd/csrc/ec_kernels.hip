@@ -1015,21 +1015,22 @@ const void* wq_vec(int k, int r) {
     }
 }
 #ifdef HEC_EXPERIMENTAL
-// measurement: k = 10 in 256-thread blocks (key 4 = 256, key 1 = 2) on the queue
-template <int WQ>
+// measurement: k = 10 in 256-thread blocks (key 4 = 256, key 1 = 2 or 4) on the queue
+template <int WQ, int U>
 const void* wq_vec_k10_256(int r) {
     switch (r) {
-        case 1: return reinterpret_cast<const void*>(&gf_matmul_v16<10, 1, 2, true, 256, WQ>);
-        case 2: return reinterpret_cast<const void*>(&gf_matmul_v16<10, 2, 2, true, 256, WQ>);
-        case 3: return reinterpret_cast<const void*>(&gf_matmul_v16<10, 3, 2, true, 256, WQ>);
-        default: return reinterpret_cast<const void*>(&gf_matmul_v16<10, 4, 2, true, 256, WQ>);
+        case 1: return reinterpret_cast<const void*>(&gf_matmul_v16<10, 1, U, true, 256, WQ>);
+        case 2: return reinterpret_cast<const void*>(&gf_matmul_v16<10, 2, U, true, 256, WQ>);
+        case 3: return reinterpret_cast<const void*>(&gf_matmul_v16<10, 3, U, true, 256, WQ>);
+        default: return reinterpret_cast<const void*>(&gf_matmul_v16<10, 4, U, true, 256, WQ>);
     }
 }
 #endif
 
-const void* pick_wq(int k, int r, int wq, int block = 0) {
+const void* pick_wq(int k, int r, int wq, int block = 0, int unroll = 0) {
 #ifdef HEC_EXPERIMENTAL
-    if (k == 10 && block == 256) return wq == 2 ? wq_vec_k10_256<2>(r) : wq_vec_k10_256<1>(r);
+    if (k == 10 && block == 256 && unroll == 4) return wq_vec_k10_256<1, 4>(r);
+    if (k == 10 && block == 256) return wq == 2 ? wq_vec_k10_256<2, 2>(r) : wq_vec_k10_256<1, 2>(r);
     return wq == 2 ? wq_vec<2>(k, r) : wq_vec<1>(k, r);
 #else
     (void)block;
@@ -1205,12 +1206,12 @@ int launch_gf_matmul(const MatmulArgs& in, int device, hipStream_t stream) {
         // the register kernel's default shapes take the work queue (tune key
         // 27, measurement build: 1 / 2 rounds per atomic, 3 = the fixed order)
         int wq = 0;
-        const bool k10_256 = kExperimental && a.k == 10 && sh.block == 256 && sh.unroll == 2;  // measurement shape
+        const bool k10_256 = kExperimental && a.k == 10 && sh.block == 256 && (sh.unroll == 2 || sh.unroll == 4);  // measurement
         if (!fn && !sh.dma && sh.nt &&
             ((sh.unroll == (sh.block == 512 ? 2 : 4) && (sh.block == 512) == (a.k == 10)) || k10_256)) {
             wq = default_wq(a.k);
             if (kExperimental && tn.matmul_wq) wq = tn.matmul_wq == 3 ? 0 : tn.matmul_wq;
-            const void* f = wq ? pick_wq(a.k, a.r, wq, sh.block) : nullptr;
+            const void* f = wq ? pick_wq(a.k, a.r, wq, sh.block, sh.unroll) : nullptr;
             a.queue = f ? stream_counters(device, stream) : nullptr;
             if (a.queue) {
                 fn = f;

@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 5: RS(10,4) register kernel shapes on the work queue
 set -o pipefail
-out=gpurun_out/r05ab
+out=gpurun_out/r05ah
 mkdir -p $out
 export TMPDIR=/tmp
 timeout -k 10 600 python3 -u -m pytest tests/test_gpu_experimental.py -m gpu -x -q --timeout 300 --timeout-method thread \

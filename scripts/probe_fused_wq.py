@@ -25,6 +25,12 @@ SETS = int(os.environ.get("PROBE_SETS", "2"))
 ROUNDS = int(os.environ.get("PROBE_ROUNDS", "5"))
 REPS = int(os.environ.get("PROBE_REPS", "6"))
 VARIANTS = [("block tiles", 2), ("queue", 1)]
+# PROBE_ENC4=1: encode + CRC only, adds the queue at 4 slabs with input pairs
+# (tune keys 28 = 1, 10 = 4) where the default is 8 slabs
+ENC4 = os.environ.get("PROBE_ENC4") == "1"
+if ENC4:
+    VARIANTS = [("block tiles", [(28, 2)]), ("queue", [(28, 1)]), ("queue 4 slabs", [(28, 1), (10, 4)]),
+                ("block 4 slabs", [(28, 2), (10, 4)])]
 
 
 def main():
@@ -60,9 +66,12 @@ def main():
 
     def run(c, i, wq):
         p, sums, pp, ps = c["outs"][i]
-        H.tune_set(28, wq, lib)
+        pairs = wq if isinstance(wq, list) else [(28, wq)]
+        for key, val in pairs:
+            H.tune_set(key, val, lib)
         c["coder"].encode_crc_device(c["dp"], c["ds"], pp, ps, CELL, c["S"], 512, sums.data_ptr(), sp)
-        H.tune_set(28, 0, lib)
+        for key, _ in pairs:
+            H.tune_set(key, 0, lib)
 
     def run_verify(c, wq):
         # decode data 0..m-1 + verify the k survivors against the sums the
@@ -77,6 +86,30 @@ def main():
                                         sums.data_ptr(), c["bad"].data_ptr(), sp)
         H.tune_set(28, 0, lib)
 
+    if ENC4:
+        for c in cases:
+            for i, (_, wq) in enumerate(VARIANTS):
+                run(c, i, wq)
+            torch.cuda.synchronize()
+            for i in range(1, len(VARIANTS)):
+                assert torch.equal(c["outs"][i][0], c["outs"][0][0]), (c["name"], "parity")
+                assert torch.equal(c["outs"][i][1], c["outs"][0][1]), (c["name"], "sums")
+        for _ in range(ROUNDS):
+            for c in cases:
+                for i, (v, wq) in enumerate(VARIANTS):
+                    run(c, i, wq)
+                    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    a.record(stream)
+                    for _ in range(REPS):
+                        run(c, i, wq)
+                    b.record(stream)
+                    torch.cuda.synchronize()
+                    c["t"][v].append(a.elapsed_time(b) / REPS)
+        for c in cases:
+            print(f"{c['name']:22s} " + "  ".join(
+                f"{v} {statistics.median(ts):.4f} ms ({c['bytes'] / (statistics.median(ts) * 1e-3) / 8e12:.3f})"
+                for v, ts in c["t"].items()), flush=True)
+        return
     for c in cases:
         for _, wq in VARIANTS:  # compile both specialised decode + verify kernels now
             H.tune_set(28, wq, lib)

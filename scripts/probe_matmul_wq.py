@@ -39,8 +39,8 @@ if C64K:
 K10 = os.environ.get("PROBE_K10") == "1"
 if K10:
     CONFIGS = [(10, 4, 256), (10, 4, 1024)]
-    VARIANTS = [("512 x1/CU", [(27, 1)]), ("256 x1/CU", [(27, 1), (4, 256), (1, 2)]),
-                ("256 x2/CU", [(27, 1), (4, 256), (1, 2), (3, 2)]), ("fixed 512 x8/CU", [(27, 3)])]
+    VARIANTS = [("512 x1/CU", [(27, 1)]), ("256 U4 x1/CU", [(27, 1), (4, 256), (1, 4)]),
+                ("256 U4 x2/CU", [(27, 1), (4, 256), (1, 4), (3, 2)]), ("256 x2/CU", [(27, 1), (4, 256), (1, 2), (3, 2)])]
 
 
 def main():
