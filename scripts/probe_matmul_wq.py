@@ -34,6 +34,17 @@ if C64K:
         CONFIGS = [(6, 3, int(x.split(":")[1]), int(x.split(":")[0])) for x in os.environ["PROBE_CELLS"].split(",")]
         SETS = 1
     VARIANTS = [("LDS-DMA", [(5, 0)]), ("register queue", [(5, 1)]), ("register fixed", [(5, 1), (27, 3)])]
+# PROBE_BPC=1: RS(6,3) / RS(3,2) on the queue at 1 block per CU (the default)
+# against 2 (key 3 = 2: two waves per SIMD)
+if os.environ.get("PROBE_BPC") == "1":
+    CONFIGS = [(6, 3, 1024), (3, 2, 1024)]
+    VARIANTS = [("queue 1/CU", [(27, 0)]), ("queue 2/CU", [(27, 0), (3, 2)]), ("queue x2 2/CU", [(27, 2), (3, 2)])]
+# PROBE_GROUP=1: the tile-order group (tune key 8: stripes interleaved
+# column-major; default 4) on the queue
+if os.environ.get("PROBE_GROUP") == "1":
+    CONFIGS = [(6, 3, 1024), (10, 4, 256)]
+    VARIANTS = [("group 4", [(27, 0)]), ("group 1", [(27, 0), (8, 1)]), ("group 2", [(27, 0), (8, 2)]),
+                ("group 8", [(27, 0), (8, 8)]), ("group 16", [(27, 0), (8, 16)])]
 # PROBE_K10=1: RS(10,4) only, its 512-thread shape against 256-thread blocks
 # (tune keys 4 = 256, 1 = 2) at 1 and 2 blocks per CU (key 3), all on the queue
 K10 = os.environ.get("PROBE_K10") == "1"
