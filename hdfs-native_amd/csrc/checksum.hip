@@ -79,6 +79,8 @@ __device__ __forceinline__ void emit_sum(const CrcArgs& a, uint64_t cell_idx, ui
     const uint64_t at = cell * a.chunks_per_cell + chunk;
     if (a.expected) {
         if (reinterpret_cast<const uint32_t*>(a.expected)[at] != bswap32(crc)) a.bad[cell] = 1;
+    } else if (a.sums_nt) {
+        __builtin_nontemporal_store(bswap32(crc), reinterpret_cast<uint32_t*>(a.out) + at);
     } else {
         reinterpret_cast<uint32_t*>(a.out)[at] = bswap32(crc);
     }
@@ -476,12 +478,14 @@ const void* crc_pick(int scheme, int pf) {
     }
 #endif
 #ifdef HEC_EXPERIMENTAL
-    // the fold with the work queue (tune key 29 = 1 / 2 / 4 tasks per unit)
+    // the fold with the work queue (tune key 29 = 1 / 2 / 4 / 8 / 16 tasks per unit)
     if (scheme == 12 && pf < 0) {
         if constexpr (KIND == crc::kCrc32c) {
             if (pf == -1) return reinterpret_cast<const void*>(&checksum_chunks512<KIND, 12, 1, 1>);
             if (pf == -2) return reinterpret_cast<const void*>(&checksum_chunks512<KIND, 12, 1, 2>);
             if (pf == -4) return reinterpret_cast<const void*>(&checksum_chunks512<KIND, 12, 1, 4>);
+            if (pf == -8) return reinterpret_cast<const void*>(&checksum_chunks512<KIND, 12, 1, 8>);
+            if (pf == -16) return reinterpret_cast<const void*>(&checksum_chunks512<KIND, 12, 1, 16>);
         }
         return nullptr;
     }
@@ -521,6 +525,7 @@ int launch_checksum(const CrcArgs& in, int device, hipStream_t stream) {
         aligned &= ((reinterpret_cast<uintptr_t>(a.base[i]) | a.stride[i]) & 15u) == 0;
     const int cus = num_cus(device);
     const Tune tn = tune_snapshot();
+    a.sums_nt = tn.crc_sums_nt == 1 ? 1u : 0u;  // measurement (key 30)
     void* args[] = {&a};
     hipError_t e;
     if (aligned && a.bytes_per_checksum == 512) {

@@ -39,6 +39,7 @@ struct CrcArgs {
     uint64_t chunks_per_cell;  // filled by the launcher
     uint64_t groups_per_cell;  // filled by the launcher (fast path)
     uint32_t* queue;           // work-queue variant (measurement build, key 29): the stream's launch counters
+    uint32_t sums_nt;          // compute mode: non-temporal sum stores (measurement build, key 30)
 };
 
 // 0 ok, -1 invalid sizes, >0 hipError_t.
@@ -55,6 +56,7 @@ struct FusedCrcArgs {
     uint32_t n_total;         // shards per stripe in the sums layout (k + m)
     int32_t kind;             // crc::Kind
     uint8_t shard_id[64];     // sums index of launch input i (verify: survivor shard ids) / output K + j
+    uint32_t sums_nt;         // encode: non-temporal sum stores (measurement build, key 30)
 };
 
 // Fused encode + CRC32C of all k inputs and r outputs per 512-B chunk.

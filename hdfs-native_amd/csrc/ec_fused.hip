@@ -589,6 +589,7 @@ int launch_fused(const MatmulArgs& in, const FusedCrcArgs& cs, bool verify, int 
     if (wq && !tn.grid) grid = uint64_t(num_cus(device)) * (wpe == 3 ? 1 : 2);  // the resident blocks drain the queue
     if (grid > total) grid = total;
     FusedCrcArgs c = cs;
+    c.sums_nt = tn.crc_sums_nt == 1 ? 1u : 0u;  // measurement (key 30)
     void* args[] = {&a, &c};
     if (vk.fn) {
         jit::count_launch();

@@ -232,7 +232,10 @@ __global__ __launch_bounds__(crcdev::sliced(SCHEME) ? 128 * WPE * (WPE - 1) : 51
                 if constexpr (VERIFY) {
                     if (be != want) cs.bad[sum_cell(first)] = 1;
                 } else {
-                    out_sums[sum_cell(first) * nck + cbyte / 512] = be;
+                    if (cs.sums_nt)
+                        __builtin_nontemporal_store(be, out_sums + sum_cell(first) * nck + cbyte / 512);
+                    else
+                        out_sums[sum_cell(first) * nck + cbyte / 512] = be;
                 }
             }
             __builtin_amdgcn_wave_barrier();

@@ -50,7 +50,8 @@ struct Tune {
     int jit_pfd = 0;            // key 24: fused load schedule (0 default, 2 = two pairs ahead at 4 slabs, 3 = early issue at 8, 4 = sums per tile, 5 = early outputs)
     int matmul_wq = 0;          // key 27: register kernel's work queue of wave-tiles (0 = default: 2 rounds per atomic for k <= 3, 1 for k = 6, 10; 1 / 2 forced; 3 = the fixed tile order)
     int fused_wq = 0;           // key 28: fused kernels' work queue (0 = default: encode + CRC at k = 3, 10, decode + verify at every k; 1 = everywhere; 2 = block tiles)
-    int crc_wq = 0;             // key 29: CRC32C checksum kernel with the work queue (0 = off; 1 / 2 / 4 tasks per unit)
+    int crc_wq = 0;             // key 29: CRC32C checksum kernel with the work queue (0 = off; 1 / 2 / 4 / 8 / 16 tasks per unit)
+    int crc_sums_nt = 0;        // key 30: 1 = the CRC kernels store the sums non-temporal (measurement)
     int mixed_wq = 0;           // key 26: mixed decode work queue of wave-tiles (0 = default: 1 round of wave-tiles per atomic for k >= 6, 4 below; 1 / 2 / 4 forced; 3 = the fixed tile order)
 };
 

@@ -2,7 +2,7 @@
 # round 5: CRC32C checksum kernel on the work queue (tune key 29) -- parity
 # of the variants, then the same-buffer A/B on the bench layouts
 set -o pipefail
-out=gpurun_out/r05aa
+out=gpurun_out/r05am
 mkdir -p $out
 export TMPDIR=/tmp
 timeout -k 10 600 python3 -u -m pytest tests/test_gpu_experimental.py -m gpu -x -q --timeout 300 --timeout-method thread \

@@ -31,6 +31,11 @@ ENC4 = os.environ.get("PROBE_ENC4") == "1"
 if ENC4:
     VARIANTS = [("block tiles", [(28, 2)]), ("queue", [(28, 1)]), ("queue 4 slabs", [(28, 1), (10, 4)]),
                 ("block 4 slabs", [(28, 2), (10, 4)])]
+# PROBE_NT=1: encode + CRC only, the sums stored non-temporal (tune key 30)
+if os.environ.get("PROBE_NT") == "1":
+    ENC4 = True
+    CONFIGS = [(6, 3, 1024)]
+    VARIANTS = [("default", [(28, 0)]), ("sums nt", [(30, 1)]), ("queue sums nt", [(28, 1), (30, 1)])]
 
 
 def main():

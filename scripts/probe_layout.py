@@ -10,8 +10,9 @@ Kernels: checksum_chunks512 (CRC32C of all k+m cells), gf_matmul_v16
 (encode), the fused encode + CRC32C and the plan-specialised fused decode
 {0,1,2} + verify.  Prints one line per (layout, set).
 PROBE_CRC_AB=1: the measurement build instead, CRC32C of all k+m cells by the
-default register-staged kernel and by the same kernel on the work queue (tune
-key 29 = 1 / 2 / 4 tasks per unit), compute and verify mode, same buffers,
+default register-staged kernel, the same with non-temporal sum stores (tune
+key 30 = 1) and on the work queue (key 29 = 4 tasks per unit), compute and
+verify mode, same buffers,
 rounds alternated; PROBE_CRC_DMA=1 adds the LDS-DMA kernel (key 11 = 13;
 profiles/r05n ran it with the DMA kernel as the default and the register one
 on the key: the same kernels).
@@ -118,8 +119,8 @@ def main():
                 coder.checksum_verify_device(H.CHECKSUM_CRC32C, cells, cstr, CELL, S, BPC, st["sums"].data_ptr(),
                                              st["bad"].data_ptr(), sp)
 
-            kernels[(lay, i)] = {"crc_reg": crc, "crc_wq1": tuned(crc, 1, 29), "crc_wq2": tuned(crc, 2, 29),
-                                 "crc_wq4": tuned(crc, 4, 29), "verify_reg": ver, "verify_wq2": tuned(ver, 2, 29)}
+            kernels[(lay, i)] = {"crc_reg": crc, "crc_wq4": tuned(crc, 4, 29), "crc_wq8": tuned(crc, 8, 29),
+                                 "crc_wq16": tuned(crc, 16, 29), "verify_reg": ver, "verify_wq8": tuned(ver, 8, 29)}
             if os.environ.get("PROBE_CRC_DMA") == "1":
                 kernels[(lay, i)].update({"crc_dma": tuned(crc, 13), "verify_dma": tuned(ver, 13)})
             continue
@@ -141,7 +142,7 @@ def main():
     algo = {"crc_only": (K + M) * CELL * S + 4 * NCH * (K + M) * S, "encode": (K + M) * CELL * S,
             "encode_crc": (K + M) * CELL * S + 4 * NCH * (K + M) * S,
             "decode_verify": (K + len(MISS)) * CELL * S + 4 * NCH * K * S}
-    for n in ("crc_dma", "crc_reg", "verify_dma", "verify_reg", "crc_wq1", "crc_wq2", "crc_wq4", "verify_wq2"):
+    for n in ("crc_dma", "crc_reg", "verify_dma", "verify_reg", "crc_wq1", "crc_wq2", "crc_wq4", "verify_wq2", "crc_nt", "crc_wq8", "crc_wq16", "verify_wq8"):
         algo[n] = algo["crc_only"]
     for key, per in times.items():
         parts = []

@@ -145,7 +145,7 @@ def test_crc_schemes_vs_oracle(xlib, dev, ctype, cell, bpc, n, variant, pf):
 
 
 @pytest.mark.parametrize("cell,bpc,n", [c for c in P.CRC32C_CASES if c[1] == 512])
-@pytest.mark.parametrize("wq", [1, 2, 4])
+@pytest.mark.parametrize("wq", [1, 2, 4, 8, 16])
 def test_crc_wq_vs_oracle(xlib, dev, cell, bpc, n, wq):
     """Tune key 29: the CRC32C fold kernel on the work queue, 1 / 2 / 4 tasks
     per unit (partial last tasks, short last chunks, units that run past the
@@ -153,7 +153,7 @@ def test_crc_wq_vs_oracle(xlib, dev, cell, bpc, n, wq):
     P.crc32c_body(dev, cell, bpc, n, P.coder(6, 3, xlib), [(29, wq)], xlib)
 
 
-@pytest.mark.parametrize("wq", [1, 2, 4])
+@pytest.mark.parametrize("wq", [1, 4, 16])
 def test_crc_wq_full_size_compute_and_verify(xlib, dev, wq):
     """Key 29 at full size (9 x 1 MiB x 64 cells), three launches in a row
     on one stream (the counters must come back to zero): sums equal the
@@ -451,7 +451,7 @@ def test_tune_set_concurrent_with_launches(xlib, dev, c_oracle):
 
 
 def test_tune_set_rejects_unknown_values(xlib):
-    for key, value in [(3, 99), (1, 5), (5, 6), (11, 8), (16, 1), (17, 6), (19, 3), (20, 3), (21, 4), (22, 2), (23, 2), (24, 6), (25, 4097), (26, 5), (27, 4), (28, 3), (29, 3), (30, 0), (0, 0)]:
+    for key, value in [(3, 99), (1, 5), (5, 6), (11, 8), (16, 1), (17, 6), (19, 3), (20, 3), (21, 4), (22, 2), (23, 2), (24, 6), (25, 4097), (26, 5), (27, 4), (28, 3), (29, 3), (30, 2), (31, 0), (0, 0)]:
         with pytest.raises(ValueError):
             H.tune_set(key, value, xlib)
 
