@@ -957,8 +957,8 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
             "traffic_source": traffic_src,
-            "kernel": f"gf_matmul_v16<{k},{m}> (encode and decode launches)" if cell > (256 << 10) else
-                      f"gf_matmul_dma<{k},{m}> (encode and decode launches)",
+            "kernel": (f"gf_matmul_v16<{k},{m}> (encode and decode launches; work queue of wave-tiles)"
+                       if k in (2, 3, 6, 10) else f"gf_matmul_v16<{k},{m}> (encode and decode launches)"),
             "algorithmic_bytes_per_launch": algo_bytes,
             "avg_launch_ms": round(avg_launch_ms, 4),
             "frac_of_measured_copy": round(achieved / HBM_COPY_GBS, 4),
