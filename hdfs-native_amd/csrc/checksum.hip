@@ -118,7 +118,7 @@ struct CrcShape : crcdev::TableLayout<SCHEME> {
 // one unit per atomic; the next task is still loaded during this one.
 template <int KIND, int SCHEME, int PF, int WQ = 0>
 __global__ __launch_bounds__(CrcShape<SCHEME>::kBlock) void checksum_chunks512(CrcArgs a) {
-    static_assert(WQ == 0 || PF == 1, "the queue runs one task of prefetch");
+    static_assert(WQ == 0 || PF == 1, "the queue (and the runs, WQ < 0) run one task of prefetch");
     using Sh = CrcShape<SCHEME>;
     using Spec = crc::Spec<KIND>;
     constexpr bool REFL = Spec::kReflected;
@@ -194,6 +194,22 @@ __global__ __launch_bounds__(CrcShape<SCHEME>::kBlock) void checksum_chunks512(C
             const bool unit_end = (task % WQ) == WQ - 1 || task + 1 >= tasks;
             run_task(task, v, unit_end ? task_of(q.peek()) : task + 1);
             task = unit_end ? task_of(q.next()) : task + 1;
+        }
+        return;
+    }
+    if constexpr (WQ < 0) {
+        // measurement (tune key 31): fixed order in runs of -WQ consecutive
+        // tasks of one cell per wave, so a wave writes whole lines of sums
+        constexpr uint64_t SEQ = uint64_t(-WQ);
+        const uint64_t wstep = SEQ * step;
+        uint64_t task = (uint64_t(blockIdx.x) * Sh::kWaves + wave) * SEQ;
+        auto next_of = [&](uint64_t t) { return (t % SEQ) != SEQ - 1 ? t + 1 : t - (SEQ - 1) + wstep; };
+        u32x4 v[8];
+        if (task < tasks) load_task(a, groups, task, lane, v);
+        while (task < tasks) {
+            const uint64_t nt = next_of(task);
+            run_task(task, v, nt);
+            task = nt;
         }
         return;
     }
@@ -486,6 +502,10 @@ const void* crc_pick(int scheme, int pf) {
             if (pf == -4) return reinterpret_cast<const void*>(&checksum_chunks512<KIND, 12, 1, 4>);
             if (pf == -8) return reinterpret_cast<const void*>(&checksum_chunks512<KIND, 12, 1, 8>);
             if (pf == -16) return reinterpret_cast<const void*>(&checksum_chunks512<KIND, 12, 1, 16>);
+            if (pf == -102) return reinterpret_cast<const void*>(&checksum_chunks512<KIND, 12, 1, -2>);
+            if (pf == -104) return reinterpret_cast<const void*>(&checksum_chunks512<KIND, 12, 1, -4>);
+            if (pf == -108) return reinterpret_cast<const void*>(&checksum_chunks512<KIND, 12, 1, -8>);
+            if (pf == -116) return reinterpret_cast<const void*>(&checksum_chunks512<KIND, 12, 1, -16>);
         }
         return nullptr;
     }
@@ -578,6 +598,11 @@ int launch_checksum(const CrcArgs& in, int device, hipStream_t stream) {
         if (grid > cap) grid = cap;
         const void* fn = a.kind == crc::kCrc32c ? crc_pick<crc::kCrc32c>(scheme, pf) : crc_pick<crc::kCksum>(scheme, pf);
 #ifdef HEC_EXPERIMENTAL
+        // tune key 31: the fold kernel in runs of 2 / 4 consecutive tasks per wave
+        if (tn.crc_runs && scheme == 12 && a.kind == crc::kCrc32c && pf == 1) {
+            const void* f = crc_pick<crc::kCrc32c>(12, -100 - tn.crc_runs);
+            if (f) fn = f;
+        }
         // tune key 29: the fold kernel with the work queue, 1 / 2 / 4 tasks per
         // unit, the resident blocks only
         if (tn.crc_wq && scheme == 12 && a.kind == crc::kCrc32c && pf == 1 &&

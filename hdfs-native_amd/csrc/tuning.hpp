@@ -52,6 +52,7 @@ struct Tune {
     int fused_wq = 0;           // key 28: fused kernels' work queue (0 = default: encode + CRC at k = 3, 10, decode + verify at every k; 1 = everywhere; 2 = block tiles)
     int crc_wq = 0;             // key 29: CRC32C checksum kernel with the work queue (0 = off; 1 / 2 / 4 / 8 / 16 tasks per unit)
     int crc_sums_nt = 0;        // key 30: 1 = the CRC kernels store the sums non-temporal (measurement)
+    int crc_runs = 0;           // key 31: CRC32C checksum kernel in runs of 2 / 4 consecutive tasks per wave (measurement)
     int mixed_wq = 0;           // key 26: mixed decode work queue of wave-tiles (0 = default: 1 round of wave-tiles per atomic for k >= 6, 4 below; 1 / 2 / 4 forced; 3 = the fixed tile order)
 };
 

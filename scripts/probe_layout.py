@@ -119,8 +119,8 @@ def main():
                 coder.checksum_verify_device(H.CHECKSUM_CRC32C, cells, cstr, CELL, S, BPC, st["sums"].data_ptr(),
                                              st["bad"].data_ptr(), sp)
 
-            kernels[(lay, i)] = {"crc_reg": crc, "crc_wq4": tuned(crc, 4, 29), "crc_wq8": tuned(crc, 8, 29),
-                                 "crc_wq16": tuned(crc, 16, 29), "verify_reg": ver, "verify_wq8": tuned(ver, 8, 29)}
+            kernels[(lay, i)] = {"crc_reg": crc, "crc_runs4": tuned(crc, 4, 31), "crc_runs8": tuned(crc, 8, 31),
+                                 "crc_runs16": tuned(crc, 16, 31), "verify_reg": ver, "verify_runs8": tuned(ver, 8, 31)}
             if os.environ.get("PROBE_CRC_DMA") == "1":
                 kernels[(lay, i)].update({"crc_dma": tuned(crc, 13), "verify_dma": tuned(ver, 13)})
             continue
@@ -142,7 +142,7 @@ def main():
     algo = {"crc_only": (K + M) * CELL * S + 4 * NCH * (K + M) * S, "encode": (K + M) * CELL * S,
             "encode_crc": (K + M) * CELL * S + 4 * NCH * (K + M) * S,
             "decode_verify": (K + len(MISS)) * CELL * S + 4 * NCH * K * S}
-    for n in ("crc_dma", "crc_reg", "verify_dma", "verify_reg", "crc_wq1", "crc_wq2", "crc_wq4", "verify_wq2", "crc_nt", "crc_wq8", "crc_wq16", "verify_wq8"):
+    for n in ("crc_dma", "crc_reg", "verify_dma", "verify_reg", "crc_wq1", "crc_wq2", "crc_wq4", "verify_wq2", "crc_nt", "crc_wq8", "crc_wq16", "verify_wq8", "crc_runs2", "crc_runs4", "verify_runs2", "crc_runs8", "crc_runs16", "verify_runs8"):
         algo[n] = algo["crc_only"]
     for key, per in times.items():
         parts = []

@@ -153,6 +153,23 @@ def test_crc_wq_vs_oracle(xlib, dev, cell, bpc, n, wq):
     P.crc32c_body(dev, cell, bpc, n, P.coder(6, 3, xlib), [(29, wq)], xlib)
 
 
+@pytest.mark.parametrize("cell,bpc,n", [c for c in P.CRC32C_CASES if c[1] == 512])
+@pytest.mark.parametrize("runs", [2, 4, 8, 16])
+def test_crc_runs_vs_oracle(xlib, dev, cell, bpc, n, runs):
+    """Tune key 31: the CRC32C fold kernel in runs of 2 / 4 consecutive tasks
+    per wave, against the oracle, and at full size against the default."""
+    P.crc32c_body(dev, cell, bpc, n, P.coder(6, 3, xlib), [(31, runs)], xlib)
+    S, nn, c1 = 16, 9, 1 << 20
+    x = torch.empty((S, nn, c1), dtype=torch.uint8, device=dev)
+    x.random_(0, 256, generator=torch.Generator(device=dev).manual_seed(31 + runs))
+    c = xcoder(xlib, 6, 3)
+    want = H.crc32c_batch(c, x, 512)
+    with P.knobs([(31, runs)], xlib):
+        got = H.crc32c_batch(c, x, 512)
+        torch.cuda.synchronize()
+    assert torch.equal(got, want)
+
+
 @pytest.mark.parametrize("wq", [1, 4, 16])
 def test_crc_wq_full_size_compute_and_verify(xlib, dev, wq):
     """Key 29 at full size (9 x 1 MiB x 64 cells), three launches in a row
@@ -451,7 +468,7 @@ def test_tune_set_concurrent_with_launches(xlib, dev, c_oracle):
 
 
 def test_tune_set_rejects_unknown_values(xlib):
-    for key, value in [(3, 99), (1, 5), (5, 6), (11, 8), (16, 1), (17, 6), (19, 3), (20, 3), (21, 4), (22, 2), (23, 2), (24, 6), (25, 4097), (26, 5), (27, 4), (28, 3), (29, 3), (30, 2), (31, 0), (0, 0)]:
+    for key, value in [(3, 99), (1, 5), (5, 6), (11, 8), (16, 1), (17, 6), (19, 3), (20, 3), (21, 4), (22, 2), (23, 2), (24, 6), (25, 4097), (26, 5), (27, 4), (28, 3), (29, 3), (30, 2), (31, 3), (32, 0), (0, 0)]:
         with pytest.raises(ValueError):
             H.tune_set(key, value, xlib)
 
