@@ -30,8 +30,11 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <functional>
 #include <map>
 #include <mutex>
+#include <thread>
+#include <tuple>
 
 #include "bitslice.hpp"
 #include "ec_kernels.hpp"
@@ -1118,12 +1121,15 @@ Shape default_shape(int k, uint64_t cell_len) {
 // kMixedQueueStride apart, zero at rest (each launch leaves them zero, see
 // gf_matmul_v16), zeroed on the stream when first made.  Launches on one
 // stream run in order, so they share a set; launches on different streams
-// get different sets.  Never freed (2 KiB per stream that ever launched).
+// get different sets (hipStreamPerThread: one set per thread).  Never freed
+// (2 KiB per stream that ever launched).
 uint32_t* stream_counters(int device, hipStream_t stream) {
     static std::mutex mu;
-    static std::map<std::pair<int, uintptr_t>, uint32_t*> sets;
+    static std::map<std::tuple<int, uintptr_t, size_t>, uint32_t*> sets;
+    // hipStreamPerThread names a different stream in every thread
+    const size_t thread = stream == hipStreamPerThread ? std::hash<std::thread::id>()(std::this_thread::get_id()) : 0;
     std::lock_guard<std::mutex> lk(mu);
-    uint32_t*& c = sets[{device, reinterpret_cast<uintptr_t>(stream)}];
+    uint32_t*& c = sets[{device, reinterpret_cast<uintptr_t>(stream), thread}];
     if (!c) {
         const size_t bytes = size_t(kMixedQueues) * kMixedQueueStride;
         if (hipMalloc(reinterpret_cast<void**>(&c), bytes) != hipSuccess) {

@@ -3,7 +3,7 @@
 # the measurement build does not travel), smoke, the default bench line, and
 # the rocprofv3 kernel-trace summary of that same bench command
 set -o pipefail
-out=gpurun_out/r05final2
+out=gpurun_out/r05final3
 mkdir -p $out
 export TMPDIR=/tmp
 timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $out/tests.txt 2>&1

@@ -469,6 +469,45 @@ def test_work_queue_counters_reset_across_launches(dev, c_oracle):
             assert torch.equal(ps[i], want[i]), (rep, i)
 
 
+def test_work_queue_per_thread_default_stream(dev):
+    """hipStreamPerThread ((hipStream_t)2) is a different stream in every
+    thread: the work-queue counters are kept per thread for it, so threads
+    encoding at once on that handle never share a counter set."""
+    import threading
+    k, m, S, cell = 6, 3, 48, 1 << 20
+    ds = [_device_random((S, k, cell), dev, seed=70 + i) for i in range(4)]
+    want = []
+    for d in ds:
+        p = torch.empty((S, m, cell), dtype=torch.uint8, device=dev)
+        H.encode_batch(coder(k, m), d, p)
+        want.append(p)
+    torch.cuda.synchronize()
+    errors = []
+
+    def work(i):
+        try:
+            c = H.Coder(k, m, 0)
+            dp, dst = H.stripe_layout_ptrs(ds[i], k)
+            for _ in range(4):
+                p = torch.zeros((S, m, cell), dtype=torch.uint8, device=dev)
+                torch.cuda.synchronize()
+                pp, pst = H.stripe_layout_ptrs(p, m)
+                c.encode_device(dp, dst, pp, pst, cell, S, 2)  # hipStreamPerThread
+                torch.cuda.synchronize()  # every stream of the device, this thread's included
+                if not torch.equal(p, want[i]):
+                    errors.append(i)
+            c.close()
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    ts = [threading.Thread(target=work, args=(i,)) for i in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errors, errors
+
+
 def test_linearity(dev):
     k, m, S, cell = 6, 3, 16, 1 << 18
     a = _device_random((S, k, cell), dev, 1)
