@@ -184,8 +184,9 @@ __global__ __launch_bounds__(CrcShape<SCHEME>::kBlock) void checksum_chunks512(C
     if constexpr (WQ > 0) {
         // units of WQ tasks; the launcher keeps the unit count below 2^32
         const uint32_t units = uint32_t((tasks + WQ - 1) / WQ);
+        queue_zero_next(a.queue_zero);
         WaveQueue q;
-        q.init(a.queue, units, Sh::kWaves);
+        q.init(a.queue, units);
         auto task_of = [&](uint32_t u) { return u < units ? uint64_t(u) * WQ : tasks; };
         uint64_t task = task_of(q.next());
         u32x4 v[8];
@@ -548,6 +549,7 @@ int launch_checksum(const CrcArgs& in, int device, hipStream_t stream) {
     a.sums_nt = tn.crc_sums_nt == 1 ? 1u : 0u;  // measurement (key 30)
     void* args[] = {&a};
     hipError_t e;
+    QueueLease lease;  // work-queue counters (held until the launch is enqueued)
     if (aligned && a.bytes_per_checksum == 512) {
         a.groups_per_cell = (a.chunks_per_cell + 15) / 16;
         const uint64_t tasks = a.groups_per_cell * a.n_shards * a.stripes;
@@ -608,7 +610,9 @@ int launch_checksum(const CrcArgs& in, int device, hipStream_t stream) {
         if (tn.crc_wq && scheme == 12 && a.kind == crc::kCrc32c && pf == 1 &&
             (tasks + uint64_t(tn.crc_wq) - 1) / uint64_t(tn.crc_wq) < (uint64_t(1) << 32)) {
             const void* f = crc_pick<crc::kCrc32c>(12, -tn.crc_wq);
-            a.queue = f ? stream_counters(device, stream) : nullptr;
+            if (f) lease = queue_lease(device, stream);
+            a.queue = lease.use;
+            a.queue_zero = lease.zero;
             if (a.queue) {
                 fn = f;
                 grid = uint64_t(cus) * per_cu;
@@ -618,6 +622,7 @@ int launch_checksum(const CrcArgs& in, int device, hipStream_t stream) {
         }
 #endif
         e = hipLaunchKernel(fn, dim3(uint32_t(grid)), dim3(uint32_t(waves * 64)), args, 0, stream);
+        if (e == hipSuccess) lease.launched();
     } else {
         const uint64_t total = a.chunks_per_cell * a.n_shards * a.stripes;
         uint64_t grid = (total + kCrcBlock - 1) / kCrcBlock;

@@ -38,7 +38,8 @@ struct CrcArgs {
     uint64_t bytes_per_checksum;
     uint64_t chunks_per_cell;  // filled by the launcher
     uint64_t groups_per_cell;  // filled by the launcher (fast path)
-    uint32_t* queue;           // work-queue variant (measurement build, key 29): the stream's launch counters
+    uint32_t* queue;           // work-queue variant: this launch's counters (zero when it starts)
+    uint32_t* queue_zero;      // the set this launch zeroes for the stream's next launch (nullptr: none)
     uint32_t sums_nt;          // compute mode: non-temporal sum stores (measurement build, key 30)
 };
 

@@ -506,6 +506,7 @@ int hec_coder_create_codec(const char* codec, size_t data_units, size_t parity_u
                 HEC_HIP(hipEventCreateWithFlags(&c->ev_k[i], hipEventDisableTiming), HEC_ERR_DEVICE);
                 HEC_HIP(hipEventCreateWithFlags(&c->ev_out[i], hipEventDisableTiming), HEC_ERR_DEVICE);
             }
+            hec::queue_reserve(device);  // graph-capture counter sets, outside any capture
             return HEC_OK;
         }();
         if (rc != HEC_OK) {
@@ -2004,6 +2005,17 @@ int numa_node_of(int device) {
 }
 
 }  // namespace
+
+void hec_queue_stats(int device, uint64_t* streams, uint64_t* graph_sets, int* keyed_by_id) {
+    try {
+        hec::queue_stats(device, streams, graph_sets);
+        if (keyed_by_id) *keyed_by_id = hec::queue_keyed_by_id();
+    } catch (...) {
+        if (streams) *streams = 0;
+        if (graph_sets) *graph_sets = 0;
+        if (keyed_by_id) *keyed_by_id = 0;
+    }
+}
 
 int hec_device_numa_node(int device) {
     try {

@@ -534,6 +534,7 @@ int launch_fused(const MatmulArgs& in, const FusedCrcArgs& cs, bool verify, int 
     // 0.697-0.698, RS(6,3) x 1024 0.697-0.709 vs 0.703-0.712.  Tune key 28
     // (measurement build): 1 = the queue at k = 3, 6, 10; 2 = block tiles.
     bool wq = false;
+    QueueLease lease;  // work-queue counters (held until the launch is enqueued)
     const bool wq_want = kExperimental && tn.fused_wq ? tn.fused_wq == 1 : (a.k == 3 || a.k == 10);
     const bool wq_shape = slabs == fused_slabs(a.k, a.r) || (kExperimental && slabs == 4);
     if (wq_want && !verify && !split && fn && scheme == 12 && wpe == 2 && !vk.fn && wq_shape &&
@@ -545,20 +546,22 @@ int launch_fused(const MatmulArgs& in, const FusedCrcArgs& cs, bool verify, int 
             case 10 * 16 + 4: f = encode_wq_fn<10, 4>(slabs); break;
             default: break;
         }
-        a.queue = f ? stream_counters(device, stream) : nullptr;
-        if (a.queue) {
+        if (f) lease = queue_lease(device, stream);
+        if (lease) {
             fn = f;
             wq = true;
         }
     }
     if (vk.fn && vwq) {
-        a.queue = stream_counters(device, stream);
-        if (a.queue)
+        lease = queue_lease(device, stream);
+        if (lease)
             wq = true;
         else
             vk.fn = nullptr;  // no counters: the generic kernel (below) instead
         if (!vk.fn) use_slabs = slabs;
     }
+    a.queue = lease.use;
+    a.queue_zero = lease.zero;
     if (!fn && !vk.fn) return -1;
     const uint64_t chunks = a.cell_len / 16;
     // split: 4 GF waves x 8 KiB per tile; else waves x slabs x 1 KiB (work
@@ -595,10 +598,14 @@ int launch_fused(const MatmulArgs& in, const FusedCrcArgs& cs, bool verify, int 
         jit::count_launch();
         const hipError_t e =
             hipModuleLaunchKernel(vk.fn, uint32_t(grid), 1, 1, uint32_t(waves * 64), 1, 1, 0, stream, args, nullptr);
-        return e == hipSuccess ? 0 : int(e);
+        if (e != hipSuccess) return int(e);
+        lease.launched();
+        return 0;
     }
     const hipError_t e = hipLaunchKernel(fn, dim3(uint32_t(grid)), dim3(uint32_t(waves * 64)), args, 0, stream);
-    return e == hipSuccess ? 0 : int(e);
+    if (e != hipSuccess) return int(e);
+    lease.launched();
+    return 0;
 }
 
 }  // namespace

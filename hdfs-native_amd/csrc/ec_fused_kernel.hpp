@@ -160,7 +160,10 @@ __global__ __launch_bounds__(crcdev::sliced(SCHEME) ? 128 * WPE * (WPE - 1) : 51
     bool have_next = false;
     u32x4 x[SLABS], xn[SLABS];
     WaveQueue wq;
-    if constexpr (WQ) wq.init(a.queue, total, WAVES);
+    if constexpr (WQ) {
+        queue_zero_next(a.queue_zero);
+        wq.init(a.queue, total);
+    }
     // the wave's byte offset inside a block tile (WQ: a wave-tile is the wave's own)
     const uint32_t wave_off = WQ ? 0u : uint32_t(wave) * WAVE_BYTES;
     for (uint32_t tile = WQ ? wq.next() : blockIdx.x; tile < total; tile = WQ ? wq.next() : tile + gridDim.x) {

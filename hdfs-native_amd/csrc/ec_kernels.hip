@@ -28,17 +28,22 @@
 // HEC_EXPERIMENTAL library.
 #include <hip/hip_runtime.h>
 
+#include <dlfcn.h>
+
 #include <algorithm>
 #include <cstdint>
 #include <functional>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <tuple>
+#include <vector>
 
 #include "bitslice.hpp"
 #include "ec_kernels.hpp"
 #include "gf_device.hpp"
+#include "work_queue.hpp"
 #include "xor_networks.hpp"
 
 namespace hec {
@@ -83,9 +88,9 @@ __device__ __forceinline__ void gstore16(gbyte* p, u32x4 v) {
 // kMixedQueues, i.e. one per XCD), WQ rounds per atomic, the next batch
 // fetched while the current one is coded.  Fast CUs take more tiles than slow
 // ones, and the waves still walk the tile order together.  The counters are
-// zero at rest: every wave makes exactly one fetch past the end, so a
-// counter's last value is known (its in-range batches + its waves) and the
-// wave that draws it resets the counter for the stream's next launch.
+// zero when the launch starts: the stream's previous launch zeroed this set
+// (a.queue) and this one zeroes the other (a.queue_zero) for the next launch
+// (work_queue.hpp queue_zero_next, ec_kernels.hip queue_lease).
 template <int K, int R, int U, bool NT, int BS, int WQ = 0>
 __global__ __launch_bounds__(BS) void gf_matmul_v16(MatmulArgs a) {
     static_assert(WQ == 0 || K > 0, "the work queue needs compile-time k");
@@ -117,31 +122,24 @@ __global__ __launch_bounds__(BS) void gf_matmul_v16(MatmulArgs a) {
     // WQ: this wave's counter, its next batch (lane 0, in flight) and the
     // rounds left of the current one; tile = round * wq_n + counter
     // counters in use: one per block up to kMixedQueues (a grid smaller than
-    // that, tune key 7, must still reach every tile)
+    // that, tune key 7, must still reach every tile).  The counters are zero
+    // at the launch's start (queue_zero_next, work_queue.hpp): this launch
+    // zeroes the set of the stream's next launch and never resets its own.
     const uint32_t wq_n = gridDim.x < kMixedQueues ? gridDim.x : kMixedQueues;
     const uint32_t wq_q = blockIdx.x % wq_n;
     uint32_t* const wq_ctr = WQ ? a.queue + wq_q * (kMixedQueueStride / 4) : nullptr;
-    uint32_t wq_last = 0;  // the counter's last value this launch
-    if constexpr (WQ > 0) {
-        const uint32_t rounds = total > wq_q ? (total - 1 - wq_q) / wq_n + 1 : 0;
-        const uint32_t blocks = (gridDim.x - 1 - wq_q) / wq_n + 1;
-        wq_last = (rounds + WQ - 1) / WQ + blocks * (BS / 64) - 1;
-    }
+    if constexpr (WQ > 0) queue_zero_next(a.queue_zero);
     uint32_t wq_next, wq_round = 0, wq_left = 0;
-    // Every fetch is read back, the one past the end included (a batch that
-    // runs out mid-way still reads the fetch issued behind it), so exactly
-    // one wave reads the counter's last value.
+    // defined in every lane (only lane 0's is read): the atomic's result is
+    // not merged with an undefined value (as gf_decode_mixed's v_next)
+    asm volatile("" : "=v"(wq_next));
     auto next_tile = [&]() -> uint32_t {
         for (;;) {
             if (wq_left == 0) {
                 const uint32_t v = uint32_t(__builtin_amdgcn_readfirstlane(int(wq_next)));
                 wq_round = v * uint32_t(WQ);
                 wq_left = WQ;
-                if (uint64_t(wq_round) * wq_n + wq_q >= total) {
-                    if ((threadIdx.x & 63u) == 0 && v == wq_last)
-                        (void)atomicExch(wq_ctr, 0u);  // every fetch of this counter is done
-                    return total;
-                }
+                if (uint64_t(wq_round) * wq_n + wq_q >= total) return total;  // the wave is done
                 if ((threadIdx.x & 63u) == 0) wq_next = atomicAdd(wq_ctr, 1u);
             } else {
                 wq_round++;
@@ -1117,33 +1115,224 @@ Shape default_shape(int k, uint64_t cell_len) {
 
 }  // namespace
 
-// The work-queue counters of (device, stream): kMixedQueues of them,
-// kMixedQueueStride apart, zero at rest (each launch leaves them zero, see
-// gf_matmul_v16), zeroed on the stream when first made.  Launches on one
-// stream run in order, so they share a set; launches on different streams
-// get different sets (hipStreamPerThread: one set per thread).  Never freed
-// (2 KiB per stream that ever launched).
-uint32_t* stream_counters(int device, hipStream_t stream) {
+// ---------------------------------------------------------------------------
+// Work-queue counter sets (DESIGN.md §3.1 "Counter sets", round 6).  A set is
+// kMixedQueues counters kMixedQueueStride bytes apart (2 KiB).
+//  * Direct launches: every stream has two sets and alternates between them.
+//    Launch i counts on set i % 2 and zeroes set (i + 1) % 2 from its block 0
+//    (queue_zero_next) -- the set launch i-1 used, which has completed since
+//    a stream runs its launches in order.  So a launch starts on zeroed
+//    counters whatever the previous launch left behind: a miscount, an early
+//    exit or a fault can no longer leak tiles into the next launch.  Both sets
+//    are zeroed on the stream when the stream is first seen.
+//  * Streams are keyed by hipStreamGetId where the HIP runtime in the
+//    process has it (ROCm >= 7.1; looked up at run time, so the library
+//    still loads next to an older runtime such as the one a torch wheel
+//    bundles): ids are unique for the process's life, handles are not.
+//    Otherwise by handle: a handle comes back only after hipStreamDestroy,
+//    which waits for the stream's work (scripts/probe_stream_id.py), so the
+//    new stream inherits sets whose last launch has completed -- the same
+//    state a stream's next launch sees.  hipStreamPerThread is a different
+//    stream in every thread under one handle: its sets are thread_local
+//    (only the owning thread launches on them).
+//  * Stream capture: a launch into a capturing stream takes a set of its own
+//    from the device's graph pool (allocated outside any capture by
+//    queue_reserve) and a memset node zeroing it is captured right before the
+//    kernel, so every replay starts from zero and no replay shares counters
+//    with direct launches on the capture stream or another graph.  Graph sets
+//    are never returned (the graph may be replayed at any time).
+//  * Bounds: kMaxStreamSets streams and kGraphSets graph launches per device.
+//    Past them (or when HIP refuses an allocation / a query) the lease is
+//    empty and the caller launches the fixed-order kernel: slower, never
+//    wrong.  Stream sets are never freed (a destroyed stream's id never comes
+//    back, but its last launch may still be in flight when it is destroyed).
+// ---------------------------------------------------------------------------
+namespace {
+
+constexpr size_t kSetBytes = size_t(kMixedQueues) * kMixedQueueStride;
+constexpr size_t kMaxStreamSets = 4096;  // 2 sets x 2 KiB each: 16 MiB per device at most
+constexpr size_t kGraphSets = 256;       // 512 KiB per device
+
+struct StreamSets {
+    std::mutex mu;
+    uint32_t* set[2] = {nullptr, nullptr};
+    unsigned cur = 0;     // the set the stream's next launch counts on
+    bool zeroed = false;  // both sets zeroed on the stream (its first lease)
+};
+
+struct DeviceQueues {
+    std::mutex mu;
+    std::map<unsigned long long, std::unique_ptr<StreamSets>> streams;  // by stream id (or handle)
+    std::vector<std::unique_ptr<StreamSets>> thread_sets;                // hipStreamPerThread, one per thread
+    uint32_t* graph_pool = nullptr;
+    size_t graph_next = 0;
+    bool reserved = false;
+};
+
+DeviceQueues& device_queues(int device) {
     static std::mutex mu;
-    static std::map<std::tuple<int, uintptr_t, size_t>, uint32_t*> sets;
-    // hipStreamPerThread names a different stream in every thread
-    const size_t thread = stream == hipStreamPerThread ? std::hash<std::thread::id>()(std::this_thread::get_id()) : 0;
+    static std::map<int, std::unique_ptr<DeviceQueues>> all;
     std::lock_guard<std::mutex> lk(mu);
-    uint32_t*& c = sets[{device, reinterpret_cast<uintptr_t>(stream), thread}];
-    if (!c) {
-        const size_t bytes = size_t(kMixedQueues) * kMixedQueueStride;
-        if (hipMalloc(reinterpret_cast<void**>(&c), bytes) != hipSuccess) {
-            (void)hipGetLastError();
-            c = nullptr;
-            return nullptr;
+    auto& d = all[device];
+    if (!d) d.reset(new DeviceQueues);
+    return *d;
+}
+
+}  // namespace
+
+QueueLease::QueueLease(QueueLease&& o) noexcept : use(o.use), zero(o.zero), st_(o.st_) {
+    o.use = o.zero = nullptr;
+    o.st_ = nullptr;
+}
+
+QueueLease& QueueLease::operator=(QueueLease&& o) noexcept {
+    if (this != &o) {
+        if (st_) static_cast<StreamSets*>(st_)->mu.unlock();
+        use = o.use;
+        zero = o.zero;
+        st_ = o.st_;
+        o.use = o.zero = nullptr;
+        o.st_ = nullptr;
+    }
+    return *this;
+}
+
+QueueLease::~QueueLease() {
+    if (st_) static_cast<StreamSets*>(st_)->mu.unlock();
+}
+
+void QueueLease::launched() {
+    if (st_) static_cast<StreamSets*>(st_)->cur ^= 1u;
+}
+
+void queue_reserve(int device) {
+    DeviceQueues& d = device_queues(device);
+    std::lock_guard<std::mutex> lk(d.mu);
+    if (d.reserved) return;
+    d.reserved = true;
+    void* p = nullptr;
+    if (hipMalloc(&p, kGraphSets * kSetBytes) != hipSuccess) {
+        (void)hipGetLastError();
+        return;
+    }
+    d.graph_pool = static_cast<uint32_t*>(p);
+}
+
+void queue_stats(int device, uint64_t* streams, uint64_t* graph_sets) {
+    DeviceQueues& d = device_queues(device);
+    std::lock_guard<std::mutex> lk(d.mu);
+    if (streams) *streams = d.streams.size() + d.thread_sets.size();
+    if (graph_sets) *graph_sets = d.graph_next;
+}
+
+namespace {
+
+typedef hipError_t (*StreamGetIdFn)(hipStream_t, unsigned long long*);
+
+// hipStreamGetId of the HIP runtime this library is bound to, or nullptr
+StreamGetIdFn stream_get_id() {
+    static const StreamGetIdFn fn = []() -> StreamGetIdFn {
+        Dl_info info;
+        if (!dladdr(reinterpret_cast<void*>(&hipMemsetAsync), &info) || !info.dli_fname) return nullptr;
+        void* h = dlopen(info.dli_fname, RTLD_LAZY | RTLD_NOLOAD);
+        if (!h) return nullptr;
+        void* f = dlsym(h, "hipStreamGetId");
+        dlclose(h);  // NOLOAD: only drops the reference just taken
+        return reinterpret_cast<StreamGetIdFn>(f);
+    }();
+    return fn;
+}
+
+// new sets for a stream: both zeroed on the stream itself (ordered before
+// the stream's first queue kernel); nullptr when HIP refuses
+std::unique_ptr<StreamSets> make_sets() {
+    std::unique_ptr<StreamSets> n(new StreamSets);
+    void* p = nullptr;
+    if (hipMalloc(&p, 2 * kSetBytes) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    n->set[0] = static_cast<uint32_t*>(p);
+    n->set[1] = n->set[0] + kSetBytes / 4;
+    return n;
+}
+
+}  // namespace
+
+int queue_keyed_by_id() { return stream_get_id() ? 1 : 0; }
+
+QueueLease queue_lease(int device, hipStream_t stream) {
+    QueueLease l;
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(stream, &cap) != hipSuccess) {
+        (void)hipGetLastError();
+        return l;  // e.g. the legacy stream while another stream captures
+    }
+    DeviceQueues& d = device_queues(device);
+    if (cap != hipStreamCaptureStatusNone) {
+        if (cap != hipStreamCaptureStatusActive) return l;  // invalidated capture: nothing to add to
+        uint32_t* set = nullptr;
+        {
+            std::lock_guard<std::mutex> lk(d.mu);
+            if (d.graph_pool && d.graph_next < kGraphSets) set = d.graph_pool + d.graph_next++ * (kSetBytes / 4);
         }
-        if (hipMemsetAsync(c, 0, bytes, stream) != hipSuccess) {
+        if (!set) return l;
+        if (hipMemsetAsync(set, 0, kSetBytes, stream) != hipSuccess) {  // captured: a memset node
             (void)hipGetLastError();
-            (void)hipFree(c);
-            c = nullptr;
+            return l;
+        }
+        l.use = set;
+        return l;
+    }
+    StreamSets* st = nullptr;
+    if (stream == hipStreamPerThread) {
+        // this thread's own stream: sets of its own, per device (kept for
+        // the thread's life and after: its last launches may be in flight)
+        thread_local std::map<int, StreamSets*> mine;
+        StreamSets*& t = mine[device];
+        if (!t) {
+            std::lock_guard<std::mutex> lk(d.mu);
+            if (d.streams.size() + d.thread_sets.size() >= kMaxStreamSets) return l;
+            std::unique_ptr<StreamSets> n = make_sets();
+            if (!n) return l;
+            t = n.get();
+            d.thread_sets.push_back(std::move(n));
+        }
+        st = t;
+    } else {
+        unsigned long long key = reinterpret_cast<uintptr_t>(stream);
+        if (StreamGetIdFn get_id = stream_get_id()) {
+            if (get_id(stream, &key) != hipSuccess) {
+                (void)hipGetLastError();
+                return l;
+            }
+        }
+        std::lock_guard<std::mutex> lk(d.mu);
+        auto it = d.streams.find(key);
+        if (it != d.streams.end()) {
+            st = it->second.get();
+        } else if (d.streams.size() + d.thread_sets.size() < kMaxStreamSets) {
+            std::unique_ptr<StreamSets> n = make_sets();
+            if (!n) return l;
+            st = n.get();
+            d.streams.emplace(key, std::move(n));
         }
     }
-    return c;
+    if (!st) return l;
+    st->mu.lock();
+    if (!st->zeroed) {
+        // first launch on this stream: both sets zeroed on the stream itself
+        if (hipMemsetAsync(st->set[0], 0, 2 * kSetBytes, stream) != hipSuccess) {
+            (void)hipGetLastError();
+            st->mu.unlock();
+            return l;  // the stream's next lease tries again
+        }
+        st->zeroed = true;
+    }
+    l.st_ = st;
+    l.use = st->set[st->cur];
+    l.zero = st->set[st->cur ^ 1u];
+    return l;
 }
 
 bool rs_parity_matrix(const MatmulArgs& a) {
@@ -1190,6 +1379,7 @@ int launch_gf_matmul(const MatmulArgs& in, int device, hipStream_t stream) {
             }
         }
         const void* fn = nullptr;
+        QueueLease lease;   // work-queue counters (held until the launch is enqueued)
         int tile_mult = 1;  // column tiles per scheduling unit (output-burst kernel)
 #ifdef HEC_EXPERIMENTAL
         ExpKernel ek;
@@ -1218,7 +1408,9 @@ int launch_gf_matmul(const MatmulArgs& in, int device, hipStream_t stream) {
             wq = default_wq(a.k);
             if (kExperimental && tn.matmul_wq) wq = tn.matmul_wq == 3 ? 0 : tn.matmul_wq;
             const void* f = wq ? pick_wq(a.k, a.r, wq, sh.block, sh.unroll) : nullptr;
-            a.queue = f ? stream_counters(device, stream) : nullptr;
+            if (f) lease = queue_lease(device, stream);
+            a.queue = lease.use;
+            a.queue_zero = lease.zero;
             if (a.queue) {
                 fn = f;
                 if (!tn.blocks_per_cu) sh.blocks_per_cu = 1;  // resident blocks only: each one drains the queue
@@ -1248,6 +1440,7 @@ int launch_gf_matmul(const MatmulArgs& in, int device, hipStream_t stream) {
         void* args[] = {&a};
         const hipError_t e = hipLaunchKernel(fn, dim3(uint32_t(grid)), dim3(sh.block), args, 0, stream);
         if (e != hipSuccess) return int(e);
+        lease.launched();
     }
     uint64_t begin = chunks * 16;
     if (begin == 0 && !aligned && a.cell_len >= 8 && a.r >= 1 && a.r <= kMaxR && tn.unaligned != 1) {

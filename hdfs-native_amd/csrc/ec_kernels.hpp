@@ -37,7 +37,8 @@ struct MatmulArgs {
     uint32_t grouped_tiles;       // tiles of the whole G-stripe groups; the remainder stripes go stripe-major
     uint32_t drain;               // register kernel: 1 = wait for the tile's stores before the next tile's loads
     uint32_t col_rot = 0;         // tile order: stripe s starts its columns at (s * col_rot) % tiles (0 = none)
-    uint32_t* queue = nullptr;    // work-queue register kernel: the stream's launch counters (zero at rest)
+    uint32_t* queue = nullptr;       // work-queue kernels: this launch's counters (zero when it starts)
+    uint32_t* queue_zero = nullptr;  // the set this launch zeroes for the stream's next launch (nullptr: none)
 };
 
 // One coefficient's v_perm_b32 product tables (see ec_kernels.hip): c*x =
@@ -83,9 +84,41 @@ struct MixedArgs {
     uint32_t* queue;                  // this launch's zeroed tile counters (work-queue variant, key 26)
 };
 
-// The work-queue launch counters of (device, stream) (ec_kernels.hip): zero
-// at rest, made and zeroed on the stream on first use; nullptr on failure.
-uint32_t* stream_counters(int device, hipStream_t stream);
+#ifndef __HIPCC_RTC__
+// The work-queue counter sets of one launch (ec_kernels.hip, DESIGN.md §3.1
+// "Counter sets").  A direct launch takes its stream's current set (`use`,
+// zero) and zeroes the stream's other set (`zero`) for the next launch; the
+// stream is held (its sets' lock) from queue_lease() until the lease ends, so
+// launches from several threads on one stream still alternate in their
+// stream order.  A launch into a stream that is being captured gets a set of
+// its own (the graph keeps it for good) zeroed by a memset node captured
+// just before the kernel; `zero` is then nullptr.  An empty lease (use ==
+// nullptr) means: launch the fixed-order kernel.
+struct QueueLease {
+    uint32_t* use = nullptr;
+    uint32_t* zero = nullptr;
+    QueueLease() = default;
+    QueueLease(QueueLease&& o) noexcept;
+    QueueLease& operator=(QueueLease&& o) noexcept;
+    QueueLease(const QueueLease&) = delete;
+    QueueLease& operator=(const QueueLease&) = delete;
+    ~QueueLease();
+    explicit operator bool() const { return use != nullptr; }
+    // The kernel was enqueued: the stream's next launch takes `zero`.  A lease
+    // whose kernel was not enqueued leaves the stream on `use` (still zero).
+    void launched();
+    void* st_ = nullptr;  // the stream's sets (held while the lease lives)
+};
+QueueLease queue_lease(int device, hipStream_t stream);
+// Allocates the device's pool of graph-capture sets, outside any capture
+// (hec_coder_create calls it); a capture with no set left launches the
+// fixed-order kernels.
+void queue_reserve(int device);
+// Counter sets in use on a device: {direct streams, graph sets handed out}.
+void queue_stats(int device, uint64_t* streams, uint64_t* graph_sets);
+// 1 when streams are told apart by hipStreamGetId, 0 when by handle.
+int queue_keyed_by_id();
+#endif
 
 // Mixed-pattern decode of one group of missing rows row0 .. row0+rows-1
 // (rows <= kMaxR).  Requires k in {2,3,6,10}, 16-B aligned bases/strides

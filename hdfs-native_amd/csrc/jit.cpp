@@ -206,6 +206,9 @@ std::string device_arch(int device) {
     return cache[device] = arch;
 }
 
+// hiprtc options past the arch (part of the disk-cache key)
+constexpr const char* kRtcOptions = "-O3 -std=c++17 -mllvm -amdgpu-atomic-optimizer-strategy=None";
+
 enum class State { kQueued, kCompiling, kReady, kFailed };
 
 struct Entry {
@@ -268,7 +271,7 @@ struct Jit {
         if (r.ok) r.version(&maj, &mnr);
         const std::string dir = cache_dir();
         const uint64_t h = fnv1a(name + "\n" + en.arch + "\n" + std::to_string(maj) + "." + std::to_string(mnr) +
-                                 "\n" + src + kHeaderDigest);
+                                 "\n" + kRtcOptions + "\n" + src + kHeaderDigest);
         char hex[17];
         std::snprintf(hex, sizeof hex, "%016llx", static_cast<unsigned long long>(h));
         const std::string path = dir.empty() ? "" : dir + "/dv-" + hex + ".co";
@@ -304,8 +307,12 @@ struct Jit {
                 const std::string expr = "&" + name;
                 r.add_name(prog, expr.c_str());
                 const std::string arch_opt = "--offload-arch=" + en.arch;
-                const char* opts[] = {arch_opt.c_str(), "-O3", "-std=c++17"};
-                if (r.compile(prog, 3, opts) == 0) {
+                // the ahead-of-time library's flags (Makefile): the work queue's
+                // one-lane fetch must not become a wave-combined atomic waited
+                // for at issue
+                const char* opts[] = {arch_opt.c_str(), "-O3", "-std=c++17", "-mllvm",
+                                      "-amdgpu-atomic-optimizer-strategy=None"};
+                if (r.compile(prog, 5, opts) == 0) {
                     size_t n = 0;
                     const char* low = nullptr;
                     if (r.code_size(prog, &n) == 0 && n > 0 && r.lowered(prog, expr.c_str(), &low) == 0 && low) {

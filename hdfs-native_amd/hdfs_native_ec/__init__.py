@@ -53,7 +53,7 @@ EXPORTS = [
     "hec_device_alloc", "hec_device_free", "hec_device_numa_node", "hec_host_alloc", "hec_host_free",
     "hec_coder_acquire", "hec_coder_release", "hec_coder_pool_trim", "hec_coder_set_host_limit",
     "hec_coder_host_limit", "hec_gf_matmul_host", "hec_host_isa", "hec_encode_rows_host",
-    "hec_coder_prepare_decode", "hec_jit_warm", "hec_jit_stats",
+    "hec_coder_prepare_decode", "hec_jit_warm", "hec_jit_stats", "hec_queue_stats",
     "hec_encode_rows_workspace_size", "hec_encode_rows_device", "hec_decode_rows_host",
 ]
 
@@ -158,6 +158,7 @@ def _load(path: str = LIB_PATH) -> ctypes.CDLL:
         "hec_coder_prepare_decode": ([P, P, I, P], I),
         "hec_jit_warm": ([S, S, P, I], I),
         "hec_jit_stats": ([P, P, P, P], None),
+        "hec_queue_stats": ([I, P, P, P], None),
         "hec_gf_matmul_host": ([P, S, S, PP, PP, S], I),
         "hec_host_isa": ([], ctypes.c_char_p),
         "hec_encode_rows_host": ([P, P, S, P, S, S], I),
@@ -560,6 +561,16 @@ def jit_stats() -> dict:
     v = [ctypes.c_uint64(0) for _ in range(4)]
     lib.hec_jit_stats(*[ctypes.byref(x) for x in v])
     return dict(zip(("compiled", "from_disk", "failed", "launches"), (x.value for x in v)))
+
+
+def queue_stats(device: int = 0) -> dict:
+    """hec_queue_stats: the work-queue counter sets of `device` (streams that
+    launched a queue kernel, graph sets handed out to captured launches, and
+    whether streams are told apart by hipStreamGetId or by handle)."""
+    v = [ctypes.c_uint64(0) for _ in range(2)]
+    by_id = ctypes.c_int(0)
+    lib.hec_queue_stats(device, *[ctypes.byref(x) for x in v], ctypes.byref(by_id))
+    return {"streams": v[0].value, "graph_sets": v[1].value, "keyed_by_id": bool(by_id.value)}
 
 
 def stripe_layout_ptrs(t, units: int):

@@ -313,6 +313,18 @@ int hec_coder_prepare_decode(hec_coder_t *coder, const uint8_t *present, int che
 int hec_jit_warm(size_t data_units, size_t parity_units, const uint8_t *present, int checksum_type);
 void hec_jit_stats(uint64_t *compiled, uint64_t *from_disk, uint64_t *failed, uint64_t *launches);
 
+/* ---- work-queue counter sets (diagnostic) -------------- *
+ * The coding kernels deal their tiles from launch counters.  Every stream
+ * that launched one has two counter sets it alternates between (each launch
+ * zeroes the set of the stream's next launch); a launch into a capturing
+ * stream gets a set of its own, zeroed by a memset node in the graph.
+ * hec_queue_stats: streams with sets and graph sets handed out on `device`
+ * (process totals; past 4096 streams / 256 graph launches per device the
+ * kernels fall back to their fixed tile order), and *keyed_by_id = 1 when
+ * streams are told apart by hipStreamGetId (HIP >= 7.1 in the process), 0
+ * when by handle.  Any pointer may be NULL. */
+void hec_queue_stats(int device, uint64_t *streams, uint64_t *graph_sets, int *keyed_by_id);
+
 /* Encode plus CRC32C of the k data and m parity cells (shard order
  * 0..k+m-1, same output layout as hec_crc32c_device): everything a striped
  * writer needs to emit its k+m packet streams.  One fused pass (the

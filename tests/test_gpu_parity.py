@@ -438,10 +438,11 @@ def test_full_size_roundtrip_and_oracle(dev, c_oracle, k, m, cell, S):
 
 def test_work_queue_counters_reset_across_launches(dev, c_oracle):
     """The register kernel deals wave-tiles from per-stream launch counters
-    that each launch leaves at zero (ec_kernels.hip gf_matmul_v16): launches
-    of different tile counts back to back on one stream (fewer tiles than
-    counters, fewer than CUs, many), then two streams at once -- a counter
-    left non-zero would skip tiles of the next launch."""
+    (ec_kernels.hip queue_lease: two sets per stream, each launch zeroes the
+    next launch's): launches of different tile counts back to back on one
+    stream (fewer tiles than counters, fewer than CUs, many), then three
+    streams at once -- a counter not zero at a launch's start would skip
+    tiles of that launch."""
     k, m = 6, 3
     cod = coder(k, m)
     for S, cell in [(1, 1 << 20), (3, 1 << 20), (1, 4096), (200, 1 << 20), (5, 8192 + 16), (64, 1 << 20)]:
@@ -471,8 +472,9 @@ def test_work_queue_counters_reset_across_launches(dev, c_oracle):
 
 def test_work_queue_per_thread_default_stream(dev):
     """hipStreamPerThread ((hipStream_t)2) is a different stream in every
-    thread: the work-queue counters are kept per thread for it, so threads
-    encoding at once on that handle never share a counter set."""
+    thread: the work-queue counter sets are keyed by hipStreamGetId, which
+    resolves the handle to the thread's own stream, so threads encoding at
+    once on that handle never share a counter set."""
     import threading
     k, m, S, cell = 6, 3, 48, 1 << 20
     ds = [_device_random((S, k, cell), dev, seed=70 + i) for i in range(4)]
@@ -506,6 +508,211 @@ def test_work_queue_per_thread_default_stream(dev):
     for t in ts:
         t.join()
     assert not errors, errors
+
+
+SENTINEL = 0xA5
+
+
+@pytest.mark.parametrize("k,m", [(2, 1), (3, 2), (6, 3), (10, 4)])
+@pytest.mark.parametrize("cell", [8192 + 16, 3 * 65536 + 48])
+def test_work_queue_kernels_back_to_back_sentinel(dev, c_oracle, k, m, cell):
+    """Every work-queue kernel of the product, back to back on ONE stream,
+    over batches of 3, 1 and 40 stripes whose cells end in partial wave-
+    tiles (8208 B: RS(2,1) x 3 stripes is the r05u/r05v failure, DESIGN.md
+    §3.1): the plain encode (gf_matmul_v16), the fused encode + CRC (the
+    queue at k = 3 and 10), the plan-specialised decode + verify (the queue
+    at every k) and the plain decode.  Every output starts as a sentinel
+    byte, so a tile the queue never dealt shows up; parity, sums and the
+    rebuilt shards are checked against the oracle."""
+    bpc = 512
+    cod = H.Coder(k, m, 0)
+    lost = list(range(min(m, k)))
+    assert cod.prepare_decode(lost, H.CHECKSUM_CRC32C), "hiprtc unavailable on the GPU box"
+    st = torch.cuda.Stream()
+    with torch.cuda.stream(st):
+        for rep, S in enumerate([3, 1, 40, 3]):
+            data = batch_data(S, k, cell, first=cell + 13 * S + rep)
+            par = oracle_batch_encode(c_oracle, k, m, data)
+            nch = (cell + bpc - 1) // bpc
+            edge = [0, S - 1] if S > 1 else [0]  # the Python CRC oracle is slow: first and last stripe
+            want_sums = _oracle_sums(np.concatenate([data[edge], par[edge]], axis=1), bpc)
+            d = torch.from_numpy(data).to(dev)
+            # plain encode
+            p = torch.full((S, m, cell), SENTINEL, dtype=torch.uint8, device=dev)
+            H.encode_batch(cod, d, p, st)
+            # fused encode + CRC
+            p2 = torch.full((S, m, cell), SENTINEL, dtype=torch.uint8, device=dev)
+            sums = torch.full((S, k + m, nch, 4), SENTINEL, dtype=torch.uint8, device=dev)
+            dp, ds = H.stripe_layout_ptrs(d, k)
+            pp, ps = H.stripe_layout_ptrs(p2, m)
+            cod.encode_crc_device(dp, ds, pp, ps, cell, S, bpc, sums.data_ptr(), st.cuda_stream)
+            # decode + verify (specialised), data shards `lost` missing
+            out = torch.full((S, k, cell), SENTINEL, dtype=torch.uint8, device=dev)
+            bad = torch.full((S, k + m), 7, dtype=torch.uint8, device=dev)
+            ptrs = [None if i in lost else dp[i] for i in range(k)] + pp
+            op, os_ = H.stripe_layout_ptrs(out, k)
+            before = H.jit_stats()["launches"]
+            cod.decode_verify_device(H.CHECKSUM_CRC32C, ptrs, ds + ps, op, os_, cell, S, bpc,
+                                     sums.data_ptr(), bad.data_ptr(), st.cuda_stream)
+            # plain decode of the same shards
+            out2 = torch.full((S, k, cell), SENTINEL, dtype=torch.uint8, device=dev)
+            H.decode_batch(cod, d, p2, lost, out2, st)
+            # every stripe's sums against the fixed-order CRC kernel (another kernel)
+            ref = H.crc32c_batch(cod, torch.cat([d, torch.from_numpy(par).to(dev)], dim=1), bpc, st)
+            st.synchronize()
+            assert H.jit_stats()["launches"] > before
+            assert np.array_equal(p.cpu().numpy(), par), (rep, S)
+            assert np.array_equal(p2.cpu().numpy(), par), (rep, S)
+            assert np.array_equal(sums.cpu().numpy()[edge], want_sums), (rep, S)
+            assert torch.equal(sums, ref), (rep, S)
+            assert not bad.cpu().numpy().any(), (rep, S)
+            for o in (out, out2):
+                on = o.cpu().numpy()
+                assert np.array_equal(on[:, lost], data[:, lost]), (rep, S)
+                assert (on[:, len(lost):] == SENTINEL).all(), (rep, S)  # present shards never written
+    cod.close()
+
+
+def _hip_runtime():
+    """torch's libamdhip64 (the one HIP runtime of the process)."""
+    import ctypes
+    with open("/proc/self/maps") as f:
+        for line in f:
+            if "libamdhip64" in line:
+                return ctypes.CDLL(line.split()[-1])
+    raise RuntimeError("libamdhip64 not mapped")
+
+
+def test_work_queue_stream_churn(dev, c_oracle):
+    """Streams created and destroyed one after another (HIP hands the same
+    handle out again): every encode / decode on the fresh streams is exact.
+    With hipStreamGetId in the process each new stream gets sets of its own
+    (the set count grows by one per stream); without it (the HIP a torch
+    wheel bundles) a reused handle inherits its destroyed stream's sets,
+    whose last launch hipStreamDestroy has waited for."""
+    import ctypes
+    hip = _hip_runtime()
+    k, m, S, cell = 6, 3, 5, 8192 + 16
+    cod = coder(k, m)
+    data = batch_data(S, k, cell, first=4242)
+    par = oracle_batch_encode(c_oracle, k, m, data)
+    d = torch.from_numpy(data).to(dev)
+    torch.cuda.synchronize()
+    before = H.queue_stats(0)["streams"]
+    handles = set()
+    n = 40
+    for i in range(n):
+        s = ctypes.c_void_p()
+        assert hip.hipStreamCreateWithFlags(ctypes.byref(s), 1) == 0  # hipStreamNonBlocking
+        handles.add(s.value)
+        p = torch.full((S, m, cell), SENTINEL, dtype=torch.uint8, device=dev)
+        out = torch.full((S, k, cell), SENTINEL, dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize()
+        dp, ds = H.stripe_layout_ptrs(d, k)
+        pp, ps = H.stripe_layout_ptrs(p, m)
+        cod.encode_device(dp, ds, pp, ps, cell, S, s.value)
+        op, os_ = H.stripe_layout_ptrs(out, k)
+        ptrs = [None, None, None] + dp[3:] + pp
+        cod.decode_device(ptrs, ds + ps, op, os_, cell, S, s.value)
+        assert hip.hipStreamSynchronize(s) == 0
+        assert hip.hipStreamDestroy(s) == 0
+        assert np.array_equal(p.cpu().numpy(), par), i
+        assert np.array_equal(out[:, :3].cpu().numpy(), data[:, :3]), i
+    grown = H.queue_stats(0)["streams"] - before
+    if H.queue_stats(0)["keyed_by_id"]:
+        assert grown == n, (grown, len(handles))
+    else:  # handles the library saw before (destroyed coders' streams) may come back too
+        assert grown <= len(handles), (grown, len(handles))
+
+
+def test_work_queue_one_stream_two_threads(dev):
+    """Two threads enqueue encodes on the SAME stream at once: the lease holds
+    the stream's sets from choosing a set to enqueuing the kernel, so the
+    launches alternate sets in their stream order and every output is exact."""
+    import threading
+    k, m, S, cell = 6, 3, 7, 3 * 65536 + 48
+    cod = coder(k, m)
+    ds = [_device_random((S, k, cell), dev, seed=90 + i) for i in range(2)]
+    want = []
+    for d in ds:
+        p = torch.empty((S, m, cell), dtype=torch.uint8, device=dev)
+        H.encode_batch(cod, d, p)
+        want.append(p)
+    torch.cuda.synchronize()
+    st = torch.cuda.Stream()
+    outs = [[torch.full((S, m, cell), SENTINEL, dtype=torch.uint8, device=dev) for _ in range(16)]
+            for _ in range(2)]
+    torch.cuda.synchronize()
+    errors = []
+
+    def work(i):
+        try:
+            c = H.Coder(k, m, 0)
+            dp, dst = H.stripe_layout_ptrs(ds[i], k)
+            for p in outs[i]:
+                pp, pst = H.stripe_layout_ptrs(p, m)
+                c.encode_device(dp, dst, pp, pst, cell, S, st.cuda_stream)
+            st.synchronize()
+            c.close()
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    ts = [threading.Thread(target=work, args=(i,)) for i in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errors, errors
+    for i in range(2):
+        for j, p in enumerate(outs[i]):
+            assert torch.equal(p, want[i]), (i, j)
+
+
+def test_work_queue_graph_capture_replay(dev, c_oracle):
+    """torch.cuda.graph (global capture mode) around an encode and a decode:
+    the captured launches take graph counter sets of their own, zeroed by a
+    memset node at every replay.  Replays on the capture stream between
+    direct launches there, and on a second stream while the first runs
+    direct launches, are all exact against the oracle."""
+    k, m, S, cell = 6, 3, 6, 65536 + 48
+    cod = H.Coder(k, m, 0)
+    d_s = torch.zeros((S, k, cell), dtype=torch.uint8, device=dev)
+    p_s = torch.zeros((S, m, cell), dtype=torch.uint8, device=dev)
+    o_s = torch.zeros((S, k, cell), dtype=torch.uint8, device=dev)
+    # warm-up outside the capture (first use of the capture stream's sets is
+    # not needed: captured launches never touch them)
+    torch.cuda.synchronize()
+    g0 = H.queue_stats(0)["graph_sets"]
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        H.encode_batch(cod, d_s, p_s)
+        H.decode_batch(cod, d_s, p_s, [0, 1, 2], o_s)
+    assert H.queue_stats(0)["graph_sets"] - g0 == 2  # both launches took the work queue
+    other = torch.cuda.Stream()
+    d2 = _device_random((40, k, cell), dev, seed=11)
+    p2 = torch.empty((40, m, cell), dtype=torch.uint8, device=dev)
+    for rep in range(6):
+        data = batch_data(S, k, cell, first=rep * 7 + 1)
+        par = oracle_batch_encode(c_oracle, k, m, data)
+        d_s.copy_(torch.from_numpy(data))
+        p_s.fill_(SENTINEL)
+        o_s.fill_(SENTINEL)
+        torch.cuda.synchronize()
+        if rep % 2 == 0:
+            H.encode_batch(cod, d2, p2)     # direct launches on the current stream
+            g.replay()                      # ... the graph between them
+            H.encode_batch(cod, d2, p2)
+        else:
+            with torch.cuda.stream(other):
+                g.replay()                  # the graph on another stream
+            H.encode_batch(cod, d2, p2)     # while the current stream runs direct launches
+            H.encode_batch(cod, d2, p2)
+        torch.cuda.synchronize()
+        assert np.array_equal(p_s.cpu().numpy(), par), rep
+        assert torch.equal(o_s[:, :3], d_s[:, :3]), rep
+    O.c_check_batch(c_oracle, k, m, d2[:3].cpu().numpy(), p2[:3].cpu().numpy(), threads=1)
+    del g
+    cod.close()
 
 
 def test_linearity(dev):
