@@ -311,6 +311,16 @@ def gather_ranks(ident, world, dist):
     return sorted(out, key=lambda r: r["rank"])
 
 
+def gather_list(value, world, dist):
+    """Every rank's `value`, in rank order (all_gather_object over the
+    process group; timing and shard metadata only, no data)."""
+    if world == 1 or not dist.is_initialized():
+        return [value]
+    out = [None] * world
+    dist.all_gather_object(out, value)
+    return out
+
+
 def process_group_info(args, world, dist):
     init = dist.is_available() and dist.is_initialized()
     return {"backend": dist.get_backend() if init else None, "requested_backend": args.backend,
@@ -337,15 +347,17 @@ def dry_run(args, world, rank):
     ranks = gather_ranks(rank_identity(rank, int(os.environ.get("LOCAL_RANK", "0")), None), world, dist)
     extra = {}
     for cfg in EXTRA_CONFIGS:  # the same per-rank split extra_configs() runs
-        _, share = shard_range(cfg["global_stripes"], world, rank)
+        c_first, share = shard_range(cfg["global_stripes"], world, rank)
         extra[cfg["name"]] = {"scaling": "strong", "stripes_per_gpu_rank0": share,
-                              "stripes_summed_over_ranks": int(sum_over_ranks(float(share))), "value_GiBps": None}
+                              "stripes_summed_over_ranks": int(sum_over_ranks(float(share))), "value_GiBps": None,
+                              "shards": gather_list([c_first, share], world, dist)}
+    shards = gather_list([first, S], world, dist)
     if rank == 0:
         print(json.dumps({"metric": METRIC, "value": None, "unit": "GiB/s", "n_gpus": world, "dry_run": True,
                           "scaling": "strong" if args.global_stripes else "weak",
                           "config": {"k": args.k, "m": args.m, "cell_bytes": args.cell, "stripes_per_gpu": S,
                                      "global_stripes": args.global_stripes or S * world,
-                                     "stripes_summed_over_ranks": int(total)},
+                                     "stripes_summed_over_ranks": int(total), "shards": shards},
                           "extra_configs": extra, "ranks": ranks,
                           "process_group": process_group_info(args, world, dist),
                           "max_elapsed_s": el}), flush=True)
@@ -921,6 +933,10 @@ def main():
         achieved = (algo_bytes + dec_bytes) / (enc_avg + dec_avg) / 1e9
 
     traffic, traffic_src = traffic_for(args.traffic, k, m, cell, S, args.decode_mode) if not args.tune else (None, None)
+    # every rank's own launch average and stripe range (rank order): an N-rank
+    # line shows each GPU's kernel time, not only rank 0's and the max
+    launch_per_rank = [round(x, 4) for x in gather_list(avg_launch_ms, world, dist)]
+    shards = gather_list([first, S], world, dist)
 
     result = {
         "metric": METRIC,
@@ -945,6 +961,7 @@ def main():
                         + (" (encode only)" if args.encode_only else ""),
             "k": k, "m": m, "cell_bytes": cell, "stripes_per_gpu": S,
             "global_stripes": args.global_stripes or S * world,
+            "shards": shards,
             "parallelism": f"stripe-sharded x{world}, no collectives",
             "decode_mode": args.decode_mode,
             "codec": args.codec,
@@ -961,6 +978,7 @@ def main():
                        if k in (2, 3, 6, 10) else f"gf_matmul_v16<{k},{m}> (encode and decode launches)"),
             "algorithmic_bytes_per_launch": algo_bytes,
             "avg_launch_ms": round(avg_launch_ms, 4),
+            "avg_launch_ms_per_rank": launch_per_rank,
             "frac_of_measured_copy": round(achieved / HBM_COPY_GBS, 4),
         },
         "encode_GiBps": round(k * cell * S / (sum(enc_ms) / len(enc_ms) * 1e-3) / GIB, 2),
@@ -1059,14 +1077,17 @@ def verify_batch(args, ec_oracle, clib, data, parity, rec, k, m):
             f" == C oracle ({threads} threads, {time.perf_counter() - t0:.1f} s)")
 
 
-EXTRA_CONFIGS = [  # the other multi-GPU BASELINE configs (BASELINE.json configs[3], [4]), split over the ranks
+EXTRA_CONFIGS = [  # split over the ranks: the headline's strong-scaling twin (1024 stripes in all, not per
+    # GPU) and the other multi-GPU BASELINE configs (BASELINE.json configs[3], [4])
+    {"name": "rs63_1MiB_x1024_strong", "k": 6, "m": 3, "cell": 1 << 20, "global_stripes": 1024},
     {"name": "rs104_1MiB_x2048", "k": 10, "m": 4, "cell": 1 << 20, "global_stripes": 2048},
     {"name": "rs63_64KiB_x65536", "k": 6, "m": 3, "cell": 1 << 16, "global_stripes": 65536},
 ]
 
 
 def extra_configs(args, H, dist, world, rank, dev, max_over_ranks, shard_range):
-    """RS(10,4) 1 MiB x 2048 and RS(6,3) 64 KiB x 65536, each split into
+    """The headline's strong-scaling twin (RS(6,3) 1 MiB x 1024 stripes IN
+    ALL), RS(10,4) 1 MiB x 2048 and RS(6,3) 64 KiB x 65536, each split into
     contiguous per-rank shares (strong scaling, no collective): encode +
     worst-case decode per step, allocation and warmup outside the timed
     loop, barrier + max-over-ranks time, every rank's batch checked against
@@ -1122,6 +1143,8 @@ def extra_configs(args, H, dist, world, rank, dev, max_over_ranks, shard_range):
                  [evs[i][1].elapsed_time(evs[i][2]) for i in range(steps)]
         avg_ms = sum(launch) / len(launch)
         avg_max = max_over_ranks(avg_ms, dev)
+        per_rank = [round(x, 4) for x in gather_list(avg_ms, world, dist)]
+        shards = gather_list([first, S], world, dist)
         algo = (k + m) * cell * S
         total = cfg["global_stripes"]
         out[cfg["name"]] = {
@@ -1131,6 +1154,7 @@ def extra_configs(args, H, dist, world, rank, dev, max_over_ranks, shard_range):
             "value_GiBps": round(2 * k * cell * total * steps / elapsed / GIB, 2),
             "ms_per_step": round(elapsed / steps * 1e3, 4),
             "avg_launch_ms_rank0": round(avg_ms, 4), "avg_launch_ms_max_over_ranks": round(avg_max, 4),
+            "avg_launch_ms_per_rank": per_rank, "shards": shards,
             "frac_rank0": round(algo / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "algorithmic_bytes_per_launch_rank0": algo,
             "check": "rebuilt == original on every rank (device)",

@@ -1986,6 +1986,26 @@ int hec_device_free(int device, void* ptr) {
     });
 }
 
+int hec_device_copy(int device, void* dst, const void* src, size_t bytes) {
+    if (bytes == 0) return HEC_OK;
+    if (!dst || !src) return HEC_ERR_INVALID_ARG;
+    return guarded([&] {
+        DeviceGuard g(device);
+        if (!g.ok) return fail(HEC_ERR_DEVICE, "hipSetDevice", hipErrorInvalidDevice);
+        HEC_HIP(hipMemcpy(dst, src, bytes, hipMemcpyDefault), HEC_ERR_DEVICE);
+        return HEC_OK;
+    });
+}
+
+int hec_device_synchronize(int device, void* hip_stream) {
+    return guarded([&] {
+        DeviceGuard g(device);
+        if (!g.ok) return fail(HEC_ERR_DEVICE, "hipSetDevice", hipErrorInvalidDevice);
+        HEC_HIP(hipStreamSynchronize(static_cast<hipStream_t>(hip_stream)), HEC_ERR_DEVICE);
+        return HEC_OK;
+    });
+}
+
 // ---- NUMA-placed pinned host buffers -------------------------------------
 
 namespace {

@@ -779,6 +779,158 @@ __global__ __launch_bounds__(BS) void gf_decode_mixed(MixedArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Wave-pair kernel for wide codes (round 6, RS(10,4)):
+// the register kernel's memory schedule at RS(6,3) -- U = 4 chunks of 1 KiB
+// per lane and input stream, one wave-tile per queue fetch -- for K = 10,
+// whose K x U = 40 loads do not fit one wave beside its accumulators.  A
+// 128-thread block is one wave PAIR working one wave-tile together: wave w
+// loads and multiplies inputs [w K/2, (w+1) K/2) into partial sums of all R
+// rows, hands the other wave the partials of ITS rows through LDS (double-
+// buffered, one barrier per tile), XORs in the partials it receives and
+// stores its own rows (wave 0 rows [0, R0), wave 1 [R0, R), R0 = ceil(R/2)).
+// Each wave streams 5 inputs x 4 KiB (RS(6,3)'s wave streams 6), so the
+// DRAM sees the same 4-KiB runs per stream, and the GF math per wave halves
+// against one wave doing all 10 inputs.  The pair fetches its tiles from the
+// work queue (wave 0, lane 0; the next tile travels through LDS with the
+// partials), so its loop bound is block-uniform and both waves meet every
+// barrier.
+// ---------------------------------------------------------------------------
+template <int K, int R, int U>
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))) void gf_matmul_pair(MatmulArgs a) {
+    static_assert(K % 2 == 0 && K <= 2 * 8, "the pair splits an even K");
+    constexpr int KH = K / 2, R0 = (R + 1) / 2, R1 = R - R0, BS = 128;
+    __shared__ PermTable s_tab[R][K];
+    __shared__ uint8_t s_exp[512];
+    __shared__ uint8_t s_log[256];
+    __shared__ uint8_t s_coef[R * kMaxK];
+    // partials for the other wave: [buffer][row slot][u][lane]; rows [0, R0)
+    // are wave 0's (written by wave 1), rows [R0, R) wave 1's
+    __shared__ u32x4 s_part[2][R][U][64];
+    __shared__ uint32_t s_tile[2];
+    const int tid = threadIdx.x;
+    for (int t = tid; t < 256; t += BS) {
+        s_exp[t] = kDevGf.exp[t];
+        s_exp[t + 256] = kDevGf.exp[t + 256];
+        s_log[t] = kDevGf.log[t];
+    }
+    for (int t = tid; t < R * kMaxK; t += BS) s_coef[t] = a.coef[t];
+    queue_zero_next(a.queue_zero);
+    const uint32_t n = gridDim.x < kMixedQueues ? gridDim.x : kMixedQueues;
+    const uint32_t q = blockIdx.x % n;
+    uint32_t* const ctr = a.queue + q * (kMixedQueueStride / 4);
+    const uint32_t total = a.total_tiles;
+    auto tile_of = [&](uint32_t v) -> uint32_t {
+        const uint64_t t = uint64_t(v) * n + q;
+        return t < total ? uint32_t(t) : total;
+    };
+    if (tid == 0) s_tile[0] = tile_of(atomicAdd(ctr, 1u));
+    __syncthreads();
+    for (int t = tid; t < R * K; t += BS) {
+        const int j = t / K, i = t - j * K;
+        build_perm_table(&s_tab[j][i], s_coef[j * kMaxK + i], s_exp, s_log);
+    }
+    __syncthreads();
+
+    const int w = __builtin_amdgcn_readfirstlane(tid / 64);  // wave in the pair
+    const uint32_t lane = tid & 63u;
+    const uint32_t chunks = a.chunks;
+    constexpr uint32_t TILE = 64 * U;
+    uint32_t tile = uint32_t(__builtin_amdgcn_readfirstlane(int(s_tile[0])));
+    for (int buf = 0; tile < total; buf ^= 1) {
+        uint32_t stripe, tcol;
+        tile_coords(tile, a, stripe, tcol);
+        asm volatile("" ::: "memory");
+        bool live[U];
+        uint32_t offs[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint32_t col = tcol * TILE + u * 64 + lane;
+            live[u] = col < chunks;
+            offs[u] = (live[u] ? col : 0u) * 16u;
+        }
+        u32x4 x[U][KH];
+#pragma unroll
+        for (int u = 0; u < U; u++)
+#pragma unroll
+            for (int i = 0; i < KH; i++) {
+                const int ii = w * KH + i;
+                x[u][i] = load16<true>((a.in[ii] + uint64_t(stripe) * a.in_stride[ii]) + offs[u]);
+            }
+        uint32_t fetch;
+        asm volatile("" : "=v"(fetch));  // defined in every lane; lane 0's is the one used
+        if (tid == 0) fetch = atomicAdd(ctr, 1u);  // the pair's next tile, in flight while this one is coded
+        __builtin_amdgcn_sched_barrier(0);
+        u32x4 acc[U][R];
+#pragma unroll
+        for (int i = 0; i < KH; i++) {
+            uint32_t toff = uint32_t(w * KH + i) * uint32_t(sizeof(PermTable));
+            asm volatile("" : "+v"(toff));
+            if (i > 0) {
+#pragma unroll
+                for (int u = 0; u < U; u++)
+#pragma unroll
+                    for (int j = 0; j < R; j++) asm volatile("" : "+v"(acc[u][j]) : "v"(toff));
+            }
+            Sel sl[U][4];
+#pragma unroll
+            for (int u = 0; u < U; u++)
+#pragma unroll
+                for (int d = 0; d < 4; d++) sl[u][d] = make_sel(x[u][i][d]);
+#pragma unroll
+            for (int j = 0; j < R; j++) {
+                const PermTable& t =
+                    *reinterpret_cast<const PermTable*>(reinterpret_cast<const char*>(&s_tab[j][0]) + toff);
+                const uint32_t t0lo = t.t0lo, t0hi = t.t0hi, t1lo = t.t1lo, t1hi = t.t1hi, t2 = t.t2;
+#pragma unroll
+                for (int u = 0; u < U; u++)
+#pragma unroll
+                    for (int d = 0; d < 4; d++) {
+                        const uint32_t pr = gf_mul4(t0lo, t0hi, t1lo, t1hi, t2, sl[u][d].s0, sl[u][d].s1, sl[u][d].s2);
+                        acc[u][j][d] = i == 0 ? pr : (acc[u][j][d] ^ pr);
+                    }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        // hand over the other wave's rows, take the next tile, meet
+#pragma unroll
+        for (int j = 0; j < R; j++) {
+            if ((j < R0) == (w == 0)) continue;  // my own row
+#pragma unroll
+            for (int u = 0; u < U; u++) s_part[buf][j][u][lane] = acc[u][j];
+        }
+        if (tid == 0) s_tile[buf ^ 1] = tile_of(fetch);
+        __syncthreads();
+        // every partial of my rows read before the first store (one wait)
+#pragma unroll
+        for (int j = 0; j < R; j++) {
+            if ((j < R0) != (w == 0)) continue;  // the other wave's row
+#pragma unroll
+            for (int u = 0; u < U; u++) acc[u][j] ^= s_part[buf][j][u][lane];
+        }
+        if ((tcol + 1) * TILE <= chunks) {  // block-uniform: the whole tile lies inside the cell
+#pragma unroll
+            for (int j = 0; j < R; j++) {
+                if ((j < R0) != (w == 0)) continue;
+#pragma unroll
+                for (int u = 0; u < U; u++)
+                    store16<true>((a.out[j] + uint64_t(stripe) * a.out_stride[j]) + offs[u], acc[u][j]);
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < R; j++) {
+                if ((j < R0) != (w == 0)) continue;
+#pragma unroll
+                for (int u = 0; u < U; u++)
+                    if (live[u]) store16<true>((a.out[j] + uint64_t(stripe) * a.out_stride[j]) + offs[u], acc[u][j]);
+            }
+        }
+        if (a.drain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        tile = uint32_t(__builtin_amdgcn_readfirstlane(int(s_tile[buf ^ 1])));
+    }
+    (void)R1;
+}
+
+// ---------------------------------------------------------------------------
 // Unaligned layouts: 8 bytes per lane from naturally aligned dword loads.
 // A batch whose base pointers or strides are off the 16-B grid cannot take
 // the dwordx4 kernels.  Here lane g of stripe s owns bytes [8g, 8g+8) of the
@@ -1039,6 +1191,23 @@ const void* pick_wq(int k, int r, int wq, int block = 0, int unroll = 0) {
     if (k == 2 || k == 3) return wq == 2 ? wq_vec<2>(k, r) : nullptr;
     return wq == 1 ? wq_vec<1>(k, r) : nullptr;
 #endif
+}
+
+// The wave-pair kernel for k = 10 (tune key 32 = 1, measurement build).
+const void* pick_pair(int k, int r) {
+#ifdef HEC_EXPERIMENTAL
+    if (k == 10) {
+        switch (r) {
+            case 1: return reinterpret_cast<const void*>(&gf_matmul_pair<10, 1, 4>);
+            case 2: return reinterpret_cast<const void*>(&gf_matmul_pair<10, 2, 4>);
+            case 3: return reinterpret_cast<const void*>(&gf_matmul_pair<10, 3, 4>);
+            default: return reinterpret_cast<const void*>(&gf_matmul_pair<10, 4, 4>);
+        }
+    }
+#endif
+    (void)k;
+    (void)r;
+    return nullptr;
 }
 
 // Rounds of wave-tiles per atomic: same process, same buffers, 2 sets x 5
@@ -1402,8 +1571,23 @@ int launch_gf_matmul(const MatmulArgs& in, int device, hipStream_t stream) {
         // the register kernel's default shapes take the work queue (tune key
         // 27, measurement build: 1 / 2 rounds per atomic, 3 = the fixed order)
         int wq = 0;
+        bool pair = false;  // the wave-pair kernel (k = 10; tune key 32)
+        if (!fn && tn.matmul_pair == 1 && sh.nt) {
+            const void* f = pick_pair(a.k, a.r);
+            if (f) lease = queue_lease(device, stream);
+            if (f && lease) {
+                fn = f;
+                pair = true;
+                wq = 1;
+                a.queue = lease.use;
+                a.queue_zero = lease.zero;
+                sh.unroll = 4;
+                sh.block = 128;
+                if (!tn.blocks_per_cu) sh.blocks_per_cu = 4;  // two waves per SIMD
+            }
+        }
         const bool k10_256 = kExperimental && a.k == 10 && sh.block == 256 && (sh.unroll == 2 || sh.unroll == 4);  // measurement
-        if (!fn && !sh.dma && sh.nt &&
+        if (!fn && !pair && !sh.dma && sh.nt &&
             ((sh.unroll == (sh.block == 512 ? 2 : 4) && (sh.block == 512) == (a.k == 10)) || k10_256)) {
             wq = default_wq(a.k);
             if (kExperimental && tn.matmul_wq) wq = tn.matmul_wq == 3 ? 0 : tn.matmul_wq;

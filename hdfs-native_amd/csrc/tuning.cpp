@@ -15,7 +15,7 @@ namespace {
 std::atomic<int> g_cus[64];
 
 #ifdef HEC_EXPERIMENTAL
-constexpr int kKeys = 31;
+constexpr int kKeys = 32;
 std::atomic<int> g_knob[kKeys + 1];  // index = key; zero-initialised (static storage)
 std::atomic<int> g_nt{-1};           // key 2 defaults to -1 (non-temporal on)
 
@@ -58,6 +58,7 @@ Tune tune_snapshot() {
     t.crc_wq = load(29);
     t.crc_sums_nt = load(30);
     t.crc_runs = load(31);
+    t.matmul_pair = load(32);
     return t;
 }
 
@@ -99,6 +100,7 @@ int tune_store(int key, int value) {
         case 29: ok = value == 0 || value == 1 || value == 2 || value == 4 || value == 8 || value == 16; break;
         case 30: ok = value == 0 || value == 1; break;
         case 31: ok = value == 0 || value == 2 || value == 4 || value == 8 || value == 16; break;
+        case 32: ok = value == 0 || value == 1; break;
         default: ok = false;
     }
     if (!ok) return HEC_ERR_INVALID_ARG;

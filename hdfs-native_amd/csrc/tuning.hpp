@@ -53,6 +53,7 @@ struct Tune {
     int crc_wq = 0;             // key 29: CRC32C checksum kernel with the work queue (0 = off; 1 / 2 / 4 / 8 / 16 tasks per unit)
     int crc_sums_nt = 0;        // key 30: 1 = the CRC kernels store the sums non-temporal (measurement)
     int crc_runs = 0;           // key 31: CRC32C checksum kernel in runs of 2 / 4 consecutive tasks per wave (measurement)
+    int matmul_pair = 0;        // key 32: 1 = the wave-pair register kernel for k = 10 (measurement)
     int mixed_wq = 0;           // key 26: mixed decode work queue of wave-tiles (0 = default: 1 round of wave-tiles per atomic for k >= 6, 4 below; 1 / 2 / 4 forced; 3 = the fixed tile order)
 };
 

@@ -50,7 +50,8 @@ EXPORTS = [
     "hec_decode_verify_device", "hec_group_create", "hec_group_destroy", "hec_group_size", "hec_group_coder",
     "hec_group_range", "hec_group_encode_host_batch", "hec_group_decode_host_batch", "hec_group_encode_device",
     "hec_group_decode_device",
-    "hec_device_alloc", "hec_device_free", "hec_device_numa_node", "hec_host_alloc", "hec_host_free",
+    "hec_device_alloc", "hec_device_free", "hec_device_copy", "hec_device_synchronize", "hec_device_numa_node",
+    "hec_host_alloc", "hec_host_free",
     "hec_coder_acquire", "hec_coder_release", "hec_coder_pool_trim", "hec_coder_set_host_limit",
     "hec_coder_host_limit", "hec_gf_matmul_host", "hec_host_isa", "hec_encode_rows_host",
     "hec_coder_prepare_decode", "hec_jit_warm", "hec_jit_stats", "hec_queue_stats",
@@ -148,6 +149,8 @@ def _load(path: str = LIB_PATH) -> ctypes.CDLL:
         "hec_device_alloc": ([I, S, ctypes.c_uint, ctypes.POINTER(P)], I),
         "hec_device_free": ([I, P], I),
         "hec_device_numa_node": ([I], I),
+        "hec_device_copy": ([I, P, P, S], I),
+        "hec_device_synchronize": ([I, P], I),
         "hec_host_alloc": ([I, S, I, ctypes.POINTER(P)], I),
         "hec_host_free": ([P], I),
         "hec_coder_acquire": ([ctypes.c_char_p, S, S, I, ctypes.POINTER(P)], I),

@@ -457,6 +457,13 @@ int hec_group_decode_device(hec_group_t *group, const uint8_t *const *d_shards, 
 #define HEC_ALLOC_CONTIGUOUS 1
 int hec_device_alloc(int device, size_t bytes, unsigned flags, void **out);
 int hec_device_free(int device, void *ptr);
+/* hec_device_copy: `bytes` from src to dst, host or device memory either
+ * side (unified addressing), synchronous; for callers without a HIP binding
+ * of their own (the Rust shim's DeviceBuffer).  hec_device_synchronize: wait
+ * for `hip_stream` on `device` (NULL = the device's default stream) -- the
+ * device calls above only enqueue. */
+int hec_device_copy(int device, void *dst, const void *src, size_t bytes);
+int hec_device_synchronize(int device, void *hip_stream);
 
 /* ---- NUMA-placed pinned host buffers (host-batch / group calls) -------- *
  * hec_host_alloc: `bytes` of page-locked host memory whose pages live on

@@ -74,6 +74,20 @@
  *         last input's CRC round
  * key 25: fused kernels: stripe s starts its tile columns at (s * value) mod
  *         the tiles per stripe (0 = default, no rotation; up to 4096)
+ * key 26: mixed-pattern decode work queue: 0 = default (1 round of wave-tiles
+ *         per atomic for k >= 6, 4 below); 1 / 2 / 4 forced; 3 = fixed order
+ * key 27: register kernel work queue: 0 = default (2 rounds per atomic for
+ *         k <= 3, 1 for k = 6, 10); 1 / 2 forced; 3 = the fixed tile order
+ * key 28: fused kernels' work queue: 0 = default (encode + CRC at k = 3, 10,
+ *         decode + verify at every k); 1 = everywhere; 2 = block tiles
+ * key 29: CRC32C checksum kernel on the work queue, 1 / 2 / 4 / 8 / 16 tasks
+ *         per unit (0 = default: the fixed order)
+ * key 30: 1 = the CRC kernels store their sums non-temporal
+ * key 31: CRC32C checksum kernel in runs of 2 / 4 / 8 / 16 consecutive tasks
+ *         of one cell per wave (fixed order)
+ * key 32: 1 = the wave-pair register kernel for k = 10 (gf_matmul_pair: two
+ *         waves per wave-tile, 5 inputs each, partials exchanged in LDS);
+ *         key 3 sets its 128-thread blocks per CU (0 = 4: two waves per SIMD)
  * Returns HEC_OK, or HEC_ERR_INVALID_ARG for an unknown key / value.
  */
 #ifndef HDFS_EC_AMD_EXP_H

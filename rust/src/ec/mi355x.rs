@@ -28,7 +28,9 @@
 //! at a time on pageable cells, which the engine codes with its host routine
 //! (DESIGN.md §1 measures the device route at those call shapes: it loses).
 //! `GpuCoder::encode_rows` / `decode_rows` are the pinned-memory batched
-//! forms for callers that hold many rows at once (a reconstruct worker).
+//! forms for callers that hold many rows at once (a reconstruct worker);
+//! `GpuCoder::encode_device` / `decode_device` with `DeviceBuffer` the
+//! device-resident forms (the patch's `mi355x` group of rust/benches/ec.rs).
 
 use std::ffi::{c_char, c_int, c_void, CStr};
 
@@ -78,6 +80,16 @@ unsafe extern "C" {
                                 shard_strides: *const usize, d_out: *const *mut u8, out_strides: *const usize,
                                 cell_len: usize, stripes: usize, bytes_per_checksum: usize, d_sums: *const u8,
                                 d_bad: *mut u8, stream: *mut c_void) -> c_int;
+    fn hec_encode_device(c: *mut HecCoder, d_data: *const *const u8, data_strides: *const usize,
+                         d_parity: *const *mut u8, parity_strides: *const usize, cell_len: usize, stripes: usize,
+                         stream: *mut c_void) -> c_int;
+    fn hec_decode_device(c: *mut HecCoder, d_shards: *const *const u8, shard_strides: *const usize,
+                         d_out: *const *mut u8, out_strides: *const usize, cell_len: usize, stripes: usize,
+                         stream: *mut c_void) -> c_int;
+    fn hec_device_alloc(device: c_int, bytes: usize, flags: u32, out: *mut *mut c_void) -> c_int;
+    fn hec_device_free(device: c_int, ptr: *mut c_void) -> c_int;
+    fn hec_device_copy(device: c_int, dst: *mut c_void, src: *const c_void, bytes: usize) -> c_int;
+    fn hec_device_synchronize(device: c_int, stream: *mut c_void) -> c_int;
     fn hec_group_create(codec: *const c_char, k: usize, m: usize, devices: *const c_int, n_devices: usize,
                         out: *mut *mut HecGroup) -> c_int;
     fn hec_group_destroy(g: *mut HecGroup);
@@ -119,6 +131,7 @@ pub struct GpuCoder {
     raw: *mut HecCoder,
     data_units: usize,
     parity_units: usize,
+    device: i32,
 }
 
 unsafe impl Send for GpuCoder {}
@@ -131,7 +144,59 @@ impl GpuCoder {
         let name = std::ffi::CString::new(codec).map_err(|_| HdfsError::InvalidArgument(codec.to_string()))?;
         let mut raw = std::ptr::null_mut();
         check(unsafe { hec_coder_create_codec(name.as_ptr(), data_units, parity_units, device, &mut raw) })?;
-        Ok(Self { raw, data_units, parity_units })
+        Ok(Self { raw, data_units, parity_units, device })
+    }
+
+    /// The coder's device ordinal.
+    pub fn device(&self) -> i32 {
+        self.device
+    }
+
+    /// Batched `Coder::encode` on stripes already in HBM (`hec_encode_device`):
+    /// shard i of stripe s at `data[i] + s * data_strides[i]`, parity row j at
+    /// `parity[j] + s * parity_strides[j]`; enqueued on `stream` (null = the
+    /// device's default stream), complete after `synchronize`.
+    ///
+    /// # Safety
+    /// Device pointers valid for `stripes` cells of `cell` bytes in that
+    /// layout, on this coder's device; `stream` belongs to it.
+    #[allow(clippy::too_many_arguments)]
+    pub unsafe fn encode_device(&self, data: &[*const u8], data_strides: &[usize], parity: &[*mut u8],
+                                parity_strides: &[usize], cell: usize, stripes: usize,
+                                stream: *mut c_void) -> Result<()> {
+        let (k, m) = (self.data_units, self.parity_units);
+        assert!(data.len() == k && data_strides.len() == k, "one slot per data shard");
+        assert!(parity.len() == m && parity_strides.len() == m, "one slot per parity shard");
+        check(unsafe {
+            hec_encode_device(self.raw, data.as_ptr(), data_strides.as_ptr(), parity.as_ptr(),
+                              parity_strides.as_ptr(), cell, stripes, stream)
+        })
+    }
+
+    /// Batched `Coder::decode` on stripes already in HBM (`hec_decode_device`),
+    /// one erasure pattern for the batch: `shards[k+m]` (null = missing),
+    /// missing data shard i rebuilt into `out[i]` (the other `out` slots are
+    /// never written; null is fine there).  `Err(ErasureCodingError)` when
+    /// fewer than k shards are present.
+    ///
+    /// # Safety
+    /// As `encode_device`.
+    #[allow(clippy::too_many_arguments)]
+    pub unsafe fn decode_device(&self, shards: &[*const u8], shard_strides: &[usize], out: &[*mut u8],
+                                out_strides: &[usize], cell: usize, stripes: usize,
+                                stream: *mut c_void) -> Result<()> {
+        let (k, m) = (self.data_units, self.parity_units);
+        assert!(shards.len() == k + m && shard_strides.len() == k + m, "one slot per shard");
+        assert!(out.len() == k && out_strides.len() == k, "one output slot per data shard");
+        check(unsafe {
+            hec_decode_device(self.raw, shards.as_ptr(), shard_strides.as_ptr(), out.as_ptr(), out_strides.as_ptr(),
+                              cell, stripes, stream)
+        })
+    }
+
+    /// Waits for `stream` (null = the default stream) on the coder's device.
+    pub fn synchronize(&self, stream: *mut c_void) -> Result<()> {
+        check(unsafe { hec_device_synchronize(self.device, stream) })
     }
 
     /// `Coder::encode` (gf256.rs:61-80): m freshly allocated parity shards.
@@ -217,6 +282,59 @@ impl GpuCoder {
             hec_decode_verify_device(self.raw, checksum_type, shards.as_ptr(), strides.as_ptr(), out.as_ptr(),
                                      out_strides.as_ptr(), cell, rows, bytes_per_checksum, sums, bad, stream)
         })
+    }
+}
+
+/// HBM on one device (`hec_device_alloc`), freed on drop: the stripe
+/// buffers of `encode_device` / `decode_device` for a caller (the `mi355x`
+/// Criterion group of rust/benches/ec.rs) with no HIP binding of its own.
+pub struct DeviceBuffer {
+    device: i32,
+    ptr: *mut u8,
+    len: usize,
+}
+
+unsafe impl Send for DeviceBuffer {}
+unsafe impl Sync for DeviceBuffer {}
+
+impl DeviceBuffer {
+    pub fn new(device: i32, len: usize) -> Result<Self> {
+        let mut p = std::ptr::null_mut();
+        check(unsafe { hec_device_alloc(device, len, 0, &mut p) })?;
+        Ok(Self { device, ptr: p.cast(), len })
+    }
+
+    /// A buffer holding a copy of `host`.
+    pub fn upload(device: i32, host: &[u8]) -> Result<Self> {
+        let b = Self::new(device, host.len())?;
+        check(unsafe { hec_device_copy(device, b.ptr.cast(), host.as_ptr().cast(), host.len()) })?;
+        Ok(b)
+    }
+
+    /// Copies the buffer into `host` (`host.len()` bytes from its start).
+    pub fn download(&self, host: &mut [u8]) -> Result<()> {
+        assert!(host.len() <= self.len, "read past the buffer");
+        check(unsafe { hec_device_copy(self.device, host.as_mut_ptr().cast(), self.ptr.cast(), host.len()) })
+    }
+
+    /// Device address of byte `off`.
+    pub fn at(&self, off: usize) -> *mut u8 {
+        assert!(off <= self.len, "offset past the buffer");
+        self.ptr.wrapping_add(off)
+    }
+
+    pub fn len(&self) -> usize {
+        self.len
+    }
+
+    pub fn is_empty(&self) -> bool {
+        self.len == 0
+    }
+}
+
+impl Drop for DeviceBuffer {
+    fn drop(&mut self) {
+        unsafe { hec_device_free(self.device, self.ptr.cast()) };
     }
 }
 

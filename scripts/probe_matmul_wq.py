@@ -53,6 +53,14 @@ if K10:
     VARIANTS = [("512 x1/CU", [(27, 1)]), ("256 U4 x1/CU", [(27, 1), (4, 256), (1, 4)]),
                 ("256 U4 x2/CU", [(27, 1), (4, 256), (1, 4), (3, 2)]), ("256 x2/CU", [(27, 1), (4, 256), (1, 2), (3, 2)])]
 
+# PROBE_PAIR=1 (round 6): RS(10,4) on the wave-pair kernel (tune key 32 = 1:
+# two waves per wave-tile, 5 inputs x 4 KiB each, partials exchanged in LDS)
+# at 4 and 2 blocks of 128 threads per CU against the 512-thread default
+if os.environ.get("PROBE_PAIR") == "1":
+    CONFIGS = [(10, 4, 256), (10, 4, 1024)]
+    VARIANTS = [("512 x1/CU", [(27, 0)]), ("pair x4/CU", [(32, 1)]), ("pair x2/CU", [(32, 1), (3, 2)]),
+                ("pair x3/CU", [(32, 1), (3, 3)])]
+
 
 def main():
     dev = torch.device("cuda:0")

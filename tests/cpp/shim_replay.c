@@ -23,6 +23,9 @@
  *                        (HEC_DEVICE_HOST); decode reads only the first k
  *                        present shards (a shorter shard past them is fine,
  *                        matrix.rs:212-216)
+ *   the patch's device group of rust/benches/ec.rs (bench_mi355x) ->
+ *                        hec_device_alloc / hec_device_copy, hec_encode_device
+ *                        / hec_decode_device + hec_device_synchronize
  * The host-only part runs first and needs no GPU (exit 2 after it when no
  * device is visible).  Built by __graft_entry__.build(); run by
  * tests/test_shim_replay.py. */
@@ -423,6 +426,87 @@ static void host_only_replay(void) {
     printf("host-only replay %s\n", failures ? "FAILED" : "ok");
 }
 
+/* The patch's `mi355x` Criterion group of rust/benches/ec.rs (bench_mi355x),
+ * call for call: GpuCoder::new -> hec_coder_create_codec; DeviceBuffer::upload
+ * / new -> hec_device_alloc + hec_device_copy; the reference bench's six
+ * 16 MiB slices (big-endian i32 counters, v + i * slice_size) in one HBM
+ * image; encode_device + synchronize -> hec_encode_device (1 stripe, default
+ * stream) + hec_device_synchronize; decode with 1, 2, 3 data slices missing
+ * -> hec_decode_device + hec_device_synchronize; DeviceBuffer::download ->
+ * hec_device_copy.  Parity against the oracle, rebuilt slices against the
+ * originals; each leg timed over its iterations (Criterion's Throughput::
+ * Bytes(slice_size * 6)). */
+static void replay_bench_device(void) {
+    enum { SLICE = 16 << 20, ENC_IT = 30, DEC_IT = 10 };
+    hec_coder_t *c = NULL;
+    int rc = hec_coder_create_codec("rs", K, M, 0, &c);
+    CHECK(rc == HEC_OK, "bench coder %s", hec_strerror(rc));
+    if (rc != HEC_OK) return;
+    uint8_t *host = malloc((size_t)K * SLICE), *hpar = malloc((size_t)M * SLICE), *want[M];
+    for (int i = 0; i < K; i++)
+        for (uint32_t v = 0; v < SLICE / 4; v++) {
+            const uint32_t x = v + (uint32_t)i * SLICE; /* put_i32: big-endian */
+            uint8_t *q = host + (size_t)i * SLICE + 4 * (size_t)v;
+            q[0] = (uint8_t)(x >> 24), q[1] = (uint8_t)(x >> 16), q[2] = (uint8_t)(x >> 8), q[3] = (uint8_t)x;
+        }
+    const uint8_t *hin[K];
+    for (int i = 0; i < K; i++) hin[i] = host + (size_t)i * SLICE;
+    for (int j = 0; j < M; j++) want[j] = malloc(SLICE);
+    CHECK(orc_encode(K, M, hin, SLICE, want) == 0, "oracle encode of the bench slices");
+    void *data = NULL, *parity = NULL, *rebuilt = NULL;
+    CHECK(hec_device_alloc(0, (size_t)K * SLICE, 0, &data) == HEC_OK, "alloc data");
+    CHECK(hec_device_alloc(0, (size_t)M * SLICE, 0, &parity) == HEC_OK, "alloc parity");
+    CHECK(hec_device_alloc(0, (size_t)M * SLICE, 0, &rebuilt) == HEC_OK, "alloc rebuilt");
+    if (data && parity && rebuilt) {
+        CHECK(hec_device_copy(0, data, host, (size_t)K * SLICE) == HEC_OK, "upload");
+        const uint8_t *d[K];
+        uint8_t *p[M];
+        size_t strides[K + M];
+        for (int i = 0; i < K; i++) d[i] = (const uint8_t *)data + (size_t)i * SLICE;
+        for (int j = 0; j < M; j++) p[j] = (uint8_t *)parity + (size_t)j * SLICE;
+        for (int i = 0; i < K + M; i++) strides[i] = (size_t)(K + M) * SLICE; /* one stripe: any stride */
+        double t0 = now_us();
+        for (int it = 0; it < ENC_IT; it++) {
+            rc = hec_encode_device(c, d, strides, p, strides, SLICE, 1, NULL);
+            if (rc == HEC_OK) rc = hec_device_synchronize(0, NULL);
+            if (rc != HEC_OK) break;
+        }
+        const double enc_us = (now_us() - t0) / ENC_IT;
+        CHECK(rc == HEC_OK, "encode_device %s", hec_strerror(rc));
+        CHECK(hec_device_copy(0, hpar, parity, (size_t)M * SLICE) == HEC_OK, "download parity");
+        for (int j = 0; j < M; j++) CHECK(memcmp(hpar + (size_t)j * SLICE, want[j], SLICE) == 0, "bench parity %d", j);
+        double dec_us[4] = {0};
+        for (int lost = 1; lost <= 3; lost++) {
+            const uint8_t *sh[K + M];
+            uint8_t *out[K];
+            for (int i = 0; i < K + M; i++) sh[i] = i < lost ? NULL : (i < K ? d[i] : p[i - K]);
+            for (int i = 0; i < K; i++) out[i] = i < lost ? (uint8_t *)rebuilt + (size_t)i * SLICE : NULL;
+            t0 = now_us();
+            for (int it = 0; it < DEC_IT; it++) {
+                rc = hec_decode_device(c, sh, strides, out, strides, SLICE, 1, NULL);
+                if (rc == HEC_OK) rc = hec_device_synchronize(0, NULL);
+                if (rc != HEC_OK) break;
+            }
+            dec_us[lost] = (now_us() - t0) / DEC_IT;
+            CHECK(rc == HEC_OK, "decode_device (%d lost) %s", lost, hec_strerror(rc));
+            CHECK(hec_device_copy(0, hpar, rebuilt, (size_t)lost * SLICE) == HEC_OK, "download rebuilt");
+            CHECK(memcmp(hpar, host, (size_t)lost * SLICE) == 0, "decode-%d-slice: rebuilt != originals", lost);
+        }
+        const double gib = (double)K * SLICE / (1024.0 * 1024.0 * 1024.0);
+        printf("bench ec.rs mi355x group (6 x 16 MiB, device-resident, per iteration incl. sync): "
+               "encode %.1f us = %.1f GiB/s; decode-1/2/3-slice %.1f / %.1f / %.1f us = %.1f / %.1f / %.1f GiB/s\n",
+               enc_us, gib / (enc_us * 1e-6), dec_us[1], dec_us[2], dec_us[3], gib / (dec_us[1] * 1e-6),
+               gib / (dec_us[2] * 1e-6), gib / (dec_us[3] * 1e-6));
+    }
+    hec_device_free(0, data);
+    hec_device_free(0, parity);
+    hec_device_free(0, rebuilt);
+    hec_coder_destroy(c);
+    free(host);
+    free(hpar);
+    for (int j = 0; j < M; j++) free(want[j]);
+}
+
 int main(void) {
     CHECK(hec_abi_version() == 5, "ABI %d", hec_abi_version());
     host_only_replay();
@@ -612,6 +696,8 @@ int main(void) {
     hec_coder_set_host_limit(c, 256 << 10);
     replay_batched_writer(c, 1 << 20, 4 * K * (1 << 20) + 3 * (1 << 20) + 11);
     replay_batched_reader(c, 1 << 20, ROWS_PER_CALL, 0, 1);
+
+    replay_bench_device();
 
     hec_coder_destroy(c);
     for (int i = 0; i < K; i++) free(data[i]);

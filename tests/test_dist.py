@@ -130,7 +130,8 @@ def test_bench_gpus_flag_spawns_ranks(args, want_S, want_global, scaling):
     # the other multi-GPU BASELINE configs are timed by the same invocation,
     # each split over the ranks (bench.py --extra-configs)
     ex = d["extra_configs"]
-    assert set(ex) == {"rs104_1MiB_x2048", "rs63_64KiB_x65536"}
+    assert set(ex) == {"rs63_1MiB_x1024_strong", "rs104_1MiB_x2048", "rs63_64KiB_x65536"}
+    assert ex["rs63_1MiB_x1024_strong"]["stripes_per_gpu_rank0"] == 512
     assert ex["rs104_1MiB_x2048"]["stripes_per_gpu_rank0"] == 1024
     assert ex["rs104_1MiB_x2048"]["stripes_summed_over_ranks"] == 2048
     assert ex["rs63_64KiB_x65536"]["stripes_per_gpu_rank0"] == 32768
@@ -159,3 +160,33 @@ def test_bench_refuses_more_nccl_ranks_than_gpus():
     assert out.returncode != 0
     assert "refusing" in out.stderr and "one rank per GPU" in out.stderr
     assert not [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_bench_dry_run_world_8():
+    """The 8-GPU line's plumbing at world 8 (gloo, no GPU): `bench.py --gpus 8
+    --dry-run` starts 8 ranks that rendezvous over loopback and print ONE
+    line whose shard tables tile every batch in rank order -- the weak
+    headline (1024 stripes per rank), its strong twin (1024 in all, 128 per
+    rank) and the two other BASELINE configs -- and whose `ranks` list holds
+    all 8 ranks."""
+    import subprocess
+    from conftest import ROOT
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["OMP_NUM_THREADS"] = "1"
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--backend", "gloo",
+                          "--dry-run"], capture_output=True, text=True, timeout=400, env=env, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 8 and d["scaling"] == "weak"
+    assert d["config"]["shards"] == [[1024 * r, 1024] for r in range(8)]
+    assert d["config"]["global_stripes"] == 8192
+    want = {"rs63_1MiB_x1024_strong": 1024, "rs104_1MiB_x2048": 2048, "rs63_64KiB_x65536": 65536}
+    assert set(d["extra_configs"]) == set(want)
+    for name, total in want.items():
+        assert d["extra_configs"][name]["shards"] == [[r * total // 8, total // 8] for r in range(8)], name
+        assert d["extra_configs"][name]["stripes_summed_over_ranks"] == total
+    assert [r["rank"] for r in d["ranks"]] == list(range(8))
+    assert [r["local_rank"] for r in d["ranks"]] == list(range(8))
+    assert d["process_group"]["world_size"] == 8

@@ -13,6 +13,7 @@ from conftest import ROOT
 
 REF_EC = "/root/reference/rust/src/ec"
 REF_HDFS = "/root/reference/rust/src/hdfs"
+REF_BENCH = "/root/reference/rust/benches/ec.rs"
 PATCH = os.path.join(ROOT, "rust", "patches", "ec_mi355x.patch")
 SHIM = os.path.join(ROOT, "rust", "src", "ec", "mi355x.rs")
 HEADER = os.path.join(ROOT, "include", "hdfs_ec_amd.h")
@@ -28,6 +29,8 @@ def test_forwarding_patch_applies_to_reference(tmp_path):
         shutil.copy(os.path.join(REF_EC, name), ec / name)
     for name in ("mod.rs", "block_writer.rs", "block_reader.rs"):
         shutil.copy(os.path.join(REF_HDFS, name), hd / name)
+    (tmp_path / "rust" / "benches").mkdir()
+    shutil.copy(REF_BENCH, tmp_path / "rust" / "benches" / "ec.rs")
     r = subprocess.run(["patch", "-p1", "--dry-run", "-i", PATCH], cwd=tmp_path, capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
     r = subprocess.run(["patch", "-p1", "-i", PATCH], cwd=tmp_path, capture_output=True, text=True)
@@ -49,7 +52,18 @@ def test_forwarding_patch_applies_to_reference(tmp_path):
     for name in ("mod.rs", "block_writer.rs", "block_reader.rs"):
         assert (hd / name).read_text() == open(os.path.join(REF_HDFS, name)).read(), name
     patched = {ln[6:].strip() for ln in open(PATCH) if ln.startswith("+++ b/")}
-    assert patched == {"rust/src/ec/gf256.rs", "rust/src/ec/mod.rs"}, patched
+    assert patched == {"rust/src/ec/gf256.rs", "rust/src/ec/mod.rs", "rust/benches/ec.rs"}, patched
+    # the reference's Criterion bench gains a device-resident group (features
+    # benchmark + mi355x) beside its own, which stays as it was: the same
+    # 6 x 16 MiB slices, encode and decode 1 / 2 / 3 missing through GpuCoder
+    bench = (tmp_path / "rust" / "benches" / "ec.rs").read_text()
+    ref = open(REF_BENCH).read()
+    assert bench.startswith(ref[:ref.index("criterion_group!")])
+    assert "fn bench_mi355x(c: &mut Criterion)" in bench
+    assert 'benchmark_group("rs-encode-mi355x")' in bench and 'benchmark_group("rs-decode-mi355x")' in bench
+    assert "coder.encode_device(" in bench and "coder.decode_device(" in bench
+    assert "criterion_group!(benches, bench, bench_mi355x);" in bench
+    assert '#[cfg(not(feature = "mi355x"))]\ncriterion_group!(benches, bench);' in bench
     assert not os.path.exists(os.path.join(ROOT, "rust", "src", "hdfs", "ec_rows.rs"))
 
 
