@@ -116,15 +116,20 @@ struct CrcShape : crcdev::TableLayout<SCHEME> {
 // WQ > 0 (PF = 1 only): tasks come from the work queue of wave-tiles
 // (work_queue.hpp, a.queue) in units of WQ consecutive tasks of one cell,
 // one unit per atomic; the next task is still loaded during this one.
-template <int KIND, int SCHEME, int PF, int WQ = 0>
-__global__ __launch_bounds__(CrcShape<SCHEME>::kBlock) void checksum_chunks512(CrcArgs a) {
+// BLK > 0 (measurement, tune key 33): BLK-thread blocks instead of the
+// scheme's; 768 = one block per CU with the tables staged once for 12 waves
+// (3 per SIMD, 149.5 KiB of LDS), 50 % more tasks in flight than two
+// 256-thread blocks.
+template <int KIND, int SCHEME, int PF, int WQ = 0, int BLK = 0>
+__global__ __launch_bounds__(BLK ? BLK : CrcShape<SCHEME>::kBlock) void checksum_chunks512(CrcArgs a) {
     static_assert(WQ == 0 || PF == 1, "the queue (and the runs, WQ < 0) run one task of prefetch");
     using Sh = CrcShape<SCHEME>;
     using Spec = crc::Spec<KIND>;
     constexpr bool REFL = Spec::kReflected;
-    constexpr int CH = 512, Q = CH / 4, PITCH = Q + 16, STAGE = 64 * PITCH, BS = Sh::kBlock;
+    constexpr int CH = 512, Q = CH / 4, PITCH = Q + 16, STAGE = 64 * PITCH, BS = BLK ? BLK : Sh::kBlock;
+    constexpr int WAVES = BS / 64;
     __shared__ uint32_t s_tables[Sh::kWords];
-    __shared__ __attribute__((aligned(16))) uint8_t s_stage[Sh::kWaves * STAGE];
+    __shared__ __attribute__((aligned(16))) uint8_t s_stage[WAVES * STAGE];
     uint32_t* s_main = s_tables;
     crcdev::stage_tables<SCHEME, BS>(s_tables, tables<KIND>());
     __syncthreads();
@@ -135,7 +140,7 @@ __global__ __launch_bounds__(CrcShape<SCHEME>::kBlock) void checksum_chunks512(C
     uint8_t* stage = s_stage + wave * STAGE;
     const uint64_t groups = a.groups_per_cell;
     const uint64_t tasks = groups * a.n_shards * a.stripes;
-    const uint64_t step = uint64_t(gridDim.x) * Sh::kWaves;
+    const uint64_t step = uint64_t(gridDim.x) * WAVES;
 
     // stage v (task's data), refill v with task `next`'s loads, checksum
     auto run_task = [&](uint64_t task, u32x4 (&v)[8], uint64_t next) {
@@ -203,7 +208,7 @@ __global__ __launch_bounds__(CrcShape<SCHEME>::kBlock) void checksum_chunks512(C
         // tasks of one cell per wave, so a wave writes whole lines of sums
         constexpr uint64_t SEQ = uint64_t(-WQ);
         const uint64_t wstep = SEQ * step;
-        uint64_t task = (uint64_t(blockIdx.x) * Sh::kWaves + wave) * SEQ;
+        uint64_t task = (uint64_t(blockIdx.x) * WAVES + wave) * SEQ;
         auto next_of = [&](uint64_t t) { return (t % SEQ) != SEQ - 1 ? t + 1 : t - (SEQ - 1) + wstep; };
         u32x4 v[8];
         if (task < tasks) load_task(a, groups, task, lane, v);
@@ -216,7 +221,7 @@ __global__ __launch_bounds__(CrcShape<SCHEME>::kBlock) void checksum_chunks512(C
     }
     // PF register sets in flight: task t's loads are issued while task t-PF
     // is checksummed
-    uint64_t task = uint64_t(blockIdx.x) * Sh::kWaves + wave;
+    uint64_t task = uint64_t(blockIdx.x) * WAVES + wave;
     u32x4 va[8], vb[8];
     if (task < tasks) load_task(a, groups, task, lane, va);
     if (PF == 2 && task + step < tasks) load_task(a, groups, task + step, lane, vb);
@@ -600,6 +605,15 @@ int launch_checksum(const CrcArgs& in, int device, hipStream_t stream) {
         if (grid > cap) grid = cap;
         const void* fn = a.kind == crc::kCrc32c ? crc_pick<crc::kCrc32c>(scheme, pf) : crc_pick<crc::kCksum>(scheme, pf);
 #ifdef HEC_EXPERIMENTAL
+        // tune key 33 = 768: the fold kernel (CRC32C, one task of prefetch) in
+        // one 768-thread block per CU, 3 waves per SIMD
+        if (tn.crc_block == 768 && scheme == 12 && a.kind == crc::kCrc32c && pf == 1 && !tn.crc_runs && !tn.crc_wq) {
+            fn = reinterpret_cast<const void*>(&checksum_chunks512<crc::kCrc32c, 12, 1, 0, 768>);
+            const uint64_t g = (tasks + 11) / 12;
+            grid = g < uint64_t(cus) ? g : uint64_t(cus);
+            e = hipLaunchKernel(fn, dim3(uint32_t(grid)), dim3(768), args, 0, stream);
+            return e == hipSuccess ? 0 : int(e);
+        }
         // tune key 31: the fold kernel in runs of 2 / 4 consecutive tasks per wave
         if (tn.crc_runs && scheme == 12 && a.kind == crc::kCrc32c && pf == 1) {
             const void* f = crc_pick<crc::kCrc32c>(12, -100 - tn.crc_runs);

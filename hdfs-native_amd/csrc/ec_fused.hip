@@ -24,228 +24,9 @@
 
 namespace hec {
 
-#ifdef HEC_EXPERIMENTAL
-// Role-split variant: one 512-thread block per CU, waves 0-3 are GF waves and
-// waves 4-7 CRC waves; wave w and w + 4 share a SIMD (a workgroup's waves go
-// to the SIMDs cyclically), so every SIMD always holds one wave issuing the
-// VALU-heavy GF math and one issuing the LDS-heavy lookups, instead of two
-// waves that alternate between the phases.  A pair owns 8 KiB of every cell
-// of the stripe (as SLABS = 8) and two 9-KiB images: in round n the GF wave
-// loads / multiplies / stages shard n into image n & 1 (parity rounds store
-// and stage an output) while the CRC wave checksums round n - 1 from the
-// other image; one block barrier ends a round.  Rounds run on across tiles;
-// a last round flushes the CRC of the block's last tile.  Every wave runs
-// the same rounds and barriers, whatever its role.
-// Rejected (same-box A/B, profiles/r02g/probe_split_rs*.log): RS(6,3) x 1024
-// encode + CRC 2.68 vs 2.23 ms, decode + verify 2.27-2.33 vs 2.08 ms; RS(10,4)
-// x 512 2.23-2.28 vs 1.96 ms and 1.98-2.09 vs 1.84 ms.  One CRC wave per SIMD
-// cannot keep the table lookups in flight (ds_read_b32 needs ~4 waves per
-// SIMD for its full rate), and the per-round barrier exposes the GF wave's
-// load latency.  Measurement build: RS(6,3) and RS(10,4) only.
-template <int K, int R, int KIND, bool VERIFY, bool PRIO>
-__global__ __launch_bounds__(512) void gf_fused_crc_split(MatmulArgs a, FusedCrcArgs cs) {
-    constexpr int SCHEME = 11;
-    using TL = crcdev::TableLayout<SCHEME>;
-    using Spec = crc::Spec<KIND>;
-    constexpr bool REFL = Spec::kReflected;
-    constexpr int BS = 512, SLABS = 8, PITCH = 144, STAGE = 64 * PITCH;
-    constexpr int NSUM = VERIFY ? K : K + R;
-    constexpr uint32_t WAVE_BYTES = SLABS * 1024u, TILE_BYTES = 4u * WAVE_BYTES;
-    __shared__ PermTable s_tab[R][K];
-    __shared__ uint8_t s_exp[512];
-    __shared__ uint8_t s_log[256];
-    __shared__ uint8_t s_coef[R * kMaxK];
-    __shared__ uint32_t s_ctabs[TL::kWords];
-    __shared__ __attribute__((aligned(16))) uint8_t s_stage[4][2][STAGE];
-    prologue<R, BS, K>(a, K, s_tab, s_exp, s_log, s_coef);
-    crcdev::stage_tables<SCHEME, BS>(s_ctabs, fused_tables<KIND>());
-    __syncthreads();
-    const uint32_t kfinal = fused_tables<KIND>().final512;
-
-    const uint64_t cell_len = a.cell_len;
-    const uint64_t nck = (cell_len + 511) / 512;
-    const uint32_t total = a.total_tiles;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / 64), lane = threadIdx.x & 63;
-    const bool gf = wave < 4;
-    const int pw = wave & 3;
-    if constexpr (PRIO) {
-        if (!gf) __builtin_amdgcn_s_setprio(1);
-    }
-    // CRC role: this lane's quarter row = lane = (slab lane/8, half (lane/4)&1, quarter lane&3)
-    const int qi = lane & 3, pslab = lane >> 3, half = (lane >> 2) & 1;
-    uint32_t* out_sums = reinterpret_cast<uint32_t*>(cs.sums);
-    const uint32_t* exp_sums = reinterpret_cast<const uint32_t*>(cs.expected);
-
-    // LDS writes of this wave done, then the block barrier (no vmcnt wait:
-    // the GF wave's loads and stores stay in flight across rounds)
-    auto round_end = [&]() {
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    };
-
-    // CRC of one staged round: shard `sh` of stripe `stripe`, wave bytes from `wbyte`
-    auto crc_round = [&](const uint8_t* img, uint32_t stripe, uint64_t wbyte, int sh) {
-        const uint64_t cbyte = wbyte + uint64_t(pslab) * 1024u + uint64_t(half) * 512u;
-        const bool in_cell = cbyte < cell_len;
-        const bool full = in_cell && cell_len - cbyte >= 512u;
-        const uint64_t cell = VERIFY ? uint64_t(stripe) * cs.n_total + cs.shard_id[sh]
-                                     : uint64_t(stripe) * (K + R) + uint64_t(sh);
-        uint32_t want = 0;
-        if (VERIFY && in_cell && qi == 0) want = exp_sums[cell * nck + cbyte / 512];
-        uint32_t val = 0;
-        if (full) {
-            uint32_t r = crcdev::quarter<SCHEME, REFL>(s_ctabs, img + lane * PITCH, lane);
-            if (qi < 3) r = crcdev::shift_quarter<SCHEME>(s_ctabs, qi, r);
-            val = r;
-        } else if (in_cell && qi == 0) {
-            const uint32_t len = uint32_t(cell_len - cbyte);
-            uint32_t r = Spec::kInit;
-            for (uint32_t b = 0; b < len; b++)
-                r = crcdev::byte_step<REFL, crcdev::ByteTable<SCHEME>::stride, crcdev::ByteTable<SCHEME>::bswap>(
-                    s_ctabs + crcdev::ByteTable<SCHEME>::off, r, img[(lane + b / 128) * PITCH + (b % 128)]);
-            val = r ^ Spec::kXorout;
-        }
-        val ^= __shfl_xor(val, 1);
-        val ^= __shfl_xor(val, 2);
-        if (in_cell && qi == 0) {
-            const uint32_t be = __builtin_bswap32(full ? (val ^ kfinal) : val);
-            if constexpr (VERIFY) {
-                if (be != want) cs.bad[cell] = 1;
-            } else {
-                out_sums[cell * nck + cbyte / 512] = be;
-            }
-        }
-    };
-    auto stage_piece = [&](uint8_t* img, int u, const u32x4& v) {
-        *reinterpret_cast<u32x4*>(img + (8 * u + lane / 8) * PITCH + 16 * (lane % 8)) = v;
-    };
-
-    // the pair's share of a tile: its first byte, and whether any of it is in the cell
-    auto pair_start = [&](uint32_t tile, uint32_t& stripe, uint64_t& wbyte) {
-        uint32_t tcol;
-        tile_coords(tile, a, stripe, tcol);
-        wbyte = uint64_t(tcol) * TILE_BYTES + uint64_t(pw) * WAVE_BYTES;
-        return wbyte < cell_len;  // wave-uniform, the same for both waves of a pair
-    };
-
-    // The two roles run separate loops (separate register lives) over the same
-    // tiles, NSUM rounds each, one barrier per round.
-    if (!gf) {
-        uint32_t n = 0;  // round counter: image n & 1
-        uint32_t p_stripe = 0;
-        uint64_t p_wbyte = 0;
-        int p_sh = 0;
-        bool p_live = false;  // the round staged one round earlier
-        for (uint32_t tile = blockIdx.x; tile < total; tile += gridDim.x) {
-            uint32_t stripe;
-            uint64_t wbyte;
-            const bool work = pair_start(tile, stripe, wbyte);
-            for (int s = 0; s < NSUM; s++) {
-                if (p_live) crc_round(s_stage[pw][(n - 1) & 1], p_stripe, p_wbyte, p_sh);
-                p_stripe = stripe;
-                p_wbyte = wbyte;
-                p_sh = s;
-                p_live = work;
-                n++;
-                round_end();
-            }
-        }
-        if (p_live) crc_round(s_stage[pw][(n - 1) & 1], p_stripe, p_wbyte, p_sh);  // flush
-        return;
-    }
-
-    uint32_t n = 0;
-    for (uint32_t tile = blockIdx.x; tile < total; tile += gridDim.x) {
-        uint32_t stripe;
-        uint64_t wbyte;
-        const bool work = pair_start(tile, stripe, wbyte);
-        if (!work) {
-            for (int s = 0; s < NSUM; s++) round_end();
-            n += NSUM;
-            continue;
-        }
-        const uint64_t left = cell_len - wbyte;
-        uint32_t voff[SLABS];
-        bool live[SLABS];
-        u32x4 acc[SLABS][R];
-        u32x4 x[SLABS];
-#pragma unroll
-        for (int u = 0; u < SLABS; u++) {
-            const uint32_t o = uint32_t(u) * 1024u + uint32_t(lane) * 16u;
-            live[u] = o < left;
-            voff[u] = live[u] ? o : 0u;
-#pragma unroll
-            for (int j = 0; j < R; j++) acc[u][j] = u32x4{0, 0, 0, 0};
-            x[u] = load16<true>(a.in[0] + (uint64_t(stripe) * a.in_stride[0] + wbyte) + voff[u]);
-        }
-#pragma unroll
-        for (int i = 0; i < K; i++) {
-            // input i; its loads were issued in the last round and land while
-            // the wave waits at the barrier
-            uint8_t* img = s_stage[pw][(n + i) & 1];
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int u = 0; u < SLABS; u++) stage_piece(img, u, x[u]);
-            uint32_t toff = uint32_t(i) * uint32_t(sizeof(PermTable));
-            asm volatile("" : "+v"(toff));
-#pragma unroll
-            for (int u = 0; u < SLABS; u++) {
-                asm volatile("" : "+v"(x[u]));
-#pragma unroll
-                for (int j = 0; j < R; j++) asm volatile("" : "+v"(acc[u][j]) : "v"(toff));
-            }
-            uint32_t tb[R][5];
-#pragma unroll
-            for (int j = 0; j < R; j++) {
-                const PermTable& t = *reinterpret_cast<const PermTable*>(reinterpret_cast<const char*>(&s_tab[j][0]) + toff);
-                tb[j][0] = t.t0lo;
-                tb[j][1] = t.t0hi;
-                tb[j][2] = t.t1lo;
-                tb[j][3] = t.t1hi;
-                tb[j][4] = t.t2;
-            }
-#pragma unroll
-            for (int u = 0; u < SLABS; u++)
-#pragma unroll
-                for (int d = 0; d < 4; d++) {
-                    const Sel sl = make_sel(x[u][d]);
-#pragma unroll
-                    for (int j = 0; j < R; j++)
-                        acc[u][j][d] ^= gf_mul4(tb[j][0], tb[j][1], tb[j][2], tb[j][3], tb[j][4], sl.s0, sl.s1, sl.s2);
-                }
-            __builtin_amdgcn_sched_barrier(0);
-            if (i + 1 < K) {
-#pragma unroll
-                for (int u = 0; u < SLABS; u++)
-                    x[u] = load16<true>(a.in[i + 1] + (uint64_t(stripe) * a.in_stride[i + 1] + wbyte) + voff[u]);
-            }
-            if (VERIFY && i == K - 1) {
-#pragma unroll
-                for (int j = 0; j < R; j++)
-#pragma unroll
-                    for (int u = 0; u < SLABS; u++)
-                        if (live[u])
-                            store16<true>(a.out[j] + (uint64_t(stripe) * a.out_stride[j] + wbyte) + voff[u], acc[u][j]);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            round_end();
-        }
-        if constexpr (!VERIFY) {
-#pragma unroll
-            for (int j = 0; j < R; j++) {
-                uint8_t* img = s_stage[pw][(n + K + j) & 1];
-#pragma unroll
-                for (int u = 0; u < SLABS; u++) {
-                    if (live[u]) store16<true>(a.out[j] + (uint64_t(stripe) * a.out_stride[j] + wbyte) + voff[u], acc[u][j]);
-                    stage_piece(img, u, acc[u][j]);
-                }
-                round_end();
-            }
-        }
-        n += NSUM;
-    }
-}
-
-#endif  // HEC_EXPERIMENTAL
+// The role-split variant (GF waves and CRC waves paired on each SIMD; tune
+// key 21 = 2 / 3) lost 10-20 % (profiles/r02g/probe_split_rs*.log) and was
+// removed in round 6 (git history keeps it).
 
 namespace {
 
@@ -399,28 +180,6 @@ const void* verify_fn(int kind, int scheme, int wpe, bool pair) {
 #endif
 }
 
-#ifdef HEC_EXPERIMENTAL
-// role-split kernel (tune key 21 = 2, or 3 with the CRC waves at raised priority)
-template <int K, int R>
-const void* split_fn(bool verify, int kind, bool prio) {
-    if (!verify)
-        return prio ? reinterpret_cast<const void*>(&gf_fused_crc_split<K, R, crc::kCrc32c, false, true>)
-                    : reinterpret_cast<const void*>(&gf_fused_crc_split<K, R, crc::kCrc32c, false, false>);
-    if (kind == crc::kCrc32c)
-        return prio ? reinterpret_cast<const void*>(&gf_fused_crc_split<K, R, crc::kCrc32c, true, true>)
-                    : reinterpret_cast<const void*>(&gf_fused_crc_split<K, R, crc::kCrc32c, true, false>);
-    return prio ? reinterpret_cast<const void*>(&gf_fused_crc_split<K, R, crc::kCksum, true, true>)
-                : reinterpret_cast<const void*>(&gf_fused_crc_split<K, R, crc::kCksum, true, false>);
-}
-
-template <int K>
-const void* pick_split(bool verify, int r, int kind, bool prio) {
-    if (K == 6 && r == 3) return split_fn<6, 3>(verify, kind, prio);
-    if (K == 10 && r == 4) return split_fn<10, 4>(verify, kind, prio);
-    return nullptr;
-}
-
-#endif
 
 template <int K>
 const void* pick_r(bool verify, int r, int slabs, int scheme, int kind, int wpe, bool pair, bool bsl) {
@@ -474,25 +233,10 @@ int launch_fused(const MatmulArgs& in, const FusedCrcArgs& cs, bool verify, int 
     // 1.950 -> 1.915 ms, decode + verify 1.878 -> 1.818 ms; at k <= 6 the
     // 8-slab kernel (no pairs) stays faster than 4 slabs with pairs
     const bool pair = tn.fused_pair != 1;
-#ifdef HEC_EXPERIMENTAL
-    // role-split GF / CRC waves (tune key 21 = 2 / 3): rejected, see the kernel
-    const bool split = tn.fused_split == 2 || tn.fused_split == 3;
-    const bool prio = tn.fused_split == 3;
-#else
-    constexpr bool split = false;
-#endif
-    const int waves = split ? 8 : !crcdev::sliced(scheme) ? 8 : wpe == 3 ? 12 : 4;
+    constexpr bool split = false;  // the role-split kernel is gone (round 6); key 21 is retired
+    const int waves = !crcdev::sliced(scheme) ? 8 : wpe == 3 ? 12 : 4;
     const void* fn = nullptr;
-    if (split) {
-#ifdef HEC_EXPERIMENTAL
-        switch (a.k) {
-            case 6: fn = pick_split<6>(verify, a.r, cs.kind, prio); break;
-            case 10: fn = pick_split<10>(verify, a.r, cs.kind, prio); break;
-            default: return -1;
-        }
-        if (!fn) return -1;
-#endif
-    } else {
+    {
         // encode with the RS matrix: the bit-sliced parity (tune key 22 = 1: the
         // v_perm tables, measurement build)
         const bool bsl = !verify && tn.fused_bsl != 1 && rs_parity_matrix(a);

@@ -23,9 +23,10 @@
 //    aligned dword loads + v_alignbyte, 0.79-0.84 of the aligned rate);
 //    tails (cell_len % 16, or % 8 there) a byte-granular kernel with LDS
 //    log/antilog lookups -- same results everywhere.
-// Variants measured and rejected (register double buffering, output bursts,
-// store cache policies) live in ec_experimental.hip, built only into the
-// HEC_EXPERIMENTAL library.
+// Variants measured and rejected by more than 3 % (register double
+// buffering, output bursts, store cache policies) were removed in round 6
+// (git history: csrc/ec_experimental.hip); the HEC_EXPERIMENTAL library keeps
+// the knob-selected shapes.
 #include <hip/hip_runtime.h>
 
 #include <dlfcn.h>
@@ -1549,17 +1550,7 @@ int launch_gf_matmul(const MatmulArgs& in, int device, hipStream_t stream) {
         }
         const void* fn = nullptr;
         QueueLease lease;   // work-queue counters (held until the launch is enqueued)
-        int tile_mult = 1;  // column tiles per scheduling unit (output-burst kernel)
-#ifdef HEC_EXPERIMENTAL
-        ExpKernel ek;
-        if (tn.pipeline >= 3 && experimental_matmul(tn, a.k, a.r, &ek)) {
-            fn = ek.fn;
-            sh.unroll = ek.unroll;
-            sh.block = ek.block;
-            if (!tn.blocks_per_cu) sh.blocks_per_cu = ek.blocks_per_cu;
-            tile_mult = ek.tile_mult;
-        }
-#endif
+        const int tile_mult = 1;  // column tiles per scheduling unit
 #ifdef HEC_EXPERIMENTAL
         // bit-sliced RS parity in the register / LDS-DMA kernels (tune key 23
         // = 1).  Measured and not kept: same box, RS(6,3) 1

@@ -134,15 +134,5 @@ bool rs_parity_matrix(const MatmulArgs& a);
 // success, -1 invalid sizes, otherwise the (positive) hipError_t.
 int launch_gf_matmul(const MatmulArgs& a, int device, hipStream_t stream);
 
-#ifdef HEC_EXPERIMENTAL
-// Rejected variants (ec_experimental.hip), selected by tune key 5 in {3, 4,
-// 5}: register pipe kernel, output bursts, register double buffering.
-struct ExpKernel {
-    const void* fn;
-    int unroll, block, blocks_per_cu;
-    int tile_mult;  // column tiles per scheduling unit (bursts)
-};
-bool experimental_matmul(const Tune& t, int k, int r, ExpKernel* out);
-#endif
 
 }  // namespace hec

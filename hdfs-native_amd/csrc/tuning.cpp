@@ -15,7 +15,7 @@ namespace {
 std::atomic<int> g_cus[64];
 
 #ifdef HEC_EXPERIMENTAL
-constexpr int kKeys = 32;
+constexpr int kKeys = 33;
 std::atomic<int> g_knob[kKeys + 1];  // index = key; zero-initialised (static storage)
 std::atomic<int> g_nt{-1};           // key 2 defaults to -1 (non-temporal on)
 
@@ -59,6 +59,7 @@ Tune tune_snapshot() {
     t.crc_sums_nt = load(30);
     t.crc_runs = load(31);
     t.matmul_pair = load(32);
+    t.crc_block = load(33);
     return t;
 }
 
@@ -71,7 +72,7 @@ int tune_store(int key, int value) {
             return HEC_OK;
         case 3: ok = value >= 0 && value <= 16; break;
         case 4: ok = value == 0 || value == 256 || value == 512; break;
-        case 5: ok = value >= 0 && value <= 5; break;
+        case 5: ok = value >= 0 && value <= 2; break;
         case 6: ok = value >= 0 && value <= 2; break;
         case 7: ok = value >= 0 && value <= 65536; break;
         case 8: ok = value >= 0 && value <= 65536; break;
@@ -81,15 +82,15 @@ int tune_store(int key, int value) {
                       value == 7 || value == 9 || value == 10 || value == 11 || value == 12 || value == 13;
             break;
         case 12: ok = value >= 0 && value <= 2; break;
-        case 13: ok = value >= 0 && value <= 4; break;
+        case 13: ok = value == 0; break;  // retired
         case 14: ok = value >= 0 && value <= 64; break;
-        case 15: ok = value == 0 || value == 2 || value == 3; break;
+        case 15: ok = value == 0; break;  // retired
         case 16: ok = value == 0 || value == 2 || value == 3; break;
         case 17: ok = value >= 0 && value <= 65536 && (value & 3) == 0; break;
         case 18: ok = value == 0 || value == 1; break;
         case 19: ok = value >= 0 && value <= 2; break;
         case 20: ok = value >= 0 && value <= 2; break;
-        case 21: ok = value >= 0 && value <= 3; break;
+        case 21: ok = value == 0 || value == 1; break;  // 2 / 3 (role split) retired
         case 22: ok = value == 0 || value == 1; break;
         case 23: ok = value == 0 || value == 1; break;
         case 24: ok = value >= 0 && value <= 5; break;
@@ -101,6 +102,7 @@ int tune_store(int key, int value) {
         case 30: ok = value == 0 || value == 1; break;
         case 31: ok = value == 0 || value == 2 || value == 4 || value == 8 || value == 16; break;
         case 32: ok = value == 0 || value == 1; break;
+        case 33: ok = value == 0 || value == 768; break;
         default: ok = false;
     }
     if (!ok) return HEC_ERR_INVALID_ARG;

@@ -15,9 +15,9 @@
  * key 2: non-temporal global loads/stores (0 or 1; -1 = default on)
  * key 3: blocks per CU for the grid (1..16; 0 = default)
  * key 4: threads per block (256 or 512; 0 = default)
- * key 5: kernel pipeline: 1 = register, 2 = LDS-DMA prefetch, 3 = register
- *        double-buffered (pipe), 4 = output bursts, 5 = double-buffered tiles;
- *        0 = default
+ * key 5: kernel pipeline: 1 = register, 2 = LDS-DMA prefetch, 0 = default
+ *        (3 / 4 / 5 -- register double buffering, output bursts, double-
+ *        buffered tiles -- were removed in round 6)
  * key 6: store drain per tile in the register kernels: 1 = no drain,
  *        0 / 2 = drain (default)
  * key 7: absolute grid size in blocks (0 = default)
@@ -39,11 +39,10 @@
  *         fused shapes and the specialised decode + verify)
  * key 12: CRC register prefetch depth in 8-KiB tasks: 0 = default (1 for the
  *         CRC32C fold, else 2), 1 or 2
- * key 13: store cache policy of the pipe kernel (0 = nt, 1 = sc1, 2 = sc0 sc1,
- *         3 = nt sc1, 4 = plain)
+ * key 13: retired in round 6 (store cache policy of the removed pipe kernel)
  * key 14: host threads that copy the present data cells in hec_decode_host_batch
  *         (0 = default 4)
- * key 15: column tiles per store burst of the output-burst kernel (2 or 3)
+ * key 15: retired in round 6 (the removed output-burst kernel)
  * key 16: fused kernels' waves per SIMD: 0 / 2 = default; 3
  * key 17: per-call drop-in (hec_encode / hec_decode) pipeline piece in KiB per
  *         shard, a multiple of 4 (0 = default 256)
@@ -54,9 +53,7 @@
  * key 20: mixed-pattern decode, rows past a stripe's erasure count: 0 / 2 =
  *         skipped (default), 1 = computed and dropped at the store
  * key 21: fused kernels' wave roles: 0 / 1 = every wave alternates GF math
- *         and CRC rounds (default); 2 = role-split GF / CRC waves (one
- *         512-thread block per CU, RS(6,3) and RS(10,4) only), 3 = role-split
- *         with the CRC waves at raised priority
+ *         and CRC rounds (the only form since round 6 removed the role split)
  * key 22: fused encode + CRC parity: 0 = default (bit-sliced XOR network of
  *         the RS matrix for RS(3,2), RS(6,3), RS(10,4)), 1 = v_perm tables
  * key 23: register / LDS-DMA encode kernels: 0 = default (v_perm tables),
@@ -88,6 +85,9 @@
  * key 32: 1 = the wave-pair register kernel for k = 10 (gf_matmul_pair: two
  *         waves per wave-tile, 5 inputs each, partials exchanged in LDS);
  *         key 3 sets its 128-thread blocks per CU (0 = 4: two waves per SIMD)
+ * key 33: 768 = the CRC32C checksum kernel (the fold, compute and verify) in
+ *         one 768-thread block per CU: 3 waves per SIMD (0 = default: two
+ *         256-thread blocks per CU)
  * Returns HEC_OK, or HEC_ERR_INVALID_ARG for an unknown key / value.
  */
 #ifndef HDFS_EC_AMD_EXP_H

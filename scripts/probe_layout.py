@@ -15,7 +15,9 @@ key 30 = 1) and on the work queue (key 29 = 4 tasks per unit), compute and
 verify mode, same buffers,
 rounds alternated; PROBE_CRC_DMA=1 adds the LDS-DMA kernel (key 11 = 13;
 profiles/r05n ran it with the DMA kernel as the default and the register one
-on the key: the same kernels).
+on the key: the same kernels); PROBE_CRC_768=1 (round 6) the default kernel
+against one 768-thread block per CU (key 33) and the memory side alone (key
+11 = 9, WRONG sums), compute and verify mode.
   python3 scripts/probe_layout.py
 """
 import os
@@ -121,6 +123,9 @@ def main():
 
             kernels[(lay, i)] = {"crc_reg": crc, "crc_runs4": tuned(crc, 4, 31), "crc_runs8": tuned(crc, 8, 31),
                                  "crc_runs16": tuned(crc, 16, 31), "verify_reg": ver, "verify_runs8": tuned(ver, 8, 31)}
+            if os.environ.get("PROBE_CRC_768") == "1":  # round 6: 3 waves per SIMD (key 33), the skeleton (key 11 = 9)
+                kernels[(lay, i)] = {"crc_reg": crc, "crc_768": tuned(crc, 768, 33), "crc_mem": tuned(crc, 9),
+                                     "verify_reg": ver, "verify_768": tuned(ver, 768, 33)}
             if os.environ.get("PROBE_CRC_DMA") == "1":
                 kernels[(lay, i)].update({"crc_dma": tuned(crc, 13), "verify_dma": tuned(ver, 13)})
             continue
@@ -142,7 +147,7 @@ def main():
     algo = {"crc_only": (K + M) * CELL * S + 4 * NCH * (K + M) * S, "encode": (K + M) * CELL * S,
             "encode_crc": (K + M) * CELL * S + 4 * NCH * (K + M) * S,
             "decode_verify": (K + len(MISS)) * CELL * S + 4 * NCH * K * S}
-    for n in ("crc_dma", "crc_reg", "verify_dma", "verify_reg", "crc_wq1", "crc_wq2", "crc_wq4", "verify_wq2", "crc_nt", "crc_wq8", "crc_wq16", "verify_wq8", "crc_runs2", "crc_runs4", "verify_runs2", "crc_runs8", "crc_runs16", "verify_runs8"):
+    for n in ("crc_dma", "crc_reg", "verify_dma", "verify_reg", "crc_wq1", "crc_wq2", "crc_wq4", "verify_wq2", "crc_nt", "crc_wq8", "crc_wq16", "verify_wq8", "crc_runs2", "crc_runs4", "verify_runs2", "crc_runs8", "crc_runs16", "verify_runs8", "crc_768", "verify_768", "crc_mem"):
         algo[n] = algo["crc_only"]
     for key, per in times.items():
         parts = []

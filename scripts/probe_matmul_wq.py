@@ -61,6 +61,14 @@ if os.environ.get("PROBE_PAIR") == "1":
     VARIANTS = [("512 x1/CU", [(27, 0)]), ("pair x4/CU", [(32, 1)]), ("pair x2/CU", [(32, 1), (3, 2)]),
                 ("pair x3/CU", [(32, 1), (3, 3)])]
 
+# PROBE_BSL=1 (round 6): RS(10,4) encode with the RS parity rows as bit-
+# sliced XOR networks (tune key 23 = 1, gf_encode_bsl, fixed tile order; the
+# decode keeps the v_perm tables) against the v_perm encode on the queue
+# (default) and in the fixed order (key 27 = 3)
+if os.environ.get("PROBE_BSL") == "1":
+    CONFIGS = [(10, 4, 256), (10, 4, 1024), (6, 3, 1024)]
+    VARIANTS = [("v_perm queue", [(27, 0)]), ("v_perm fixed", [(27, 3)]), ("bsl fixed", [(23, 1)])]
+
 
 def main():
     dev = torch.device("cuda:0")

@@ -1,7 +1,7 @@
 """Parity of every knob-selected shape and of the measured-and-rejected
 kernel variants, which exist only in the HEC_EXPERIMENTAL measurement build
 (hdfs-native_amd/lib/libhdfs_ec_amd_exp.so, `make -C hdfs-native_amd exp`;
-ec_experimental.hip and the #ifdef'd shapes and CRC schemes; knobs in
+the #ifdef'd shapes and CRC schemes; knobs in
 include/hdfs_ec_amd_exp.h).  Same oracle and same bit-exact bar as the
 product library; every coder here is bound to the measurement build and its
 knobs are that library's own.  The product library has no knobs: its
@@ -72,57 +72,17 @@ def run_variant(xlib, c_oracle, dev, k, m, S, cell, knobs, first):
     assert torch.equal(out[:, :m], d[:, :m])
 
 
-@pytest.mark.parametrize("unroll", [1, 2, 3])
-@pytest.mark.parametrize("grid", [0, 1, 5, 6])
-@pytest.mark.parametrize("k,m", [(2, 1), (3, 2), (6, 3), (10, 4)])
-def test_register_pipe_vs_oracle(xlib, dev, c_oracle, unroll, grid, k, m):
-    # tune key 5 = 3: register pipe kernel.  Small grids walk many tiles per
-    # block (both register sets, odd and even tile counts, the clamped
-    # past-the-end prefetch); the cell leaves a partial last tile.
-    cell = 3 * 65536 + 48
-    run_variant(xlib, c_oracle, dev, k, m, 3, cell, [(5, 3), (1, unroll), (7, grid)], cell + 7 * k + unroll)
-
-
-@pytest.mark.parametrize("unroll,block", [(4, 256), (2, 256), (1, 512)])
-@pytest.mark.parametrize("grid", [0, 1, 5, 6])
-@pytest.mark.parametrize("k,m", [(2, 1), (3, 2), (6, 3), (10, 4)])
-def test_double_buffered_vs_oracle(xlib, dev, c_oracle, unroll, block, grid, k, m):
-    # tune key 5 = 5: drain-free register double buffering (two register and
-    # two accumulator sets); grids of 1/5/6 blocks cover odd and even tile
-    # counts per block and the past-the-end re-read
-    cell = 3 * 65536 + 48
-    run_variant(xlib, c_oracle, dev, k, m, 3, cell, [(5, 5), (1, unroll), (4, block), (7, grid)],
-                cell + 13 * k + unroll)
-
-
-@pytest.mark.parametrize("tiles", [2, 3])
-@pytest.mark.parametrize("grid", [0, 1, 5])
-@pytest.mark.parametrize("k,m", [(2, 1), (3, 2), (6, 3)])
-def test_output_burst_vs_oracle(xlib, dev, c_oracle, tiles, grid, k, m):
-    # tune key 5 = 4: outputs parked in LDS, stored in bursts of `tiles`
-    # column tiles; partial super-tiles at the cell end, many per block
-    cell = 3 * 65536 + 48
-    run_variant(xlib, c_oracle, dev, k, m, 3, cell, [(5, 4), (15, tiles), (7, grid)], cell + 11 * k + tiles)
-
-
-@pytest.mark.parametrize("pol", [1, 2, 3, 4])
-@pytest.mark.parametrize("unroll", [1, 2])
-@pytest.mark.parametrize("k,m", [(6, 3), (10, 4)])
-def test_store_policies_vs_oracle(xlib, dev, c_oracle, pol, unroll, k, m):
-    # tune key 13: cache policy of the pipe kernel's stores (sc1 / sc0 sc1 /
-    # nt sc1 / plain, inline-asm stores) at the bench shapes
-    run_variant(xlib, c_oracle, dev, k, m, 5, 65536 + 32, [(5, 3), (1, unroll), (13, pol), (7, 7)], pol * 31 + unroll)
-
-
-def _oracle_sums(cells, bpc, ctype=H.CHECKSUM_CRC32C):
-    S, n, cell = cells.shape
-    nch = (cell + bpc - 1) // bpc
-    out = np.empty((S, n, nch, 4), dtype=np.uint8)
-    for s in range(S):
-        for i in range(n):
-            out[s, i] = np.frombuffer(O.chunk_checksums(cells[s, i].tobytes(), bpc, ctype),
-                                      dtype=np.uint8).reshape(nch, 4)
-    return out
+@pytest.mark.parametrize("k,m", [(10, 4), (10, 1), (10, 3)])
+@pytest.mark.parametrize("cell", [8192 + 16, 3 * 65536 + 48, 1 << 20])
+@pytest.mark.parametrize("bpc", [0, 2, 3])
+@pytest.mark.parametrize("S", [1, 3, 9])
+def test_pair_kernel_vs_oracle(xlib, dev, c_oracle, k, m, cell, bpc, S):
+    # tune key 32 = 1: RS(10,*) on the wave-pair kernel (two waves per
+    # wave-tile, partials through LDS), 1-4 rows (decode of 1..m data shards:
+    # wave 1 stores nothing at one row), partial last tiles, 2 / 3 / 4 blocks
+    # of 128 threads per CU, small batches (fewer tiles than counters)
+    knobs = [(32, 1)] + ([(3, bpc)] if bpc else [])
+    run_variant(xlib, c_oracle, dev, k, m, S, cell, knobs, cell + 7 * S + bpc)
 
 
 @pytest.mark.parametrize("ctype", [H.CHECKSUM_CRC32C, H.CHECKSUM_CRC32])
@@ -170,19 +130,26 @@ def test_crc_runs_vs_oracle(xlib, dev, cell, bpc, n, runs):
     assert torch.equal(got, want)
 
 
-@pytest.mark.parametrize("wq", [1, 4, 16])
-def test_crc_wq_full_size_compute_and_verify(xlib, dev, wq):
-    """Key 29 at full size (9 x 1 MiB x 64 cells), three launches in a row
-    on one stream (the counters must come back to zero): sums equal the
-    default kernel's, and verify mode flags exactly the corrupted cells."""
+@pytest.mark.parametrize("cell,bpc,n", [c for c in P.CRC32C_CASES if c[1] == 512])
+def test_crc_768_vs_oracle(xlib, dev, cell, bpc, n):
+    """Tune key 33 = 768: the CRC32C fold kernel in one 768-thread block per
+    CU (3 waves per SIMD), against the oracle."""
+    P.crc32c_body(dev, cell, bpc, n, P.coder(6, 3, xlib), [(33, 768)], xlib)
+
+
+@pytest.mark.parametrize("knob", [(29, 1), (29, 4), (29, 16), (33, 768)])
+def test_crc_wq_full_size_compute_and_verify(xlib, dev, knob):
+    """Keys 29 / 33 at full size (9 x 1 MiB x 64 cells), three launches in a
+    row on one stream: sums equal the default kernel's, and verify mode flags
+    exactly the corrupted cells."""
     S, n, cell = 64, 9, 1 << 20
     c = xcoder(xlib, 6, 3)
-    g = torch.Generator(device=dev).manual_seed(29 + wq)
+    g = torch.Generator(device=dev).manual_seed(29 + knob[1])
     x = torch.empty((S, n, cell), dtype=torch.uint8, device=dev)
     x.random_(0, 256, generator=g)
     want = H.crc32c_batch(c, x, 512)
     hits = {(0, 0): 0, (5, 8): cell - 1, (31, 4): cell // 2 + 3, (63, 2): 8191, (63, 6): 8192}
-    with P.knobs([(29, wq)], xlib):
+    with P.knobs([knob], xlib):
         for _ in range(3):
             got = H.crc32c_batch(c, x, 512)
             torch.cuda.synchronize()
@@ -468,7 +435,7 @@ def test_tune_set_concurrent_with_launches(xlib, dev, c_oracle):
 
 
 def test_tune_set_rejects_unknown_values(xlib):
-    for key, value in [(3, 99), (1, 5), (5, 6), (11, 8), (16, 1), (17, 6), (19, 3), (20, 3), (21, 4), (22, 2), (23, 2), (24, 6), (25, 4097), (26, 5), (27, 4), (28, 3), (29, 3), (30, 2), (31, 3), (32, 0), (0, 0)]:
+    for key, value in [(3, 99), (1, 5), (5, 6), (11, 8), (16, 1), (17, 6), (19, 3), (20, 3), (21, 2), (5, 3), (13, 1), (15, 2), (22, 2), (23, 2), (24, 6), (25, 4097), (26, 5), (27, 4), (28, 3), (29, 3), (30, 2), (31, 3), (32, 2), (33, 512), (34, 0), (0, 0)]:
         with pytest.raises(ValueError):
             H.tune_set(key, value, xlib)
 
