@@ -124,7 +124,8 @@ def main():
             kernels[(lay, i)] = {"crc_reg": crc, "crc_runs4": tuned(crc, 4, 31), "crc_runs8": tuned(crc, 8, 31),
                                  "crc_runs16": tuned(crc, 16, 31), "verify_reg": ver, "verify_runs8": tuned(ver, 8, 31)}
             if os.environ.get("PROBE_CRC_768") == "1":  # round 6: 3 waves per SIMD (key 33), the skeleton (key 11 = 9)
-                kernels[(lay, i)] = {"crc_reg": crc, "crc_768": tuned(crc, 768, 33), "crc_mem": tuned(crc, 9),
+                # the memory side first: its WRONG sums are rewritten before the verify legs
+                kernels[(lay, i)] = {"crc_mem": tuned(crc, 9), "crc_reg": crc, "crc_768": tuned(crc, 768, 33),
                                      "verify_reg": ver, "verify_768": tuned(ver, 768, 33)}
             if os.environ.get("PROBE_CRC_DMA") == "1":
                 kernels[(lay, i)].update({"crc_dma": tuned(crc, 13), "verify_dma": tuned(ver, 13)})
