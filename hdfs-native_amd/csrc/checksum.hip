@@ -236,218 +236,10 @@ __global__ __launch_bounds__(BLK ? BLK : CrcShape<SCHEME>::kBlock) void checksum
     }
 }
 
-// ---------------------------------------------------------------------------
-// LDS-DMA kernel (measurement build, key 11 = 13; CRC32C, 512-B chunks, 16-B
-// aligned cells).  The same per-lane algorithm as checksum_chunks512's fold (a
-// wave owns 16 chunks = 8 KiB of one cell, a lane one 128-B quarter, the fold
-// to a 32-B tail, the tail through slicing-by-8 tables, nibble shift tables,
-// two XOR shuffles), but the task's 8 KiB land in LDS by
-// global_load_lds_dwordx4 (no staging VGPRs, no ds_write pass) into one of NST
-// stages per wave, so NST-1 tasks are in flight while one is checksummed, at
-// one 256-thread block (one wave per SIMD) per CU.  The landing image is
-// lane-linear (64 x 16 B per instruction); the quarter walk is made bank-
-// conflict free by an XOR swizzle on the SOURCE address: piece i of quarter Q
-// lands in slot 8Q + (i ^ ((Q >> 1) & 7)), and each instruction still reads
-// one contiguous KiB (lanes permuted inside each 128-B line).  Tasks walk
-// kInter cells interleaved (consecutive tasks: group g of cells c0 .. c0+7,
-// then group g+1).  Verify mode lands the packets' expected sums with the
-// task (one more 4-B-per-lane DMA), so nothing but the DMAs is waited for.
-// Measured and not kept (round 5): on hipMalloc'd buffers it ties the
-// register kernel (0.749-0.759 vs 0.757-0.767 of HBM peak,
-// scripts/probe_crc_dma.hip, profiles/r05k, r05m); on the bench's torch
-// buffers, same process, rounds alternated (scripts/probe_layout.py
-// PROBE_CRC_AB=1, profiles/r05n) it loses 4-10 % computing and 11-14 %
-// verifying.
-#ifdef HEC_EXPERIMENTAL
-// ---------------------------------------------------------------------------
-constexpr int kDmaWaves = 4, kDmaInter = 8;
-
-struct CrcDmaShape {
-    static constexpr int kTabWords = 8 * 256 + 3 * 8 * 16;  // slice[8][256] + shift_nib[3][8][16]
-    static constexpr int kStage = 8192 + 256;               // one task's 8 KiB + its 64 expected sums (verify)
-};
-
-// wave-uniform value into an SGPR (the divisions below run on the VALU, so
-// without this every kernarg / stripe-list read indexed by them would be a
-// vector load the compiler waits for with vmcnt(0), draining the DMAs)
-__device__ __forceinline__ uint32_t uni(uint32_t x) { return uint32_t(__builtin_amdgcn_readfirstlane(int(x))); }
-
-// task -> (launch cell, group): kDmaInter cells interleaved, a short last
-// block; wave-uniform, 32-bit (the launcher keeps tasks < 2^32): a 64-bit
-// division here costs more VALU than the task's whole fold at one wave per SIMD
-__device__ __forceinline__ void dma_task_cell(uint32_t task, uint32_t groups, uint32_t ncells, uint32_t& cell,
-                                              uint32_t& g) {
-    const uint32_t span = uint32_t(kDmaInter) * groups, blk = uni(task / span), r = task - blk * span;
-    const uint32_t c0 = blk * kDmaInter, w = ncells - c0;
-    if (w >= uint32_t(kDmaInter)) {
-        cell = uni(c0 + r % uint32_t(kDmaInter));
-        g = uni(r / uint32_t(kDmaInter));
-    } else {
-        cell = uni(c0 + r % w);
-        g = uni(r / w);
-    }
-}
-
-// the sums / flags index of launch cell `cell_idx` (emit_sum's mapping);
-// sid_lane = a.sid[lane], read out by v_readlane (a dynamically indexed
-// kernarg byte would be a vector load the compiler drains vmcnt for).  A
-// stripe list is read with a vector load the compiler waits for: those are
-// phase-2 re-verifications of a few failing stripes, and the extra wait only
-// makes the counted waits below conservative.
-__device__ __forceinline__ uint64_t dma_sum_cell(const CrcArgs& a, uint32_t cell_idx, uint32_t sid_lane) {
-    if (!a.mapped) return cell_idx;
-    const uint32_t s = uni(cell_idx / a.n_shards), i = uni(cell_idx - s * a.n_shards);
-    const uint64_t stripe = a.stripe_list ? a.stripe_list[s] : s;
-    return stripe * a.n_total + uint32_t(__builtin_amdgcn_readlane(int(sid_lane), int(i)));
-}
-
-template <int NST, bool VERIFY>
-__global__ __launch_bounds__(kDmaWaves * 64) void checksum_chunks512_dma(CrcArgs a) {
-    constexpr int STAGE = CrcDmaShape::kStage;
-    // one LDS object (a second __shared__ array beside the DMA image can make
-    // hipcc add vmcnt(0) waits): the stages, then the tables
-    __shared__ __attribute__((aligned(16))) uint8_t s_mem[kDmaWaves * NST * STAGE + CrcDmaShape::kTabWords * 4];
-    uint32_t* s_tab = reinterpret_cast<uint32_t*>(s_mem + kDmaWaves * NST * STAGE);
-    // loaded before the barrier, whose wait retires it: read inside the loop
-    // it would cost a vmcnt(0) there (the loop's DMAs are younger)
-    const uint32_t sid_lane = (threadIdx.x & 63) < kCrcMaxShards ? a.sid[threadIdx.x & 63] : 0u;
-    const crc::Tables<crc::kCrc32c>& T = tables<crc::kCrc32c>();
-    for (int t = threadIdx.x; t < 8 * 256; t += kDmaWaves * 64) s_tab[t] = (&T.slice[0][0])[t];
-    for (int t = threadIdx.x; t < 3 * 8 * 16; t += kDmaWaves * 64) s_tab[8 * 256 + t] = (&T.shift_nib[0][0][0])[t];
-    __syncthreads();
-    const uint32_t kfinal = T.final512;
-
-    const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x / 64)), lane = threadIdx.x & 63;
-    const int qi = lane & 3, c = lane >> 2;
-    uint8_t* st = s_mem + wave * NST * STAGE;
-    const uint32_t groups = uint32_t(a.groups_per_cell);
-    const uint32_t ncells = uint32_t(a.n_shards * a.stripes);
-    const uint32_t tasks = groups * ncells;
-    const uint32_t nw = gridDim.x * kDmaWaves;
-    // instruction t, lane l: quarter q = 8t + l/8, piece (l % 8) ^ ((q >> 1) & 7)
-    uint32_t loff[8];
-#pragma unroll
-    for (int t = 0; t < 8; t++) {
-        const uint32_t q = 8u * uint32_t(t) + uint32_t(lane) / 8u;
-        loff[t] = 1024u * uint32_t(t) + 128u * (uint32_t(lane) / 8u) + 16u * ((uint32_t(lane) & 7u) ^ ((q >> 1) & 7u));
-    }
-    // the (launch cell, group) of the task in each stage: the stage index is a
-    // compile-time constant at every use (the main loop is unrolled NST times),
-    // so these stay in SGPRs
-    uint32_t q_cell[NST], q_g[NST];
-    auto issue = [&](uint32_t task, int s) {
-        uint32_t cell_idx, g;
-        dma_task_cell(task, groups, ncells, cell_idx, g);
-        q_cell[s] = cell_idx;
-        q_g[s] = g;
-        const uint32_t sidx = uni(cell_idx / a.n_shards);
-        const uint32_t shard = uni(cell_idx - sidx * a.n_shards);
-        const uint64_t stripe = a.stripe_list ? a.stripe_list[sidx] : sidx;
-        const uint8_t* base = a.base[shard] + stripe * a.stride[shard] + uint64_t(g) * 8192u;
-        const uint64_t left = a.cell_len - uint64_t(g) * 8192u;
-        uint8_t* dst = st + s * STAGE;
-        if (left >= 8192u) {  // wave-uniform: a whole task
-#pragma unroll
-            for (int t = 0; t < 8; t++)
-                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(base + loff[t]),
-                                                 (__attribute__((address_space(3))) void*)(dst + t * 1024), 16, 0,
-                                                 2 /* nt */);
-        } else {  // a cell's short last task: dead lanes read the cell start (never checksummed)
-#pragma unroll
-            for (int t = 0; t < 8; t++)
-                __builtin_amdgcn_global_load_lds(
-                    reinterpret_cast<const void*>(base + (loff[t] < uint32_t(left) ? loff[t] : 0u)),
-                    (__attribute__((address_space(3))) void*)(dst + t * 1024), 16, 0, 2 /* nt */);
-        }
-        if constexpr (VERIFY) {  // lane l: the expected sum of chunk l/4 (clamped to the task's last chunk)
-            const uint64_t nch = a.chunks_per_cell - uint64_t(g) * 16u;
-            const uint64_t ch = uint64_t(c) < nch ? uint64_t(c) : nch - 1;
-            const uint32_t* e = reinterpret_cast<const uint32_t*>(a.expected) +
-                                dma_sum_cell(a, cell_idx, sid_lane) * a.chunks_per_cell + uint64_t(g) * 16u + ch;
-            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(e),
-                                             (__attribute__((address_space(3))) void*)(dst + 8192), 4, 0, 0);
-        }
-    };
-    // the task in stage s, landed: checksum its 16 chunks, store / check the sums
-    auto process = [&](int s) {
-        const uint32_t cell_idx = q_cell[s], g = q_g[s];
-        const uint8_t* sb = st + s * STAGE;
-        const bool task_full = uint64_t(g + 1) * 8192u <= a.cell_len;  // wave-uniform
-        const uint64_t cstart = uint64_t(g) * 8192u + uint64_t(c) * 512u;
-        const bool live = task_full || cstart < a.cell_len;
-        const bool full = task_full || (live && a.cell_len - cstart >= 512u);  // same for the chunk's 4 lanes
-        uint32_t val = 0;
-        if (full) {
-            uint32_t w[32];
-#pragma unroll
-            for (int i = 0; i < 8; i++) {
-                const v4u_ v = *reinterpret_cast<const v4u_*>(sb + 16 * (lane * 8 + (i ^ ((lane >> 1) & 7))));
-                w[4 * i] = v.x, w[4 * i + 1] = v.y, w[4 * i + 2] = v.z, w[4 * i + 3] = v.w;
-            }
-            uint32_t r = crcdev::quarter_fold_regs_s8(w, reinterpret_cast<const uint32_t(*)[256]>(s_tab));
-            if (qi < 3) r = crcdev::apply_shift_nib(reinterpret_cast<const uint32_t(*)[8][16]>(s_tab + 8 * 256)[qi], r);
-            val = r;
-        } else if (live && qi == 0) {
-            // short last chunk of the cell: this lane walks it whole, bytewise,
-            // through the swizzled image
-            const uint32_t len = uint32_t(a.cell_len - cstart);
-            uint32_t r = crc::Spec<crc::kCrc32c>::kInit;
-            for (uint32_t p = 0; p < len; p++) {
-                const uint32_t q = 4u * uint32_t(c) + p / 128u, i = (p % 128u) / 16u;
-                r = crcdev::byte_step<true, 1>(s_tab, r, sb[16u * (q * 8u + (i ^ ((q >> 1) & 7u))) + p % 16u]);
-            }
-            val = r ^ crc::Spec<crc::kCrc32c>::kXorout;
-        }
-        val ^= __shfl_xor(val, 1);
-        val ^= __shfl_xor(val, 2);
-        if (live && qi == 0) {
-            const uint32_t be = bswap32(full ? (val ^ kfinal) : val);
-            const uint64_t cell = dma_sum_cell(a, cell_idx, sid_lane);
-            if constexpr (VERIFY) {
-                if (reinterpret_cast<const uint32_t*>(sb + 8192)[lane] != be) a.bad[cell] = 1;
-            } else {
-                reinterpret_cast<uint32_t*>(a.out)[cell * a.chunks_per_cell + uint64_t(g) * 16u + uint64_t(c)] = be;
-            }
-        }
-    };
-    // VMEM ops per task: its DMAs (+ the sums DMA when verifying); per
-    // processed task one sums store in compute mode (a task always has a live
-    // chunk 0, so the store is issued).  A flag store on a mismatch (verify)
-    // is extra and only makes the counted waits below conservative.
-    constexpr int G = VERIFY ? 9 : 8;
-    uint32_t task = blockIdx.x * kDmaWaves + uint32_t(wave);
-#pragma unroll
-    for (int s = 0; s < NST - 1; s++)
-        if (task + uint32_t(s) * nw < tasks) issue(task + uint32_t(s) * nw, s);
-    bool steady = false;  // NST-1 tasks processed (their stores are in the count)
-    for (;;) {
-#pragma unroll
-        for (int s = 0; s < NST; s++) {
-            if (task >= tasks) return;
-            const uint32_t nt = task + uint32_t(NST - 1) * nw;
-            __builtin_amdgcn_sched_barrier(0);
-            if (nt < tasks) {
-                issue(nt, (s + NST - 1) % NST);  // the stage processed in the previous step
-                // younger than this task's ops: the NST-1 newer tasks' and the
-                // sums stores issued since it (one per processed task)
-                if (VERIFY || steady)
-                    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G * (NST - 1) + (VERIFY ? 0 : NST - 1)) : "memory");
-                else if (s == 0)
-                    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G * (NST - 1)) : "memory");
-                else
-                    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G * (NST - 1) + 1) : "memory");
-            } else {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            process(s);
-            task += nw;
-            if (s == NST - 2) steady = true;
-        }
-    }
-}
-
-#endif  // HEC_EXPERIMENTAL
+// The LDS-DMA CRC kernel (tasks landed in LDS by global_load_lds_dwordx4,
+// key 11 = 13; round 5) lost 4-14 % on the bench's buffers
+// (profiles/r05n) and was removed in round 6; scripts/probe_crc_dma.hip keeps
+// its standalone probe form.
 
 // Generic path: any chunk size / alignment.  One lane per chunk, bytes from
 // global memory, slice-by-1.
@@ -558,17 +350,6 @@ int launch_checksum(const CrcArgs& in, int device, hipStream_t stream) {
     if (aligned && a.bytes_per_checksum == 512) {
         a.groups_per_cell = (a.chunks_per_cell + 15) / 16;
         const uint64_t tasks = a.groups_per_cell * a.n_shards * a.stripes;
-#ifdef HEC_EXPERIMENTAL
-        // key 11 = 13: the LDS-DMA kernel, 3 stages per wave, one block per CU
-        if (a.kind == crc::kCrc32c && tn.crc_variant == 13 && tasks < (uint64_t(1) << 32)) {
-            uint64_t grid = (tasks + kDmaWaves - 1) / kDmaWaves;
-            if (grid > uint64_t(cus)) grid = uint64_t(cus);
-            const void* fn = a.expected ? reinterpret_cast<const void*>(&checksum_chunks512_dma<3, true>)
-                                        : reinterpret_cast<const void*>(&checksum_chunks512_dma<3, false>);
-            e = hipLaunchKernel(fn, dim3(uint32_t(grid)), dim3(kDmaWaves * 64), args, 0, stream);
-            return e == hipSuccess ? 0 : int(e);
-        }
-#endif
         // 11-bit slicing (6 LDS lookups per 8 bytes), 2 tasks of prefetch,
         // was the default until the fold.  Interleaved A/B (profiles/r01d_probe_crc_w11.log): 5.32
         // TB/s vs 4.84-4.89 for slicing-by-8 (profiles/r01_probe_crc.log: 4.91

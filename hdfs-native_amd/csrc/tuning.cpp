@@ -79,7 +79,7 @@ int tune_store(int key, int value) {
         case 9: value = value ? 1 : 0; ok = true; break;
         case 10: ok = value == 0 || value == 4 || value == 8; break;
         case 11: ok = value == 0 || value == 1 || value == 2 || value == 3 || value == 4 || value == 5 || value == 6 ||
-                      value == 7 || value == 9 || value == 10 || value == 11 || value == 12 || value == 13;
+                      value == 7 || value == 9 || value == 10 || value == 11 || value == 12;  // 13 retired
             break;
         case 12: ok = value >= 0 && value <= 2; break;
         case 13: ok = value == 0; break;  // retired

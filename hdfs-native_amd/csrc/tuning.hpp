@@ -33,7 +33,7 @@ struct Tune {
     int group = 0;              // key 8: stripes per tile-order group (0 = default 4)
     int crc_unfused = 0;        // key 9: 1 = hec_encode_crc_device as encode + checksum passes
     int fused_slabs = 0;        // key 10: fused encode+CRC slabs per wave (0, 4, 8)
-    int crc_variant = 0;        // key 11: 0 default (the fold), 13 the LDS-DMA fold kernel (CRC32C checksum kernel), 1 slicing-by-8, 5 11-bit, 12 slicing-by-32 tail, 2/3/4/6/9 rejected schemes
+    int crc_variant = 0;        // key 11: 0 default (the fold), 1 slicing-by-8, 5 11-bit, 12 slicing-by-32 tail, 2/3/4/6/9 rejected schemes
     int crc_prefetch = 0;       // key 12: CRC kernel register prefetch depth (0 = scheme default: 1 for the CRC32C fold, else 2; 1, 2)
     int store_pol = 0;          // key 13: retired (the pipe kernel's store policy, round 6 pruning)
     int host_copy_threads = 0;  // key 14: hec_decode_host_batch host copy threads (0 = 4)

@@ -26,9 +26,7 @@
  * key 10: fused encode+CRC slabs per wave: 0 = default, 4 or 8
  * key 11: CRC lookups: 0 = default (CRC32C: each 128-B quarter folded by a
  *         sparse multiple of the polynomial, then 11-bit slicing over its
- *         tail; CRC32: 11-bit slicing), 13 = the CRC32C checksum kernel
- *         with its tasks landed in LDS by DMA and the tail through
- *         slicing-by-8 (round 5, not kept), 7 = the same as 0, 1 = slice-by-8, 5 =
+ *         tail; CRC32: 11-bit slicing), 7 = the same as 0, 1 = slice-by-8, 5 =
  *         11-bit slicing everywhere, 2 / 3 = bank-replicated slice-by-1 with
  *         4 / 8 chains, 4 = slice-by-8 at 4 waves per SIMD (checksum
  *         kernel), 6 = bank-replicated slice-by-2, 9 = memory side only

@@ -13,9 +13,8 @@ PROBE_CRC_AB=1: the measurement build instead, CRC32C of all k+m cells by the
 default register-staged kernel, the same with non-temporal sum stores (tune
 key 30 = 1) and on the work queue (key 29 = 4 tasks per unit), compute and
 verify mode, same buffers,
-rounds alternated; PROBE_CRC_DMA=1 adds the LDS-DMA kernel (key 11 = 13;
-profiles/r05n ran it with the DMA kernel as the default and the register one
-on the key: the same kernels); PROBE_CRC_768=1 (round 6) the default kernel
+rounds alternated (round 5 also ran the LDS-DMA kernel here, key 11 = 13,
+removed in round 6: profiles/r05n); PROBE_CRC_768=1 (round 6) the default kernel
 against one 768-thread block per CU (key 33) and the memory side alone (key
 11 = 9, WRONG sums), compute and verify mode.
   python3 scripts/probe_layout.py
@@ -127,8 +126,6 @@ def main():
                 # the memory side first: its WRONG sums are rewritten before the verify legs
                 kernels[(lay, i)] = {"crc_mem": tuned(crc, 9), "crc_reg": crc, "crc_768": tuned(crc, 768, 33),
                                      "verify_reg": ver, "verify_768": tuned(ver, 768, 33)}
-            if os.environ.get("PROBE_CRC_DMA") == "1":
-                kernels[(lay, i)].update({"crc_dma": tuned(crc, 13), "verify_dma": tuned(ver, 13)})
             continue
         kernels[(lay, i)] = {"crc_only": crc, "encode": enc, "encode_crc": enc_crc, "decode_verify": dec_ver}
     times = {key: {n: [] for n in fns} for key, fns in kernels.items()}

@@ -69,6 +69,14 @@ if os.environ.get("PROBE_BSL") == "1":
     CONFIGS = [(10, 4, 256), (10, 4, 1024), (6, 3, 1024)]
     VARIANTS = [("v_perm queue", [(27, 0)]), ("v_perm fixed", [(27, 3)]), ("bsl fixed", [(23, 1)])]
 
+# PROBE_K10OCC=1 (round 6): RS(10,4) register kernel (76 VGPRs) on the queue
+# at more resident waves: 512-thread blocks at 2 / 3 per CU (4 / 6 waves per
+# SIMD) and 256-thread blocks at 4 / 6 per CU, against the default 1 x 512
+if os.environ.get("PROBE_K10OCC") == "1":
+    CONFIGS = [(10, 4, 256), (10, 4, 1024)]
+    VARIANTS = [("512 x1/CU", [(27, 0)]), ("512 x2/CU", [(3, 2)]), ("512 x3/CU", [(3, 3)]),
+                ("256 x4/CU", [(4, 256), (1, 2), (3, 4)]), ("256 x6/CU", [(4, 256), (1, 2), (3, 6)])]
+
 
 def main():
     dev = torch.device("cuda:0")
