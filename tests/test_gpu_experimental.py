@@ -85,13 +85,25 @@ def test_pair_kernel_vs_oracle(xlib, dev, c_oracle, k, m, cell, bpc, S):
     run_variant(xlib, c_oracle, dev, k, m, S, cell, knobs, cell + 7 * S + bpc)
 
 
+def _oracle_sums(cells, bpc, ctype=H.CHECKSUM_CRC32C):
+    S, n, cell = cells.shape
+    nch = (cell + bpc - 1) // bpc
+    out = np.empty((S, n, nch, 4), dtype=np.uint8)
+    for s in range(S):
+        for i in range(n):
+            out[s, i] = np.frombuffer(O.chunk_checksums(cells[s, i].tobytes(), bpc, ctype),
+                                      dtype=np.uint8).reshape(nch, 4)
+    return out
+
+
+
+
 @pytest.mark.parametrize("ctype", [H.CHECKSUM_CRC32C, H.CHECKSUM_CRC32])
 @pytest.mark.parametrize("cell,bpc,n", [(512 * 64, 512, 3), (512 * 70 + 256, 512, 2), (1000, 512, 3)])
 @pytest.mark.parametrize("variant,pf", [(2, 2), (3, 1), (3, 2), (4, 0), (6, 1), (6, 2)])
 def test_crc_schemes_vs_oracle(xlib, dev, ctype, cell, bpc, n, variant, pf):
     """Bank-replicated slicing-by-1 (4 / 8 chains), slicing-by-8 at 4 waves
-    per SIMD and bank-replicated slicing-by-2 (tune key 11 = 2, 3, 4, 6), and
-    the LDS-DMA fold kernel (key 11 = 13, CRC32C; CRC32 takes the default)."""
+    per SIMD and bank-replicated slicing-by-2 (tune key 11 = 2, 3, 4, 6)."""
     cells = batch_data(3, n, cell, first=cell + bpc + ctype + variant)
     H.tune_set(11, variant, xlib)
     H.tune_set(12, pf, xlib)
