@@ -23,7 +23,9 @@
  *    internal lock (one coder may be shared by threads; use one coder per
  *    thread for concurrency).  The device calls are asynchronous: they only
  *    enqueue work on the caller's HIP stream (`hip_stream` is a hipStream_t
- *    passed as void*; NULL = the null stream) and are lock-free.
+ *    passed as void*; NULL = the null stream).  Their only lock is the
+ *    stream's work-queue counter-set lock, held from choosing the launch's
+ *    counter set to enqueuing its kernel (see hec_queue_stats).
  */
 #ifndef HDFS_EC_AMD_H
 #define HDFS_EC_AMD_H
