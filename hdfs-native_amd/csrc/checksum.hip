@@ -86,21 +86,6 @@ __device__ __forceinline__ void emit_sum(const CrcArgs& a, uint64_t cell_idx, ui
     }
 }
 
-// Compute mode with the store issued by every lane (SUMS = 1 below): lanes
-// of a live chunk store its sum (the 4 lanes of a chunk hold the same value
-// after the combine), lanes of a chunk past the cell's end store chunk 0's
-// sum at chunk 0's slot again -- duplicate writes of one value, so the store
-// instruction is issued by the whole wave on every task, with no branch.
-__device__ __forceinline__ void store_sum(const CrcArgs& a, uint64_t cell_idx, uint64_t chunk, uint32_t crc) {
-    uint64_t cell = cell_idx;
-    if (a.mapped) {
-        const uint64_t s = cell_idx / a.n_shards;
-        const uint64_t stripe = a.stripe_list ? a.stripe_list[s] : s;
-        cell = stripe * a.n_total + a.sid[cell_idx - s * a.n_shards];
-    }
-    reinterpret_cast<uint32_t*>(a.out)[cell * a.chunks_per_cell + chunk] = bswap32(crc);
-}
-
 // One wave's task: 16 chunks (8 KiB) of one cell, 8 coalesced 1-KiB loads.
 // `task` is wave-uniform (scalar base/stride loads); the loads are
 // unconditional with dead lanes clamped to the cell start -- a conditional
@@ -135,15 +120,7 @@ struct CrcShape : crcdev::TableLayout<SCHEME> {
 // scheme's; 768 = one block per CU with the tables staged once for 12 waves
 // (3 per SIMD, 149.5 KiB of LDS), 50 % more tasks in flight than two
 // 256-thread blocks.
-// SUMS = 1 (compute mode; the default since round 6): the sums store is
-// issued by the whole wave on every task (store_sum).  With the store behind
-// a lane condition (SUMS = 0: emit_sum, verify or compute by a.expected) the
-// compiler cannot know at the loop head whether the previous task's store
-// was issued, so it waits for the whole vector-memory queue -- that store
-// included -- before staging the last of the task's 8 loads (vmcnt(0)
-// instead of vmcnt(1)): every task waited out its predecessor's write
-// acknowledgement, which verify mode (no store) never does.
-template <int KIND, int SCHEME, int PF, int WQ = 0, int BLK = 0, int SUMS = 0>
+template <int KIND, int SCHEME, int PF, int WQ = 0, int BLK = 0>
 __global__ __launch_bounds__(BLK ? BLK : CrcShape<SCHEME>::kBlock) void checksum_chunks512(CrcArgs a) {
     static_assert(WQ == 0 || PF == 1, "the queue (and the runs, WQ < 0) run one task of prefetch");
     using Sh = CrcShape<SCHEME>;
@@ -204,13 +181,7 @@ __global__ __launch_bounds__(BLK ? BLK : CrcShape<SCHEME>::kBlock) void checksum
         }
         val ^= __shfl_xor(val, 1);
         val ^= __shfl_xor(val, 2);
-        if constexpr (SUMS == 1) {
-            const uint32_t sv = full ? (val ^ kfinal) : val;
-            const uint32_t sv0 = uint32_t(__builtin_amdgcn_readlane(int(sv), 0));  // chunk 0: always live
-            store_sum(a, cell_idx, live ? g * 16u + c : g * 16u, live ? sv : sv0);
-        } else {
-            if (live && qi == 0) emit_sum(a, cell_idx, g * 16u + c, full ? (val ^ kfinal) : val);
-        }
+        if (live && qi == 0) emit_sum(a, cell_idx, g * 16u + c, full ? (val ^ kfinal) : val);
         __builtin_amdgcn_wave_barrier();
         asm volatile("" ::: "memory");
     };
@@ -252,17 +223,6 @@ __global__ __launch_bounds__(BLK ? BLK : CrcShape<SCHEME>::kBlock) void checksum
     // is checksummed
     uint64_t task = uint64_t(blockIdx.x) * WAVES + wave;
     u32x4 va[8], vb[8];
-    if constexpr (SUMS == 1 && PF == 1) {
-        // the first task peeled: every entry to the loop body then follows a
-        // task whose sums store was issued after its successor's loads, so
-        // the staging waits count that store as the youngest operation
-        // (vmcnt(8) .. vmcnt(1)) instead of draining it
-        if (task >= tasks) return;
-        load_task(a, groups, task, lane, va);
-        run_task(task, va, task + step);
-        for (task += step; task < tasks; task += step) run_task(task, va, task + step);
-        return;
-    }
     if (task < tasks) load_task(a, groups, task, lane, va);
     if (PF == 2 && task + step < tasks) load_task(a, groups, task + step, lane, vb);
     while (task < tasks) {
@@ -425,13 +385,6 @@ int launch_checksum(const CrcArgs& in, int device, hipStream_t stream) {
         const uint64_t cap = tn.grid ? uint64_t(tn.grid) : uint64_t(cus) * per_cu;
         if (grid > cap) grid = cap;
         const void* fn = a.kind == crc::kCrc32c ? crc_pick<crc::kCrc32c>(scheme, pf) : crc_pick<crc::kCksum>(scheme, pf);
-        // compute mode at the default shapes: the sums store issued by the
-        // whole wave (SUMS = 1, round 6); measurement key 34 = 1 keeps the
-        // lane-conditional store of rounds 1-5
-        if (!a.expected && scheme == 12 && !a.sums_nt && tn.crc_sums_cond != 1 &&
-            pf == (a.kind == crc::kCrc32c ? 1 : 2))
-            fn = a.kind == crc::kCrc32c ? reinterpret_cast<const void*>(&checksum_chunks512<crc::kCrc32c, 12, 1, 0, 0, 1>)
-                                        : fn;  // CRC32 (PF = 2) keeps the conditional store
 #ifdef HEC_EXPERIMENTAL
         // tune key 33 = 768: the fold kernel (CRC32C, one task of prefetch) in
         // one 768-thread block per CU, 3 waves per SIMD

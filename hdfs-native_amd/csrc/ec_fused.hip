@@ -66,12 +66,6 @@ constexpr bool bsl_shape() {
     return bitslice::rs_net_available<K, R>() && K > 2;
 }
 
-// the shapes the store-policy A/B (tune key 34) is compiled for
-template <int K, int R>
-constexpr bool ust_ab() {
-    return kExperimental && bsl_shape<K, R>() && ((K == 3 && R == 2) || (K == 6 && R == 3) || (K == 10 && R == 4));
-}
-
 template <int K, int R, int SCHEME, bool PAIR>
 const void* encode_bsl(bool bsl) {
     constexpr int SL = fused_slabs(K, R);
@@ -93,12 +87,6 @@ const void* encode_wq_fn(int slabs = 0) {
         if (slabs == 4)
             return reinterpret_cast<const void*>(
                 &gf_fused_crc<K, R, 4, 12, crc::kCrc32c, false, 2, true, RsNet<K, R>, 1, true>);
-    // measurement: the rounds-1-5 lane-conditional sums / parity stores
-    // (tune key 34 = 1; UST in ec_fused_kernel.hpp)
-    if constexpr (ust_ab<K, R>())
-        if (slabs == SL && tune_snapshot().crc_sums_cond == 1)
-            return reinterpret_cast<const void*>(
-                &gf_fused_crc<K, R, SL, 12, crc::kCrc32c, false, 2, SL == 4, RsNet<K, R>, 1, true, false>);
 #endif
     (void)slabs;
     if constexpr (bsl_shape<K, R>() && (kExperimental || K != 6))
@@ -117,12 +105,6 @@ const void* encode_fn(int slabs, int scheme, int wpe, bool pair, bool bsl) {
     constexpr int SL = fused_slabs(K, R);
     return encode_bsl<K, R, 12, SL == 4>(bsl);
 #else
-    // the rounds-1-5 lane-conditional sums / parity stores (tune key 34 = 1)
-    if constexpr (ust_ab<K, R>())
-        if (bsl && scheme == 12 && wpe == 2 && slabs == fused_slabs(K, R) && (slabs == 8 || pair) &&
-            tune_snapshot().crc_sums_cond == 1)
-            return reinterpret_cast<const void*>(&gf_fused_crc<K, R, fused_slabs(K, R), 12, crc::kCrc32c, false, 2,
-                                                               fused_slabs(K, R) == 4, RsNet<K, R>, 1, false, false>);
     // bit-sliced parity at the default slab count (tune key 22 = 1: off)
     if (bsl && scheme == 12 && wpe != 3 && slabs == fused_slabs(K, R) && (slabs == 8 || pair))
         return encode_bsl<K, R, 12, fused_slabs(K, R) == 4>(true);

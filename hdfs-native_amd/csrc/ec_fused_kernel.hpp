@@ -86,15 +86,8 @@ __device__ __forceinline__ const uint32_t* fused_slice32() {
 // WQ: tiles are wave-tiles (SLABS KiB of one stripe's cells per wave) from
 // the work queue (gf_device.hpp WaveQueue, a.queue) instead of block tiles in
 // a fixed order.
-// UST (encode, the default since round 6): the chunk sums and parity stores
-// are issued by the whole wave every time -- lanes with nothing to store
-// repeat lane 0's store (same address, same value) -- so the compiler knows
-// at each wait for the next shard's loads that those stores are younger and
-// leaves them in flight (vmcnt(1..8)); behind a lane condition (UST = false,
-// rounds 1-5) it could not, and every CRC round drained the previous round's
-// sums store (vmcnt(0)) before the staging of the next shard.
 template <int K, int R, int SLABS, int SCHEME, int KIND, bool VERIFY, int WPE = 2, bool PAIR = false,
-          class NET = PermNet, int PFD = 1, bool WQ = false, bool UST = true>
+          class NET = PermNet, int PFD = 1, bool WQ = false>
 __global__ __launch_bounds__(crcdev::sliced(SCHEME) ? 128 * WPE * (WPE - 1) : 512)
     __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void gf_fused_crc(
     MatmulArgs a, FusedCrcArgs cs) {
@@ -193,7 +186,6 @@ __global__ __launch_bounds__(crcdev::sliced(SCHEME) ? 128 * WPE * (WPE - 1) : 51
             live[u] = o < left32;
             voff[u] = live[u] ? o : 0u;
         }
-        const bool tile_whole = left32 >= WAVE_BYTES;  // wave-uniform: every slab of every lane inside the cell
         const uint64_t cbyte = wbyte + uint64_t(pslab) * 1024u + uint64_t(half) * 512u;
         const bool in_cell = cbyte < cell_len;
         const bool full = in_cell && cell_len - cbyte >= 512u;  // same for a chunk's 4 lanes
@@ -238,20 +230,7 @@ __global__ __launch_bounds__(crcdev::sliced(SCHEME) ? 128 * WPE * (WPE - 1) : 51
             }
             val ^= __shfl_xor(val, 1);
             val ^= __shfl_xor(val, 2);
-            if constexpr (!VERIFY && UST) {
-                // every lane stores: a live chunk's 4 lanes its sum, the
-                // others lane 0's (chunk 0 of this round's first shard, which
-                // always exists)
-                const uint32_t be = __builtin_bswap32(full ? (val ^ kfinal) : val);
-                const uint32_t be0 = uint32_t(__builtin_amdgcn_readlane(int(be), 0));
-                const uint64_t at0 = (uint64_t(stripe) * (K + R) + first) * nck + wbyte / 512;
-                const uint64_t at = live_c ? sum_cell(first) * nck + cbyte / 512 : at0;
-                const uint32_t v = live_c ? be : be0;
-                if (cs.sums_nt)
-                    __builtin_nontemporal_store(v, out_sums + at);
-                else
-                    out_sums[at] = v;
-            } else if (live_c && qi == 0) {
+            if (live_c && qi == 0) {
                 const uint32_t be = __builtin_bswap32(full ? (val ^ kfinal) : val);
                 if constexpr (VERIFY) {
                     if (be != want) cs.bad[sum_cell(first)] = 1;
@@ -388,28 +367,10 @@ __global__ __launch_bounds__(crcdev::sliced(SCHEME) ? 128 * WPE * (WPE - 1) : 51
 #pragma unroll
                     for (int u = 0; u < SLABS; u++) o[u] = acc[u][j];
                 }
-                if constexpr (!VERIFY && UST) {
-                    uint8_t* const ob = a.out[j] + (uint64_t(stripe) * a.out_stride[j] + wbyte);
-                    if (tile_whole) {
 #pragma unroll
-                        for (int u = 0; u < SLABS; u++) store16<true>(ob + voff[u], o[u]);
-                    } else {
-                        // a short last tile: lanes past the cell repeat lane 0's slab 0
-                        const u32x4 o0 = u32x4{uint32_t(__builtin_amdgcn_readlane(int(o[0][0]), 0)),
-                                               uint32_t(__builtin_amdgcn_readlane(int(o[0][1]), 0)),
-                                               uint32_t(__builtin_amdgcn_readlane(int(o[0][2]), 0)),
-                                               uint32_t(__builtin_amdgcn_readlane(int(o[0][3]), 0))};
-#pragma unroll
-                        for (int u = 0; u < SLABS; u++) store16<true>(ob + voff[u], live[u] ? o[u] : o0);
-                    }
-#pragma unroll
-                    for (int u = 0; u < SLABS; u++) stage_piece((K + j) % SPR, u, o[u]);
-                } else {
-#pragma unroll
-                    for (int u = 0; u < SLABS; u++) {
-                        if (live[u]) store16<true>(a.out[j] + (uint64_t(stripe) * a.out_stride[j] + wbyte) + voff[u], o[u]);
-                        if constexpr (!VERIFY) stage_piece((K + j) % SPR, u, o[u]);
-                    }
+                for (int u = 0; u < SLABS; u++) {
+                    if (live[u]) store16<true>(a.out[j] + (uint64_t(stripe) * a.out_stride[j] + wbyte) + voff[u], o[u]);
+                    if constexpr (!VERIFY) stage_piece((K + j) % SPR, u, o[u]);
                 }
                 if constexpr (!VERIFY) after_stage(K + j);
             }
@@ -641,7 +602,24 @@ __global__ __launch_bounds__(crcdev::sliced(SCHEME) ? 128 * WPE * (WPE - 1) : 51
                 }
             }
         }
-        if constexpr (!EARLY_OUT) emit_outputs();
+        if constexpr (!EARLY_OUT) {
+#pragma unroll
+            for (int j = 0; j < R; j++) {
+                u32x4 o[SLABS];
+                if constexpr (BSL) {
+                    bsl_output(j, o);
+                } else {
+#pragma unroll
+                    for (int u = 0; u < SLABS; u++) o[u] = acc[u][j];
+                }
+#pragma unroll
+                for (int u = 0; u < SLABS; u++) {
+                    if (live[u]) store16<true>(a.out[j] + (uint64_t(stripe) * a.out_stride[j] + wbyte) + voff[u], o[u]);
+                    if constexpr (!VERIFY) stage_piece((K + j) % SPR, u, o[u]);
+                }
+                if constexpr (!VERIFY) after_stage(K + j);
+            }
+        }
     }
 }
 

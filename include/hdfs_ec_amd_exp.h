@@ -86,9 +86,6 @@
  * key 33: 768 = the CRC32C checksum kernel (the fold, compute and verify) in
  *         one 768-thread block per CU: 3 waves per SIMD (0 = default: two
  *         256-thread blocks per CU)
- * key 34: 1 = the checksum kernel's compute mode with the lane-conditional
- *         sums store of rounds 1-5 (0 = default: the store issued by the
- *         whole wave, so the next task's staging waits only for its loads)
  * Returns HEC_OK, or HEC_ERR_INVALID_ARG for an unknown key / value.
  */
 #ifndef HDFS_EC_AMD_EXP_H

@@ -6,7 +6,7 @@ and the plan-specialised decode {0..m-1} + verify the same two ways (key 28
 form).  Same process, same buffers, rounds
 alternated, HIP events around REPS back-to-back launches (median), two fresh
 buffer sets per config; parity and sums checked equal.
-  python3 scripts/probe_fused_wq.py      (PROBE_ENC4 / PROBE_NT / PROBE_UST: below)
+  python3 scripts/probe_fused_wq.py
 """
 import os
 import statistics
@@ -36,11 +36,6 @@ if os.environ.get("PROBE_NT") == "1":
     ENC4 = True
     CONFIGS = [(6, 3, 1024)]
     VARIANTS = [("default", [(28, 0)]), ("sums nt", [(30, 1)]), ("queue sums nt", [(28, 1), (30, 1)])]
-# PROBE_UST=1 (round 6): encode + CRC only, the whole-wave sums / parity
-# stores (default) against the lane-conditional ones of rounds 1-5 (key 34 = 1)
-if os.environ.get("PROBE_UST") == "1":
-    ENC4 = True
-    VARIANTS = [("uniform stores", [(28, 0)]), ("conditional stores", [(34, 1)])]
 
 
 def main():

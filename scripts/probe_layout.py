@@ -16,9 +16,7 @@ verify mode, same buffers,
 rounds alternated (round 5 also ran the LDS-DMA kernel here, key 11 = 13,
 removed in round 6: profiles/r05n); PROBE_CRC_768=1 (round 6) the default kernel
 against one 768-thread block per CU (key 33) and the memory side alone (key
-11 = 9, WRONG sums), compute and verify mode; PROBE_CRC_SUMS=1 (round 6) the
-compute mode's whole-wave sums store (default) against the lane-conditional
-one of rounds 1-5 (key 34 = 1).
+11 = 9, WRONG sums), compute and verify mode.
   python3 scripts/probe_layout.py
 """
 import os
@@ -124,9 +122,6 @@ def main():
 
             kernels[(lay, i)] = {"crc_reg": crc, "crc_runs4": tuned(crc, 4, 31), "crc_runs8": tuned(crc, 8, 31),
                                  "crc_runs16": tuned(crc, 16, 31), "verify_reg": ver, "verify_runs8": tuned(ver, 8, 31)}
-            if os.environ.get("PROBE_CRC_SUMS") == "1":  # round 6: whole-wave sums store vs the conditional one (key 34)
-                kernels[(lay, i)] = {"crc_mem": tuned(crc, 9), "crc_reg": crc, "crc_cond": tuned(crc, 1, 34),
-                                     "verify_reg": ver}
             if os.environ.get("PROBE_CRC_768") == "1":  # round 6: 3 waves per SIMD (key 33), the skeleton (key 11 = 9)
                 # the memory side first: its WRONG sums are rewritten before the verify legs
                 kernels[(lay, i)] = {"crc_mem": tuned(crc, 9), "crc_reg": crc, "crc_768": tuned(crc, 768, 33),
@@ -150,7 +145,7 @@ def main():
     algo = {"crc_only": (K + M) * CELL * S + 4 * NCH * (K + M) * S, "encode": (K + M) * CELL * S,
             "encode_crc": (K + M) * CELL * S + 4 * NCH * (K + M) * S,
             "decode_verify": (K + len(MISS)) * CELL * S + 4 * NCH * K * S}
-    for n in ("crc_dma", "crc_reg", "verify_dma", "verify_reg", "crc_wq1", "crc_wq2", "crc_wq4", "verify_wq2", "crc_nt", "crc_wq8", "crc_wq16", "verify_wq8", "crc_runs2", "crc_runs4", "verify_runs2", "crc_runs8", "crc_runs16", "verify_runs8", "crc_768", "verify_768", "crc_mem", "crc_cond"):
+    for n in ("crc_dma", "crc_reg", "verify_dma", "verify_reg", "crc_wq1", "crc_wq2", "crc_wq4", "verify_wq2", "crc_nt", "crc_wq8", "crc_wq16", "verify_wq8", "crc_runs2", "crc_runs4", "verify_runs2", "crc_runs8", "crc_runs16", "verify_runs8", "crc_768", "verify_768", "crc_mem"):
         algo[n] = algo["crc_only"]
     for key, per in times.items():
         parts = []

@@ -413,7 +413,7 @@ def test_tune_set_concurrent_with_launches(xlib, dev, c_oracle):
 
 
 def test_tune_set_rejects_unknown_values(xlib):
-    for key, value in [(3, 99), (1, 5), (5, 6), (11, 8), (11, 13), (16, 1), (17, 6), (19, 3), (20, 3), (21, 2), (5, 3), (13, 1), (15, 2), (22, 2), (23, 2), (24, 6), (25, 4097), (26, 5), (27, 4), (28, 3), (29, 3), (30, 2), (31, 3), (32, 2), (33, 512), (34, 2), (35, 0), (0, 0)]:
+    for key, value in [(3, 99), (1, 5), (5, 6), (11, 8), (11, 13), (16, 1), (17, 6), (19, 3), (20, 3), (21, 2), (5, 3), (13, 1), (15, 2), (22, 2), (23, 2), (24, 6), (25, 4097), (26, 5), (27, 4), (28, 3), (29, 3), (30, 2), (31, 3), (32, 2), (33, 512), (34, 0), (0, 0)]:
         with pytest.raises(ValueError):
             H.tune_set(key, value, xlib)
 
