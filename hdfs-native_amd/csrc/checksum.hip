@@ -120,13 +120,7 @@ struct CrcShape : crcdev::TableLayout<SCHEME> {
 // scheme's; 768 = one block per CU with the tables staged once for 12 waves
 // (3 per SIMD, 149.5 KiB of LDS), 50 % more tasks in flight than two
 // 256-thread blocks.
-// BURST > 0 (compute mode, cells a multiple of BURST tasks; measurement, tune
-// key 34): fixed order in runs of BURST consecutive tasks of one cell per
-// wave; the run's BURST x 16 sums are gathered across the wave's lanes (lane l
-// holds sums 4l .. 4l + 3) and stored at the run's end, one 16-B store per
-// lane -- one contiguous write of 1 KiB (BURST = 16) per 128 KiB read instead
-// of a 64-B write per 8-KiB task.
-template <int KIND, int SCHEME, int PF, int WQ = 0, int BLK = 0, int BURST = 0>
+template <int KIND, int SCHEME, int PF, int WQ = 0, int BLK = 0>
 __global__ __launch_bounds__(BLK ? BLK : CrcShape<SCHEME>::kBlock) void checksum_chunks512(CrcArgs a) {
     static_assert(WQ == 0 || PF == 1, "the queue (and the runs, WQ < 0) run one task of prefetch");
     using Sh = CrcShape<SCHEME>;
@@ -148,9 +142,8 @@ __global__ __launch_bounds__(BLK ? BLK : CrcShape<SCHEME>::kBlock) void checksum
     const uint64_t tasks = groups * a.n_shards * a.stripes;
     const uint64_t step = uint64_t(gridDim.x) * WAVES;
 
-    // stage v (task's data), refill v with task `next`'s loads, checksum;
-    // -> the sum of chunk (lane / 4) of the task (BURST: stored by the caller)
-    auto run_task = [&](uint64_t task, u32x4 (&v)[8], uint64_t next) -> uint32_t {
+    // stage v (task's data), refill v with task `next`'s loads, checksum
+    auto run_task = [&](uint64_t task, u32x4 (&v)[8], uint64_t next) {
         const uint64_t cell_idx = task / groups;
         const uint64_t g = task - cell_idx * groups;
         const uint64_t start = g * 16u * CH;
@@ -188,58 +181,10 @@ __global__ __launch_bounds__(BLK ? BLK : CrcShape<SCHEME>::kBlock) void checksum
         }
         val ^= __shfl_xor(val, 1);
         val ^= __shfl_xor(val, 2);
-        const uint32_t sum = full ? (val ^ kfinal) : val;
-        if constexpr (BURST == 0)
-            if (live && qi == 0) emit_sum(a, cell_idx, g * 16u + c, sum);
+        if (live && qi == 0) emit_sum(a, cell_idx, g * 16u + c, full ? (val ^ kfinal) : val);
         __builtin_amdgcn_wave_barrier();
         asm volatile("" ::: "memory");
-        return sum;
     };
-
-    if constexpr (BURST > 0) {
-        static_assert(BURST == 8 || BURST == 16, "a run's sums fill 32 or 64 lanes x 16 B");
-        // the launcher guarantees every cell is a whole number of runs of
-        // full chunks (so no run crosses a cell and every chunk is live)
-        const uint64_t runs = tasks / BURST;
-        uint64_t run = uint64_t(blockIdx.x) * WAVES + wave;
-        u32x4 v[8];
-        if (run < runs) load_task(a, groups, run * BURST, lane, v);
-        while (run < runs) {
-            const uint64_t t0 = run * BURST;
-            const uint64_t nrun = run + step;
-            u32x4 acc = u32x4{0, 0, 0, 0};
-#pragma unroll 1
-            for (int t = 0; t < BURST; t++) {
-                const uint64_t next = t + 1 < BURST ? t0 + t + 1 : (nrun < runs ? nrun * BURST : tasks);
-                const uint32_t sum = run_task(t0 + t, v, next);
-                // lane l takes chunks 4 (l % 4) .. + 3 of task l / 4; chunk c's
-                // sum sits in lanes 4c .. 4c + 3
-                const bool mine = (lane >> 2) == t;
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    const uint32_t x = uint32_t(__shfl(int(sum), 16 * (lane & 3) + 4 * j));
-                    acc[j] = mine ? __builtin_bswap32(x) : acc[j];
-                }
-            }
-            const uint64_t cell_idx = t0 / groups;
-            uint64_t cell = cell_idx;
-            if (a.mapped) {
-                const uint64_t s = cell_idx / a.n_shards;
-                const uint64_t stripe = a.stripe_list ? a.stripe_list[s] : s;
-                cell = stripe * a.n_total + a.sid[cell_idx - s * a.n_shards];
-            }
-            u32x4* const dst = reinterpret_cast<u32x4*>(reinterpret_cast<uint32_t*>(a.out) + cell * a.chunks_per_cell +
-                                                        (t0 - cell_idx * groups) * 16u) + lane;
-            if (BURST == 16 || lane < 4 * BURST) {
-                if (a.sums_nt)
-                    __builtin_nontemporal_store(acc, dst);
-                else
-                    *dst = acc;
-            }
-            run = nrun;
-        }
-        return;
-    }
 
     if constexpr (WQ > 0) {
         // units of WQ tasks; the launcher keeps the unit count below 2^32
@@ -449,18 +394,6 @@ int launch_checksum(const CrcArgs& in, int device, hipStream_t stream) {
             grid = g < uint64_t(cus) ? g : uint64_t(cus);
             e = hipLaunchKernel(fn, dim3(uint32_t(grid)), dim3(768), args, 0, stream);
             return e == hipSuccess ? 0 : int(e);
-        }
-        // tune key 34: the fold kernel in runs of 8 / 16 tasks per wave, the
-        // run's sums stored at its end in one 16-B store per lane (compute
-        // mode; cells a whole number of runs; 16-B aligned sums)
-        if (tn.crc_burst && scheme == 12 && a.kind == crc::kCrc32c && pf == 1 && !a.expected && !tn.crc_runs &&
-            !tn.crc_wq && a.cell_len % (uint64_t(tn.crc_burst) * 16u * 512u) == 0 &&
-            (reinterpret_cast<uintptr_t>(a.out) & 15u) == 0) {
-            fn = tn.crc_burst == 8 ? reinterpret_cast<const void*>(&checksum_chunks512<crc::kCrc32c, 12, 1, 0, 0, 8>)
-                                   : reinterpret_cast<const void*>(&checksum_chunks512<crc::kCrc32c, 12, 1, 0, 0, 16>);
-            const uint64_t runs = tasks / uint64_t(tn.crc_burst);
-            const uint64_t g = (runs + waves - 1) / waves;
-            if (g < grid) grid = g;
         }
         // tune key 31: the fold kernel in runs of 2 / 4 consecutive tasks per wave
         if (tn.crc_runs && scheme == 12 && a.kind == crc::kCrc32c && pf == 1) {

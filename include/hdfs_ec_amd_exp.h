@@ -86,10 +86,6 @@
  * key 33: 768 = the CRC32C checksum kernel (the fold, compute and verify) in
  *         one 768-thread block per CU: 3 waves per SIMD (0 = default: two
  *         256-thread blocks per CU)
- * key 34: 8 / 16 = the CRC32C checksum kernel (the fold, compute mode) in
- *         runs of that many consecutive 8-KiB tasks of one cell per wave,
- *         the run's sums stored at its end in one 16-B store per lane; only
- *         where every cell is a whole number of runs (else the default)
  * Returns HEC_OK, or HEC_ERR_INVALID_ARG for an unknown key / value.
  */
 #ifndef HDFS_EC_AMD_EXP_H

@@ -14,9 +14,7 @@ default register-staged kernel, the same with non-temporal sum stores (tune
 key 30 = 1) and on the work queue (key 29 = 4 tasks per unit), compute and
 verify mode, same buffers,
 rounds alternated (round 5 also ran the LDS-DMA kernel here, key 11 = 13,
-removed in round 6: profiles/r05n); PROBE_CRC_BURST=1 (round 6) the default
-kernel against runs of 8 / 16 tasks per wave with the run's sums stored at its
-end (key 34) and runs of 16 storing per task (key 31); PROBE_CRC_768=1 (round 6) the default kernel
+removed in round 6: profiles/r05n); PROBE_CRC_768=1 (round 6) the default kernel
 against one 768-thread block per CU (key 33) and the memory side alone (key
 11 = 9, WRONG sums), compute and verify mode.
   python3 scripts/probe_layout.py
@@ -124,9 +122,6 @@ def main():
 
             kernels[(lay, i)] = {"crc_reg": crc, "crc_runs4": tuned(crc, 4, 31), "crc_runs8": tuned(crc, 8, 31),
                                  "crc_runs16": tuned(crc, 16, 31), "verify_reg": ver, "verify_runs8": tuned(ver, 8, 31)}
-            if os.environ.get("PROBE_CRC_BURST") == "1":  # round 6: sums stored per run of 8 / 16 tasks (key 34)
-                kernels[(lay, i)] = {"crc_reg": crc, "crc_burst8": tuned(crc, 8, 34), "crc_burst16": tuned(crc, 16, 34),
-                                     "crc_runs16": tuned(crc, 16, 31), "verify_reg": ver}
             if os.environ.get("PROBE_CRC_768") == "1":  # round 6: 3 waves per SIMD (key 33), the skeleton (key 11 = 9)
                 # the memory side first: its WRONG sums are rewritten before the verify legs
                 kernels[(lay, i)] = {"crc_mem": tuned(crc, 9), "crc_reg": crc, "crc_768": tuned(crc, 768, 33),
@@ -150,7 +145,7 @@ def main():
     algo = {"crc_only": (K + M) * CELL * S + 4 * NCH * (K + M) * S, "encode": (K + M) * CELL * S,
             "encode_crc": (K + M) * CELL * S + 4 * NCH * (K + M) * S,
             "decode_verify": (K + len(MISS)) * CELL * S + 4 * NCH * K * S}
-    for n in ("crc_dma", "crc_reg", "verify_dma", "verify_reg", "crc_wq1", "crc_wq2", "crc_wq4", "verify_wq2", "crc_nt", "crc_wq8", "crc_wq16", "verify_wq8", "crc_runs2", "crc_runs4", "verify_runs2", "crc_runs8", "crc_runs16", "verify_runs8", "crc_768", "verify_768", "crc_mem", "crc_burst8", "crc_burst16"):
+    for n in ("crc_dma", "crc_reg", "verify_dma", "verify_reg", "crc_wq1", "crc_wq2", "crc_wq4", "verify_wq2", "crc_nt", "crc_wq8", "crc_wq16", "verify_wq8", "crc_runs2", "crc_runs4", "verify_runs2", "crc_runs8", "crc_runs16", "verify_runs8", "crc_768", "verify_768", "crc_mem"):
         algo[n] = algo["crc_only"]
     for key, per in times.items():
         parts = []

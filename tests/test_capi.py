@@ -191,7 +191,7 @@ def test_tune_set_validates_without_device():
     xlib = H.experimental_lib()
     assert xlib.hec_tune_set(3, 2) == H.HEC_OK
     assert xlib.hec_tune_set(3, 0) == H.HEC_OK
-    for key, value in [(6, 3), (11, 13), (16, 1), (3, 99), (18, 2), (17, 6), (19, 3), (20, 3), (21, 2), (5, 3), (13, 1), (15, 2), (22, 2), (23, 2), (24, 6), (25, 4097), (26, 5), (27, 4), (28, 3), (29, 3), (30, 2), (31, 3), (32, 2), (33, 512), (34, 4), (35, 0), (0, 0)]:
+    for key, value in [(6, 3), (11, 13), (16, 1), (3, 99), (18, 2), (17, 6), (19, 3), (20, 3), (21, 2), (5, 3), (13, 1), (15, 2), (22, 2), (23, 2), (24, 6), (25, 4097), (26, 5), (27, 4), (28, 3), (29, 3), (30, 2), (31, 3), (32, 2), (33, 512), (34, 0), (0, 0)]:
         assert xlib.hec_tune_set(key, value) == H.HEC_ERR_INVALID_ARG, (key, value)
 
 

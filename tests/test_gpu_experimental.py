@@ -149,18 +149,9 @@ def test_crc_768_vs_oracle(xlib, dev, cell, bpc, n):
     P.crc32c_body(dev, cell, bpc, n, P.coder(6, 3, xlib), [(33, 768)], xlib)
 
 
-@pytest.mark.parametrize("burst,cell,n", [(8, 1 << 16, 9), (8, 1 << 17, 3), (16, 1 << 17, 3), (16, 1 << 18, 2),
-                                          (16, 1 << 16, 2)])
-def test_crc_burst_vs_oracle(xlib, dev, burst, cell, n):
-    """Tune key 34: the CRC32C fold kernel in runs of 8 / 16 tasks per wave,
-    each run's sums stored at its end (one 16-B store per lane), against the
-    oracle; 64 KiB cells at 16 are not a whole run and take the default."""
-    P.crc32c_body(dev, cell, 512, n, P.coder(6, 3, xlib), [(34, burst)], xlib)
-
-
-@pytest.mark.parametrize("knob", [(29, 1), (29, 4), (29, 16), (33, 768), (34, 8), (34, 16)])
+@pytest.mark.parametrize("knob", [(29, 1), (29, 4), (29, 16), (33, 768)])
 def test_crc_wq_full_size_compute_and_verify(xlib, dev, knob):
-    """Keys 29 / 33 / 34 at full size (9 x 1 MiB x 64 cells), three launches in a
+    """Keys 29 / 33 at full size (9 x 1 MiB x 64 cells), three launches in a
     row on one stream: sums equal the default kernel's, and verify mode flags
     exactly the corrupted cells."""
     S, n, cell = 64, 9, 1 << 20
@@ -422,7 +413,7 @@ def test_tune_set_concurrent_with_launches(xlib, dev, c_oracle):
 
 
 def test_tune_set_rejects_unknown_values(xlib):
-    for key, value in [(3, 99), (1, 5), (5, 6), (11, 8), (11, 13), (16, 1), (17, 6), (19, 3), (20, 3), (21, 2), (5, 3), (13, 1), (15, 2), (22, 2), (23, 2), (24, 6), (25, 4097), (26, 5), (27, 4), (28, 3), (29, 3), (30, 2), (31, 3), (32, 2), (33, 512), (34, 4), (35, 0), (0, 0)]:
+    for key, value in [(3, 99), (1, 5), (5, 6), (11, 8), (11, 13), (16, 1), (17, 6), (19, 3), (20, 3), (21, 2), (5, 3), (13, 1), (15, 2), (22, 2), (23, 2), (24, 6), (25, 4097), (26, 5), (27, 4), (28, 3), (29, 3), (30, 2), (31, 3), (32, 2), (33, 512), (34, 0), (0, 0)]:
         with pytest.raises(ValueError):
             H.tune_set(key, value, xlib)
 
