@@ -2027,13 +2027,20 @@ int numa_node_of(int device) {
 }  // namespace
 
 void hec_queue_stats(int device, uint64_t* streams, uint64_t* graph_sets, int* keyed_by_id) {
+    if (streams) *streams = 0;
+    if (graph_sets) *graph_sets = 0;
+    if (keyed_by_id) *keyed_by_id = 0;
     try {
+        int n = 0;
+        if (device < 0 || hipGetDeviceCount(&n) != hipSuccess || device >= n) {
+            (void)hipGetLastError();
+            return;  // no such device: zeros, and no per-device state created
+        }
         hec::queue_stats(device, streams, graph_sets);
         if (keyed_by_id) *keyed_by_id = hec::queue_keyed_by_id();
     } catch (...) {
         if (streams) *streams = 0;
         if (graph_sets) *graph_sets = 0;
-        if (keyed_by_id) *keyed_by_id = 0;
     }
 }
 

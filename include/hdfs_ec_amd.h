@@ -324,7 +324,8 @@ void hec_jit_stats(uint64_t *compiled, uint64_t *from_disk, uint64_t *failed, ui
  * (process totals; past 4096 streams / 256 graph launches per device the
  * kernels fall back to their fixed tile order), and *keyed_by_id = 1 when
  * streams are told apart by hipStreamGetId (HIP >= 7.1 in the process), 0
- * when by handle.  Any pointer may be NULL. */
+ * when by handle.  Any pointer may be NULL; all zeros for a device that
+ * does not exist. */
 void hec_queue_stats(int device, uint64_t *streams, uint64_t *graph_sets, int *keyed_by_id);
 
 /* Encode plus CRC32C of the k data and m parity cells (shard order

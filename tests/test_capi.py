@@ -371,3 +371,10 @@ def test_prepare_decode_args_without_device():
     c.close()
     st = H.jit_stats()
     assert set(st) == {"compiled", "from_disk", "failed", "launches"}
+
+
+def test_queue_stats_of_a_missing_device():
+    """hec_queue_stats reports zeros for a device that does not exist (and,
+    in this container, for every device: no GPU) without creating state."""
+    for d in (-1, 4096):
+        assert H.queue_stats(d) == {"streams": 0, "graph_sets": 0, "keyed_by_id": False}
