@@ -120,17 +120,7 @@ struct CrcShape : crcdev::TableLayout<SCHEME> {
 // scheme's; 768 = one block per CU with the tables staged once for 12 waves
 // (3 per SIMD, 149.5 KiB of LDS), 50 % more tasks in flight than two
 // 256-thread blocks.
-// ORD = 1 (measurement, tune key 34): the fixed order walks groups of
-// a.cell_group cells slab-major (task t of a group = slab t / G of cell t % G),
-// so the waves in flight write their sums across G cells' sums rather than
-// one contiguous run of them.
-// ORD = 2 (measurement, tune key 35): compute mode stores a task's sums one
-// task later, after the next task's loads are issued.  The sums store sits
-// behind a lane condition, so the staging wait at the next task's start
-// counts it as possibly outstanding (vmcnt(0)); stored at the end of its own
-// task it is waited for right after issue, deferred it has a whole task's
-// checksumming to complete first.
-template <int KIND, int SCHEME, int PF, int WQ = 0, int BLK = 0, int ORD = 0>
+template <int KIND, int SCHEME, int PF, int WQ = 0, int BLK = 0>
 __global__ __launch_bounds__(BLK ? BLK : CrcShape<SCHEME>::kBlock) void checksum_chunks512(CrcArgs a) {
     static_assert(WQ == 0 || PF == 1, "the queue (and the runs, WQ < 0) run one task of prefetch");
     using Sh = CrcShape<SCHEME>;
@@ -152,10 +142,6 @@ __global__ __launch_bounds__(BLK ? BLK : CrcShape<SCHEME>::kBlock) void checksum
     const uint64_t tasks = groups * a.n_shards * a.stripes;
     const uint64_t step = uint64_t(gridDim.x) * WAVES;
 
-    // ORD == 2: the previous task's sums, stored after this task's loads issue
-    bool pend = false;
-    uint64_t pend_cell = 0, pend_chunk = 0;
-    uint32_t pend_val = 0;
     // stage v (task's data), refill v with task `next`'s loads, checksum
     auto run_task = [&](uint64_t task, u32x4 (&v)[8], uint64_t next) {
         const uint64_t cell_idx = task / groups;
@@ -167,10 +153,6 @@ __global__ __launch_bounds__(BLK ? BLK : CrcShape<SCHEME>::kBlock) void checksum
             *reinterpret_cast<u32x4*>(stage + (off / Q) * PITCH + (off % Q)) = v[t];
         }
         if (next < tasks) load_task(a, groups, next, lane, v);
-        if constexpr (ORD == 2) {
-            if (pend) emit_sum(a, pend_cell, pend_chunk, pend_val);
-            pend = false;
-        }
         // lanes read what other lanes of the SAME wave wrote: a wave's LDS ops
         // complete in order; only the compiler must not hoist the reads
         __builtin_amdgcn_wave_barrier();
@@ -199,19 +181,7 @@ __global__ __launch_bounds__(BLK ? BLK : CrcShape<SCHEME>::kBlock) void checksum
         }
         val ^= __shfl_xor(val, 1);
         val ^= __shfl_xor(val, 2);
-        const bool emit = live && qi == 0;
-        if constexpr (ORD == 2) {
-            if (!a.expected) {
-                pend = emit;
-                pend_cell = cell_idx;
-                pend_chunk = g * 16u + c;
-                pend_val = full ? (val ^ kfinal) : val;
-            } else if (emit) {
-                emit_sum(a, cell_idx, g * 16u + c, full ? (val ^ kfinal) : val);
-            }
-        } else if (emit) {
-            emit_sum(a, cell_idx, g * 16u + c, full ? (val ^ kfinal) : val);
-        }
+        if (live && qi == 0) emit_sum(a, cell_idx, g * 16u + c, full ? (val ^ kfinal) : val);
         __builtin_amdgcn_wave_barrier();
         asm volatile("" ::: "memory");
     };
@@ -249,37 +219,20 @@ __global__ __launch_bounds__(BLK ? BLK : CrcShape<SCHEME>::kBlock) void checksum
         }
         return;
     }
-    // position t of the walk -> task (cell-major index); the identity unless ORD
-    auto at = [&](uint64_t t) -> uint64_t {
-        if constexpr (ORD != 1) {
-            return t;
-        } else {
-            if (t >= tasks) return t;
-            const uint64_t G = a.cell_group, span = G * groups;
-            const uint64_t blk = t / span, r = t - blk * span;
-            const uint64_t ncells = tasks / groups, rest = ncells - blk * G;
-            const uint64_t gb = rest < G ? rest : G;  // cells in this (possibly last) group
-            const uint64_t g = r / gb;
-            return (blk * G + (r - g * gb)) * groups + g;
-        }
-    };
     // PF register sets in flight: task t's loads are issued while task t-PF
     // is checksummed
     uint64_t task = uint64_t(blockIdx.x) * WAVES + wave;
     u32x4 va[8], vb[8];
-    if (task < tasks) load_task(a, groups, at(task), lane, va);
-    if (PF == 2 && task + step < tasks) load_task(a, groups, at(task + step), lane, vb);
+    if (task < tasks) load_task(a, groups, task, lane, va);
+    if (PF == 2 && task + step < tasks) load_task(a, groups, task + step, lane, vb);
     while (task < tasks) {
-        run_task(at(task), va, at(task + PF * step));
+        run_task(task, va, task + PF * step);
         task += step;
         if constexpr (PF == 2) {
             if (task >= tasks) break;
-            run_task(at(task), vb, at(task + 2 * step));
+            run_task(task, vb, task + 2 * step);
             task += step;
         }
-    }
-    if constexpr (ORD == 2) {
-        if (pend) emit_sum(a, pend_cell, pend_chunk, pend_val);
     }
 }
 
@@ -442,15 +395,6 @@ int launch_checksum(const CrcArgs& in, int device, hipStream_t stream) {
             e = hipLaunchKernel(fn, dim3(uint32_t(grid)), dim3(768), args, 0, stream);
             return e == hipSuccess ? 0 : int(e);
         }
-        // tune key 34: the fold kernel's fixed order over groups of G cells
-        if (tn.crc_group > 0 && scheme == 12 && a.kind == crc::kCrc32c && pf == 1 && !tn.crc_runs && !tn.crc_wq) {
-            a.cell_group = uint32_t(tn.crc_group);
-            fn = reinterpret_cast<const void*>(&checksum_chunks512<crc::kCrc32c, 12, 1, 0, 0, 1>);
-        }
-        // tune key 35: the fold kernel with each task's sums stored one task later
-        if (tn.crc_defer && scheme == 12 && a.kind == crc::kCrc32c && pf == 1 && !tn.crc_runs && !tn.crc_wq &&
-            !tn.crc_group)
-            fn = reinterpret_cast<const void*>(&checksum_chunks512<crc::kCrc32c, 12, 1, 0, 0, 2>);
         // tune key 31: the fold kernel in runs of 2 / 4 consecutive tasks per wave
         if (tn.crc_runs && scheme == 12 && a.kind == crc::kCrc32c && pf == 1) {
             const void* f = crc_pick<crc::kCrc32c>(12, -100 - tn.crc_runs);

@@ -41,7 +41,6 @@ struct CrcArgs {
     uint32_t* queue;           // work-queue variant: this launch's counters (zero when it starts)
     uint32_t* queue_zero;      // the set this launch zeroes for the stream's next launch (nullptr: none)
     uint32_t sums_nt;          // compute mode: non-temporal sum stores (measurement build, key 30)
-    uint32_t cell_group;       // fixed order over groups of this many cells, slab-major (measurement, key 34)
 };
 
 // 0 ok, -1 invalid sizes, >0 hipError_t.

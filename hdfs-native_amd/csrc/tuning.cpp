@@ -15,7 +15,7 @@ namespace {
 std::atomic<int> g_cus[64];
 
 #ifdef HEC_EXPERIMENTAL
-constexpr int kKeys = 35;
+constexpr int kKeys = 33;
 std::atomic<int> g_knob[kKeys + 1];  // index = key; zero-initialised (static storage)
 std::atomic<int> g_nt{-1};           // key 2 defaults to -1 (non-temporal on)
 
@@ -60,8 +60,6 @@ Tune tune_snapshot() {
     t.crc_runs = load(31);
     t.matmul_pair = load(32);
     t.crc_block = load(33);
-    t.crc_group = load(34);
-    t.crc_defer = load(35);
     return t;
 }
 
@@ -105,8 +103,6 @@ int tune_store(int key, int value) {
         case 31: ok = value == 0 || value == 2 || value == 4 || value == 8 || value == 16; break;
         case 32: ok = value == 0 || value == 1; break;
         case 33: ok = value == 0 || value == 768; break;
-        case 34: ok = value >= 0 && value <= 65536; break;
-        case 35: ok = value == 0 || value == 1; break;
         default: ok = false;
     }
     if (!ok) return HEC_ERR_INVALID_ARG;

@@ -55,8 +55,6 @@ struct Tune {
     int crc_runs = 0;           // key 31: CRC32C checksum kernel in runs of 2 / 4 consecutive tasks per wave (measurement)
     int matmul_pair = 0;        // key 32: 1 = the wave-pair register kernel for k = 10 (measurement)
     int crc_block = 0;          // key 33: CRC32C checksum kernel threads per block (0 = 256; 768 = 3 waves per SIMD)
-    int crc_defer = 0;          // key 35: 1 = the CRC32C checksum kernel stores each task's sums one task later (compute mode)
-    int crc_group = 0;          // key 34: CRC32C checksum kernel's task order over groups of G cells, slab-major (0 = cell-major)
     int mixed_wq = 0;           // key 26: mixed decode work queue of wave-tiles (0 = default: 1 round of wave-tiles per atomic for k >= 6, 4 below; 1 / 2 / 4 forced; 3 = the fixed tile order)
 };
 

@@ -86,12 +86,6 @@
  * key 33: 768 = the CRC32C checksum kernel (the fold, compute and verify) in
  *         one 768-thread block per CU: 3 waves per SIMD (0 = default: two
  *         256-thread blocks per CU)
- * key 34: G > 0 = the CRC32C checksum kernel (fixed order, compute and
- *         verify) takes its tasks over groups of G cells slab-major, so the
- *         waves in flight write sums spread over G cells' sums instead of
- *         one contiguous run (0 = default: cell-major)
- * key 35: 1 = the CRC32C checksum kernel (fixed order, compute mode) stores
- *         each task's sums one task later, after the next task's loads
  * Returns HEC_OK, or HEC_ERR_INVALID_ARG for an unknown key / value.
  */
 #ifndef HDFS_EC_AMD_EXP_H

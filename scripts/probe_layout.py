@@ -16,10 +16,7 @@ verify mode, same buffers,
 rounds alternated (round 5 also ran the LDS-DMA kernel here, key 11 = 13,
 removed in round 6: profiles/r05n); PROBE_CRC_768=1 (round 6) the default kernel
 against one 768-thread block per CU (key 33) and the memory side alone (key
-11 = 9, WRONG sums), compute and verify mode; PROBE_CRC_GRP=16,128,1024
-(round 6) the default order against the slab-major order over groups of G
-cells (key 34), with PROBE_CRC_DEFER=1 also the sums stored one task later
-(key 35).
+11 = 9, WRONG sums), compute and verify mode.
   python3 scripts/probe_layout.py
 """
 import os
@@ -129,13 +126,6 @@ def main():
                 # the memory side first: its WRONG sums are rewritten before the verify legs
                 kernels[(lay, i)] = {"crc_mem": tuned(crc, 9), "crc_reg": crc, "crc_768": tuned(crc, 768, 33),
                                      "verify_reg": ver, "verify_768": tuned(ver, 768, 33)}
-            if os.environ.get("PROBE_CRC_GRP"):  # round 6: slab-major order over groups of G cells (key 34)
-                kernels[(lay, i)] = {"crc_reg": crc, "verify_reg": ver}
-                for gv in os.environ["PROBE_CRC_GRP"].split(","):
-                    kernels[(lay, i)][f"crc_g{gv}"] = tuned(crc, int(gv), 34)
-                if os.environ.get("PROBE_CRC_DEFER") == "1":  # key 35: sums stored one task later
-                    kernels[(lay, i)]["crc_defer"] = tuned(crc, 1, 35)
-                kernels[(lay, i)]["verify_last"] = ver  # checks the last leg's sums
             continue
         kernels[(lay, i)] = {"crc_only": crc, "encode": enc, "encode_crc": enc_crc, "decode_verify": dec_ver}
     times = {key: {n: [] for n in fns} for key, fns in kernels.items()}
@@ -155,11 +145,9 @@ def main():
     algo = {"crc_only": (K + M) * CELL * S + 4 * NCH * (K + M) * S, "encode": (K + M) * CELL * S,
             "encode_crc": (K + M) * CELL * S + 4 * NCH * (K + M) * S,
             "decode_verify": (K + len(MISS)) * CELL * S + 4 * NCH * K * S}
-    for n in ("crc_dma", "crc_reg", "verify_dma", "verify_reg", "crc_wq1", "crc_wq2", "crc_wq4", "verify_wq2", "crc_nt", "crc_wq8", "crc_wq16", "verify_wq8", "crc_runs2", "crc_runs4", "verify_runs2", "crc_runs8", "crc_runs16", "verify_runs8", "crc_768", "verify_768", "crc_mem", "verify_last"):
+    for n in ("crc_dma", "crc_reg", "verify_dma", "verify_reg", "crc_wq1", "crc_wq2", "crc_wq4", "verify_wq2", "crc_nt", "crc_wq8", "crc_wq16", "verify_wq8", "crc_runs2", "crc_runs4", "verify_runs2", "crc_runs8", "crc_runs16", "verify_runs8", "crc_768", "verify_768", "crc_mem"):
         algo[n] = algo["crc_only"]
     for key, per in times.items():
-        for name in per:
-            algo.setdefault(name, algo["crc_only"])
         parts = []
         for name, ts in per.items():
             med = statistics.median(ts)
