@@ -16,7 +16,8 @@ verify mode, same buffers,
 rounds alternated (round 5 also ran the LDS-DMA kernel here, key 11 = 13,
 removed in round 6: profiles/r05n); PROBE_CRC_768=1 (round 6) the default kernel
 against one 768-thread block per CU (key 33) and the memory side alone (key
-11 = 9, WRONG sums), compute and verify mode.
+11 = 9, WRONG sums), compute and verify mode; PROBE_CRC_PF2=1 (round 6) the
+default against two tasks of register prefetch (key 12 = 2).
   python3 scripts/probe_layout.py
 """
 import os
@@ -126,6 +127,9 @@ def main():
                 # the memory side first: its WRONG sums are rewritten before the verify legs
                 kernels[(lay, i)] = {"crc_mem": tuned(crc, 9), "crc_reg": crc, "crc_768": tuned(crc, 768, 33),
                                      "verify_reg": ver, "verify_768": tuned(ver, 768, 33)}
+            if os.environ.get("PROBE_CRC_PF2") == "1":  # round 6: two tasks of prefetch (key 12 = 2)
+                kernels[(lay, i)] = {"crc_reg": crc, "crc_pf2": tuned(crc, 2, 12), "verify_reg": ver,
+                                     "verify_pf2": tuned(ver, 2, 12)}
             continue
         kernels[(lay, i)] = {"crc_only": crc, "encode": enc, "encode_crc": enc_crc, "decode_verify": dec_ver}
     times = {key: {n: [] for n in fns} for key, fns in kernels.items()}
@@ -145,7 +149,7 @@ def main():
     algo = {"crc_only": (K + M) * CELL * S + 4 * NCH * (K + M) * S, "encode": (K + M) * CELL * S,
             "encode_crc": (K + M) * CELL * S + 4 * NCH * (K + M) * S,
             "decode_verify": (K + len(MISS)) * CELL * S + 4 * NCH * K * S}
-    for n in ("crc_dma", "crc_reg", "verify_dma", "verify_reg", "crc_wq1", "crc_wq2", "crc_wq4", "verify_wq2", "crc_nt", "crc_wq8", "crc_wq16", "verify_wq8", "crc_runs2", "crc_runs4", "verify_runs2", "crc_runs8", "crc_runs16", "verify_runs8", "crc_768", "verify_768", "crc_mem"):
+    for n in ("crc_dma", "crc_reg", "verify_dma", "verify_reg", "crc_wq1", "crc_wq2", "crc_wq4", "verify_wq2", "crc_nt", "crc_wq8", "crc_wq16", "verify_wq8", "crc_runs2", "crc_runs4", "verify_runs2", "crc_runs8", "crc_runs16", "verify_runs8", "crc_768", "verify_768", "crc_mem", "crc_pf2", "verify_pf2"):
         algo[n] = algo["crc_only"]
     for key, per in times.items():
         parts = []
